@@ -1,0 +1,117 @@
+"""Extract golden vectors from the reference's recorded CLI session.
+
+Run once in the build container (where /root/reference exists):
+    python tests/golden/make_golden.py
+It reads /root/reference/phase3_output (the transcript of the reference Java
+engine run over minidata.txt) as TEXT and writes tests/golden/phase3_golden.json:
+
+  * "bitsets": the selection BitSets printed by `bmj` (BitMapQuery ->
+    ColumnarIndexScan.getOutputPositions), one per distinct CNF, with the
+    transcript line they come from;
+  * "full_constraint_counts": "Total Outer Tuples By Full Constraint: n"
+    printed by `nlj` for its outer CNF (rows of the outer file that satisfy
+    the whole CNF);
+  * "indexes_query": the rows (A, B, C, D) and the count printed by
+    `indexes_query` (MultiIndexQuery -> ColumnarIndexScan.get_next), in the
+    engine's position order.
+
+All queries run over minidata.txt (500 rows, A:char(25) B:char(25) C:int
+D:int), committed as tests/golden/minidata.tsv (a byte copy).  Nothing under
+/root/reference is read at test time.
+"""
+import json
+import os
+import re
+import sys
+
+REF = "/root/reference/phase3_output"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "phase3_golden.json")
+
+
+def split_cnf(s):
+    """'{(A,=,x)|(B,=,y)}^{(C,=,6)}' -> [[('A','=','x'), ...], ...]"""
+    s = s.strip()
+    conjs = []
+    for part in s.split("^"):
+        part = part.strip()
+        if not (part.startswith("{") and part.endswith("}")):
+            return None
+        terms = []
+        for t in part[1:-1].split("|"):
+            t = t.strip()
+            if not (t.startswith("(") and t.endswith(")")):
+                return None
+            f = [x.strip() for x in t[1:-1].split(",")]
+            if len(f) not in (3, 4):
+                return None
+            terms.append(f)
+        conjs.append(terms)
+    return conjs
+
+
+def main():
+    lines = open(REF, encoding="utf-8", errors="replace").read().split("\n")
+    bitsets, counts, iq = {}, {}, []
+    i = 0
+    while i < len(lines):
+        ln = lines[i]
+        if not ln.startswith("> "):
+            i += 1
+            continue
+        toks = ln[2:].split()
+        cmd = toks[0] if toks else ""
+        j = i + 1
+        while j < len(lines) and not lines[j].startswith("> "):
+            j += 1
+        body = lines[i + 1:j]
+        if cmd == "bmj" and len(toks) >= 6 and toks[1] == "db":
+            outer, inner = split_cnf(toks[4]), split_cnf(toks[5])
+            for k, b in enumerate(body):
+                for tag, cnf, raw in (("OuterConstraint", outer, toks[4]), ("InnerConstraint", inner, toks[5])):
+                    if b.startswith(tag + " Bitset") and cnf is not None and k + 1 < len(body):
+                        m = re.fullmatch(r"\{([0-9, ]*)\}", body[k + 1].strip())
+                        if m:
+                            pos = [int(x) for x in m.group(1).split(",") if x.strip()]
+                            bitsets.setdefault(raw, {"cnf": cnf, "positions": pos, "line": i + k + 3})
+        elif cmd == "nlj" and len(toks) >= 6 and toks[1] == "db":
+            outer = split_cnf(toks[4])
+            for k, b in enumerate(body):
+                m = re.match(r"Total Outer Tuples By Full Constraint: (\d+)", b)
+                if m and outer is not None:
+                    counts.setdefault(toks[4], {"cnf": outer, "count": int(m.group(1)), "line": i + k + 2})
+        elif cmd == "indexes_query":
+            # rows follow the "A, B, C, D" header until the blank line
+            hs = [k for k, b in enumerate(body) if b.strip() == "A, B, C, D"]
+            if not hs:
+                i = j
+                continue
+            h = hs[0]
+            rows = []
+            k = h + 1
+            while k < len(body) and body[k].strip():
+                a, b, c, d = [x.strip() for x in body[k].split(",")]
+                rows.append([a, b, int(c), int(d)])
+                k += 1
+            cnt = None
+            for b in body:
+                m = re.match(r"Total Results Count By Query: (\d+)", b)
+                if m:
+                    cnt = int(m.group(1))
+            cnf = split_cnf(toks[4])
+            if cnf is not None and cnt is not None:
+                iq.append({"cnf": cnf, "raw": toks[4], "rows": rows, "count": cnt, "line": i + 1})
+        i = j
+    out = {
+        "source": "reference phase3_output (Minibase-Columnar CLI transcript over minidata.txt)",
+        "schema": {"A": ["string", 25], "B": ["string", 25], "C": ["int", 4], "D": ["int", 4]},
+        "bitsets": list(bitsets.values()),
+        "full_constraint_counts": list(counts.values()),
+        "indexes_query": iq,
+    }
+    with open(OUT, "w") as f:
+        json.dump(out, f, indent=1)
+    print(f"wrote {OUT}: {len(bitsets)} bitsets, {len(counts)} counts, {len(iq)} indexes_query results")
+
+
+if __name__ == "__main__":
+    sys.exit(main())
