@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json headline: scanned rows/s + HBM GB/s on the C3
+workload (100M-row 4 x int32 Columnarfile, 2-predicate conjunction + COUNT).
+
+One "step" = one ColumnarFileScan COUNT pass over the resident table:
+`query ... {(c0 < 2^19)} ^ {(c1 >= 2^19)} FILESCAN` -> Total Results Count,
+executed as ONE kernel launch (k_scan_fast<2, COUNT>; its last block folds the
+per-block partials).  Inputs are resident in HBM before the timed region.
+
+Multi-GPU (weak scaling): each rank owns its own 100M-row
+shard (rows [rank*N, (rank+1)*N) of one logical table); per step the ranks'
+counts are combined by one RCCL all_reduce on a side stream that overlaps the
+next step's scan.  value = total rows scanned by all ranks / max-over-ranks time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "scanned rows/sec + HBM GB/s, 100M-row 4×int32 conjunctive filter, 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+THRESH = 1 << 19
+
+
+def cpu_baseline(rows, min_seconds):
+    """The oracle (C restatement of ColumnarFileScan + PredEval, one core)
+    timed on the same workload definition: a host copy of the C3 table
+    (numpy PCG64, seeds 42..45), full passes until min_seconds elapsed."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import helpers
+    import oracle
+
+    cols = [(oracle.INTEGER, 4, c) for c in helpers.synthetic_int_table(rows, 4, 1 << 20, 42)]
+    t = oracle.Table(cols)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", THRESH))], [(oracle.GE, ("sym", 2), ("int", THRESH))]]
+    passes, elapsed, count = 0, 0.0, None
+    while elapsed < min_seconds and passes < 50:
+        t0 = time.perf_counter()
+        count = oracle.filescan_count(t, cnf)
+        elapsed += time.perf_counter() - t0
+        passes += 1
+    return {
+        "value": rows * passes / elapsed,
+        "unit": "rows/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{passes} full pass(es) over a {rows:,}-row 4xint32 host table (same C3 predicate, "
+                  f"count {count}); oracle/oracle.c orc_filescan, single thread, {elapsed:.1f} s total",
+    }
+
+
+def load_traffic(rows):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (profiles/*_pmc.json, written by tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "c3_scan_pmc.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("rows") == rows:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--rows", type=int, default=100_000_000, help="rows per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    import mbx_pkg
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    m = mbx_pkg.load()
+    ctx = m.Context(local_rank)
+    n = args.rows
+
+    # synthetic C3 shard, generated in HBM: 4 x int32 uniform [0, 2^20)
+    cols = []
+    for j in range(4):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(42 + j + 1000 * rank)
+        cols.append(torch.randint(0, 1 << 20, (n,), dtype=torch.int32, device="cuda", generator=g))
+    torch.cuda.synchronize()
+    table = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [c.data_ptr() for c in cols], n, None, row_offset=rank * n)
+    cnf = [[(m.mbx.LT, ("sym", 1), ("int", THRESH))], [(m.mbx.GE, ("sym", 2), ("int", THRESH))]]
+    plan = ctx.compile(table, cnf)
+
+    # correctness gate before timing: the kernel's count vs a torch reduction
+    # of the same device columns (the oracle cross-check lives in tests/)
+    got = ctx.scan_count(plan)
+    want = int(((cols[0] < THRESH) & (cols[1] >= THRESH)).sum().item())
+    assert got == want, f"rank {rank}: scan count {got} != reference {want}"
+
+    steps, warmup = args.steps, args.warmup
+    counts = torch.zeros(steps + warmup, dtype=torch.int64, device="cuda")
+    ext = torch.cuda.ExternalStream(ctx.stream)
+    xs = torch.cuda.Stream() if world > 1 else None
+    base = counts.data_ptr()
+
+    def step(k):
+        ctx.scan_count_async(plan, base + 8 * k)
+        if world > 1:  # the one exchange step: combine COUNT over ranks
+            ev = torch.cuda.Event()
+            ev.record(ext)
+            xs.wait_event(ev)
+            with torch.cuda.stream(xs):
+                dist.all_reduce(counts[k:k + 1])
+
+    for k in range(warmup):
+        step(k)
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev_s[k].record(ext)
+        step(warmup + k)
+        ev_e[k].record(ext)
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+
+    kern_ms = sum(a.elapsed_time(b) for a, b in zip(ev_s, ev_e)) / steps
+    c = counts[warmup:].cpu()
+    if world > 1:
+        assert bool((c == c[0]).all()), "per-step global counts differ"
+    else:
+        assert bool((c == got).all()), "per-step counts differ"
+
+    t_max = wall
+    if world > 1:
+        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max, kern_ms = float(tt[0]), float(tt[1])
+
+    if rank == 0:
+        total_rows = n * world * steps
+        ms_per_step = t_max * 1e3 / steps
+        algo_bytes = 2 * 4 * n  # c0 + c1 read once per launch
+        achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": total_rows / t_max,
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic: 4 x int32 uniform [0, 2^20) per row, generated in HBM (torch Philox, seed 42+col+1000*rank)",
+            "config": {
+                "workload": "C3: 100M-row 4xint32 Columnarfile, {(c0 < 2^19)} ^ {(c1 >= 2^19)} + COUNT "
+                            "(ColumnarFileScan / PredEval), 1 kernel launch per step",
+                "rows_per_gpu": n,
+                "global_rows": n * world,
+                "parallelism": f"row-range shards x{world}" + (", RCCL all_reduce of COUNT per step" if world > 1
+                                                              else ""),
+            },
+            "hbm_gbs": algo_bytes * world / (t_max / steps) / 1e9,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "mbx::k_scan_fast<2, COUNT, no-deleted>",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": load_traffic(n),
+                "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_launch": algo_bytes,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+
+    table.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,246 @@
+/*
+ * mbx.h -- C-ABI of the MI355X columnar scan/filter/aggregate executor for
+ * the Minibase-Columnar engine (drop-in for the ColumnarFileScan /
+ * ColumnIndexScan / ColumnarIndexScan / BitMapFile hot path).
+ *
+ * Plain C: no C++ or HIP types cross this boundary.  Every entry point names
+ * the reference interface it replaces; R/ = minijava/src of
+ * Neehaarika/MiniBase-Columnar-Database.  INTEGRATION.md shows the JNI glue a
+ * Java maintainer would add on top (GpuColumnarFileScan etc.).
+ *
+ * Conventions
+ *   - Every function returns MBX_OK (0) or a negative MBX_E_* code; the
+ *     message of the last failure on the calling thread is mbx_last_error().
+ *     Codes map onto the reference's checked exceptions (see below).
+ *   - One mbx_ctx per GPU; a context owns one HIP stream and is used by one
+ *     thread at a time (the reference engine is single threaded,
+ *     R/global/SystemDefs.java:6-9).  Multi-GPU = one process (or one
+ *     context) per GPU, rows sharded by range.
+ *   - Synchronous calls return with their results on the host.  *_async calls
+ *     only enqueue on the context stream; mbx_sync() waits.
+ *   - Positions: a table holds rows [row_offset, row_offset + nrows) of a
+ *     Columnarfile in position order (position == row index of a dense file,
+ *     R/heap/Heapfile.java:262-289).  row_offset must be a multiple of 64 so
+ *     bitmap words never straddle shards.  Bitmaps are table-local
+ *     java.util.BitSet images (bit p%64 of uint64 word p/64, local p);
+ *     row ids returned to the host are global positions (row_offset + p).
+ */
+#ifndef MBX_H
+#define MBX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MBX_ABI_VERSION 1
+
+/* ---- status codes (reference exception each one stands for) ------------ */
+#define MBX_OK 0
+#define MBX_E_INVALID (-1)     /* bad argument: FileScanException / IndexException / InvalidRelation */
+#define MBX_E_TYPE (-2)        /* UnknowAttrType / PredEvalException (operand type mismatch) */
+#define MBX_E_RANGE (-3)       /* FieldNumberOutOfBoundException (FldSpec offset out of range) */
+#define MBX_E_DEVICE (-4)      /* HIP runtime failure */
+#define MBX_E_NOMEM (-5)       /* device or host allocation failed */
+#define MBX_E_UNSUPPORTED (-6) /* outside the GPU path's envelope (limits below) */
+
+/* ---- global.AttrType (R/global/AttrType.java:45-49) ----------------------- */
+#define MBX_ATTR_STRING 0
+#define MBX_ATTR_INTEGER 1
+#define MBX_ATTR_REAL 2
+#define MBX_ATTR_SYMBOL 3
+#define MBX_ATTR_NULL 4
+
+/* ---- global.AttrOperator (R/global/AttrOperator.java:98-106) -------------- */
+#define MBX_OP_EQ 0
+#define MBX_OP_LT 1
+#define MBX_OP_GT 2
+#define MBX_OP_NE 3
+#define MBX_OP_LE 4
+#define MBX_OP_GE 5
+#define MBX_OP_NOT 6
+#define MBX_OP_NOP 7
+#define MBX_OP_RANGE 8
+
+/* ---- global.IndexType (R/global/IndexType.java:10-13) --------------------- */
+#define MBX_INDEX_NONE 0
+#define MBX_INDEX_BTREE 1
+#define MBX_INDEX_HASH 2
+#define MBX_INDEX_BITMAP 3
+
+/* ---- bitmap combine ops (java.util.BitSet and / or / andNot) ------------- */
+#define MBX_BM_AND 0
+#define MBX_BM_OR 1
+#define MBX_BM_ANDNOT 2
+
+/* ---- limits of one compiled predicate (checked, MBX_E_UNSUPPORTED) ------ */
+#define MBX_MAX_TERMS 32        /* CondExprs in one CNF */
+#define MBX_MAX_CONJ 32         /* conjuncts */
+#define MBX_MAX_PRED_COLS 8     /* distinct columns a CNF (+ aggregate) touches */
+#define MBX_MAX_STR_BYTES 256   /* char(n) size and string literal bytes */
+
+typedef struct mbx_ctx mbx_ctx;
+typedef struct mbx_table mbx_table;
+typedef struct mbx_plan mbx_plan;
+typedef struct mbx_bitmap mbx_bitmap;
+typedef struct mbx_cursor mbx_cursor;
+
+/* One column of a Columnarfile (Columnarfile.getAttributeTypes /
+ * getStringSizes, R/columnar/Columnarfile.java:239-359). */
+typedef struct {
+  int32_t attr_type; /* MBX_ATTR_INTEGER / _REAL / _STRING */
+  int32_t size;      /* char(n): n payload bytes; ignored (4) for int/real */
+} mbx_col_desc;
+
+/* iterator.Operand + CondExpr.typeN (R/iterator/Operand.java, CondExpr.java:12-57). */
+typedef struct {
+  int32_t type;        /* MBX_ATTR_SYMBOL: column reference; else the literal's AttrType */
+  int32_t fld;         /* FldSpec.offset, 1-based (RelSpec.outer) when type == SYMBOL */
+  int32_t integer;     /* Operand.integer */
+  float real;          /* Operand.real */
+  const char *string;  /* Operand.string as modified UTF-8 (JNI GetStringUTFChars), not NUL-terminated */
+  int32_t string_len;  /* bytes */
+} mbx_operand;
+
+/* iterator.CondExpr: `operand1 op operand2` (R/iterator/CondExpr.java:12-57). */
+typedef struct {
+  int32_t op;          /* MBX_OP_* */
+  mbx_operand operand1;
+  mbx_operand operand2;
+  int32_t index_type;  /* CondExpr.indexType (only ColumnarIndexScan reads it) */
+} mbx_condexpr;
+
+/* CondExpr[] in CNF, flattened: conjunct c is the OR-list
+ * conds[conj_offsets[c] .. conj_offsets[c+1]) (the .next chain), conjuncts
+ * are AND-ed (the null-terminated array).  nconj == 0 is `p == null` (true),
+ * R/iterator/PredEval.java:46-49. */
+typedef struct {
+  const mbx_condexpr *conds;
+  const int32_t *conj_offsets; /* nconj + 1 entries */
+  int32_t nconj;
+} mbx_cnf;
+
+/* COUNT / SUM / MIN / MAX of one column over the selected rows (no
+ * reference equivalent; COUNT == Query's resultCount, R/input/Query.java:147). */
+typedef struct {
+  int64_t count;
+  int32_t agg_type;   /* AttrType of the aggregated column */
+  int32_t pad_;
+  int64_t isum;       /* attrInteger: exact */
+  int32_t imin, imax; /* attrInteger (INT32_MAX / INT32_MIN when count == 0) */
+  double fsum;        /* attrReal: double accumulation, deterministic order */
+  float fmin, fmax;   /* attrReal (+inf / -inf when count == 0) */
+} mbx_agg;
+
+/* ---- library ------------------------------------------------------------- */
+int mbx_abi_version(void);
+const char *mbx_last_error(void);
+int mbx_device_count(int32_t *n);
+
+/* ---- context: SystemDefs (R/global/SystemDefs.java:19-95) minus the disk;
+ * one HIP stream on `device` -------------------------------------------- */
+int mbx_init(int32_t device, mbx_ctx **out);
+int mbx_free(mbx_ctx *ctx);
+int mbx_sync(mbx_ctx *ctx);
+/* the hipStream_t every launch of this context goes to (for event timing) */
+void *mbx_stream(mbx_ctx *ctx);
+
+/* ---- tables: the HBM image of a Columnarfile ------------------------------
+ * Replaces opening one heap.Scan per column (TupleScan, R/columnar/TupleScan.java:29-47)
+ * and reading `cf.md` (Columnarfile.getMarkedDeleted): columns are staged once
+ * as contiguous chunks.  host_cols[j]: nrows values in position order --
+ * int32 / float32 host order, or `size` bytes of zero-padded modified UTF-8
+ * per row for char(n).  deleted_words: the markedDeleted BitSet image
+ * (ceil(nrows/64) words) or NULL.  The library copies; the caller keeps
+ * ownership of its buffers. */
+int mbx_table_stage(mbx_ctx *ctx, const mbx_col_desc *cols, int32_t ncols, int64_t nrows,
+                    const void *const *host_cols, const uint64_t *deleted_words,
+                    int64_t row_offset, mbx_table **out);
+/* Same, over device buffers the caller already holds in the table's device
+ * layout (int32/float32 arrays; strings padded to a multiple of 4 bytes per
+ * row in the device string encoding).  No copy; buffers must
+ * outlive the table. */
+int mbx_table_wrap(mbx_ctx *ctx, const mbx_col_desc *cols, int32_t ncols, int64_t nrows,
+                   const void *const *dev_cols, const uint64_t *dev_deleted_words,
+                   int64_t row_offset, mbx_table **out);
+int mbx_table_free(mbx_table *t);
+int mbx_table_info(const mbx_table *t, int64_t *nrows, int64_t *row_offset, int32_t *ncols);
+
+/* ---- predicates: PredEval.Eval over one tuple (R/iterator/PredEval.java:25-183),
+ * compiled once for one table.  Type rules follow the reference: the
+ * comparison type is operand1's, both operands must carry it (else
+ * MBX_E_TYPE); FldSpec offsets are checked (MBX_E_RANGE). ----------------- */
+int mbx_plan_compile(mbx_ctx *ctx, const mbx_table *t, const mbx_cnf *cnf, mbx_plan **out);
+int mbx_plan_free(mbx_plan *p);
+
+/* ---- ColumnarFileScan (R/iterator/ColumnarFileScan.java:156-188) --------- */
+/* COUNT of get_next() results: Query.executeFileScan's resultCount. */
+int mbx_scan_count(mbx_ctx *ctx, const mbx_plan *p, int64_t *count);
+/* enqueue only; *dev_count (device memory) receives the count */
+int mbx_scan_count_async(mbx_ctx *ctx, const mbx_plan *p, int64_t *dev_count);
+/* the selection as a device BitSet (the get_next_tid() stream as positions) */
+int mbx_scan_bitmap(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap **out, int64_t *count);
+int mbx_scan_bitmap_async(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap *out);
+/* COUNT/SUM/MIN/MAX of column `agg_col` (0-based) over the selection */
+int mbx_scan_aggregate(mbx_ctx *ctx, const mbx_plan *p, int32_t agg_col, mbx_agg *out);
+int mbx_scan_aggregate_async(mbx_ctx *ctx, const mbx_plan *p, int32_t agg_col, mbx_agg *dev_out);
+
+/* ---- device BitSets (BitMapFile.getBitSet / java.util.BitSet, R/bitmap/BitMapFile.java:478,
+ * R/bitmap/BM.java:179-215: bit p%64 of word p/64) ------------------------ */
+int mbx_bitmap_alloc(mbx_ctx *ctx, int64_t nbits, mbx_bitmap **out);
+int mbx_bitmap_upload(mbx_ctx *ctx, int64_t nbits, const uint64_t *host_words, mbx_bitmap **out);
+int mbx_bitmap_download(mbx_ctx *ctx, const mbx_bitmap *b, uint64_t *host_words, int64_t nwords);
+int mbx_bitmap_info(const mbx_bitmap *b, int64_t *nbits, int64_t *nwords, int64_t *count);
+int mbx_bitmap_free(mbx_bitmap *b);
+/* BitSet.and / or / andNot into a new bitmap (+ cardinality) */
+int mbx_bitmap_combine(mbx_ctx *ctx, int32_t op, const mbx_bitmap *a, const mbx_bitmap *b,
+                       mbx_bitmap **out, int64_t *count);
+/* ColumnarIndexScan's CNF over index BitSets (R/index/ColumnarIndexScan.java:130-181) and
+ * ColumnIndexScan.getBitSet's value-set OR (R/index/ColumnIndexScan.java:656-740):
+ * result = AND_c ( OR_{k in conj c} bms[k] ) AND NOT deleted, in one pass.
+ * conj_offsets has nconj + 1 entries; an empty conjunct is all-zero.
+ * deleted may be NULL. */
+int mbx_bitmap_cnf(mbx_ctx *ctx, int64_t nbits, const mbx_bitmap *const *bms,
+                   const int32_t *conj_offsets, int32_t nconj, const mbx_bitmap *deleted,
+                   mbx_bitmap **out, int64_t *count);
+int mbx_bitmap_cnf_async(mbx_ctx *ctx, const mbx_bitmap *const *bms, const int32_t *conj_offsets,
+                         int32_t nconj, const mbx_bitmap *deleted, mbx_bitmap *out);
+/* Columnarfile.createBitMapIndex (R/columnar/Columnarfile.java:698-753): one
+ * BitMapFile per value, bit p set where column `col` (0-based) equals
+ * values[v]; deleted rows included, as in the reference.  One pass over the
+ * column for all values. */
+int mbx_bitmap_index_build(mbx_ctx *ctx, const mbx_table *t, int32_t col, const mbx_operand *values,
+                           int32_t nvalues, mbx_bitmap **out);
+
+/* ---- late materialisation: the nextSetBit loops + Heapfile.findRID/getRecord
+ * per output column (R/index/ColumnarIndexScan.java:287-308,
+ * R/iterator/ColumnarColumnScan.java:151-176, R/iterator/Projection.java:103-146) */
+/* ascending global positions of the set bits (BitSet.nextSetBit order) */
+int mbx_bitmap_select(mbx_ctx *ctx, const mbx_bitmap *b, int64_t row_offset, int64_t *host_ids,
+                      int64_t cap, int64_t *n);
+/* positions + projected column values of every selected row, column-major
+ * into host buffers (proj: 0-based columns; value layout as in
+ * mbx_table_stage; ids may be NULL) */
+int mbx_materialize(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *sel, const int32_t *proj,
+                    int32_t nproj, int64_t *host_ids, void *const *host_out, int64_t cap, int64_t *n);
+/* device-side variant (outputs stay in HBM: dev_ids / dev_out[j] of `cap` rows) */
+int mbx_materialize_async(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *sel,
+                          const int32_t *proj, int32_t nproj, int64_t *dev_ids,
+                          void *const *dev_out, int64_t *dev_count);
+
+/* ---- iterator.Iterator get_next() batching (R/iterator/Iterator.java:12-141):
+ * a cursor holds the materialised selection in HBM and hands it out in
+ * batches; get_next() of a Java/C++ Iterator walks one batch at a time. */
+int mbx_cursor_open(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *sel, const int32_t *proj,
+                    int32_t nproj, mbx_cursor **out);
+int mbx_cursor_count(const mbx_cursor *c, int64_t *count);
+int mbx_cursor_next(mbx_cursor *c, int64_t max_rows, int64_t *host_ids, void *const *host_out,
+                    int64_t *n);
+int mbx_cursor_restart(mbx_cursor *c); /* Iterator.restart() */
+int mbx_cursor_close(mbx_cursor *c);   /* Iterator.close(), idempotent via free */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MBX_H */

@@ -1,0 +1,1291 @@
+// mbx_api.cpp -- the C-ABI (include/mbx.h) over the CDNA4 kernels.
+//
+// Host-side responsibilities, each restating a piece of the reference:
+//   * staging (TupleScan / Columnarfile open, R/columnar/TupleScan.java:29-47):
+//     host column arrays -> HBM column chunks, char(n) into the device string
+//     image (mbx_internal.hpp);
+//   * plan compilation (PredEval.Eval type rules, R/iterator/PredEval.java:54-135):
+//     operand types, FldSpec ranges, literal-on-left orientation, constant
+//     terms, NOT == NE, NOP / RANGE never true;
+//   * result plumbing for get_next()/get_next_tid() (cursors, BitSets).
+// Nothing here computes a query result on the CPU: every row-level operation
+// is a kernel launch on the context stream.
+#include "../../include/mbx.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mbx_internal.hpp"
+
+using namespace mbx;
+
+// ------------------------------------------------------------------ errors
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess) return fail(MBX_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define NOTNULL(p) \
+  do {             \
+    if (!(p)) return fail(MBX_E_INVALID, "%s: null argument `%s`", __func__, #p); \
+  } while (0)
+
+// ----------------------------------------------------------------- objects
+
+struct mbx_ctx {
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  Partial* partials = nullptr;  // scratch, one per block of the largest scan so far
+  int64_t partials_cap = 0;
+  AggOut* dagg = nullptr;
+  int64_t* dcount = nullptr;
+  int32_t* dnan = nullptr;
+  uint32_t* ticket = nullptr;   // in-launch finalize ticket (always 0 between launches)
+  void* pinned = nullptr;       // 256 bytes of pinned host scratch
+};
+
+struct TCol {
+  int32_t attr_type = 0;
+  int32_t size = 0;
+  int32_t stride_w = 1;  // device words per row
+  void* dev = nullptr;
+  bool owned = false;
+};
+
+struct mbx_table {
+  mbx_ctx* ctx = nullptr;
+  int64_t nrows = 0;
+  int64_t row_offset = 0;
+  std::vector<TCol> cols;
+  uint64_t* deleted = nullptr;
+  bool owns_deleted = false;
+  bool aligned16 = true;
+};
+
+struct PlanVariant {
+  int32_t agg_col = -1;  // -1: filter only
+  KPlan* dev = nullptr;
+  int32_t fast_k = 0;
+  int32_t agg_kind = kInt;
+};
+
+struct mbx_plan {
+  mbx_ctx* ctx = nullptr;
+  const mbx_table* t = nullptr;
+  KPlan host{};
+  std::vector<int32_t> slot_col;  // table column of each slot
+  bool all_4byte_literal = true;  // every term `column OP literal` on 4-byte columns
+  std::vector<PlanVariant> variants;
+};
+
+struct mbx_bitmap {
+  mbx_ctx* ctx = nullptr;
+  int64_t nbits = 0;
+  int64_t nwords = 0;
+  uint64_t* words = nullptr;
+  int64_t wpb = 4;        // words per segment
+  int64_t nseg = 1;
+  Partial* segs = nullptr;  // per-segment counts (Partial.count)
+  int64_t* seg_off = nullptr;
+  int64_t count = -1;     // host copy of the cardinality, -1 = unknown
+};
+
+struct mbx_cursor {
+  mbx_ctx* ctx = nullptr;
+  int64_t count = 0;
+  int64_t next = 0;
+  const mbx_table* t = nullptr;
+  int64_t* ids = nullptr;  // device
+  std::vector<void*> outs; // device, one per projected column
+  std::vector<int32_t> proj;
+};
+
+// ----------------------------------------------------------------- helpers
+
+static int64_t tiles_per_block_for(int64_t nrows) {
+  const char* e = getenv("MBX_TILES_PER_BLOCK");
+  if (e && atoll(e) > 0) return atoll(e);
+  return choose_tiles_per_block(nrows);
+}
+
+static int ensure_partials(mbx_ctx* c, int64_t n) {
+  if (n <= c->partials_cap) return MBX_OK;
+  if (c->partials) HIPCHK(hipFree(c->partials));
+  c->partials = nullptr;
+  const int64_t cap = n < 4096 ? 4096 : n;
+  HIPCHK(hipMalloc(&c->partials, sizeof(Partial) * cap));
+  c->partials_cap = cap;
+  return MBX_OK;
+}
+
+static int set_device(mbx_ctx* c) {
+  HIPCHK(hipSetDevice(c->device));
+  return MBX_OK;
+}
+
+// device string image: modified UTF-8, C0 80 -> 00 01, zero padded to stride
+static void encode_device_string(const uint8_t* src, int32_t len, uint8_t* dst, int32_t stride) {
+  int32_t n = len < stride ? len : stride;
+  // the payload ends at the first 0x00 (zero padding never occurs inside modified UTF-8)
+  int32_t m = 0;
+  while (m < n && src[m] != 0) m++;
+  memset(dst, 0, (size_t)stride);
+  for (int32_t i = 0; i < m; i++) {
+    if (src[i] == 0xC0 && i + 1 < m && src[i + 1] == 0x80) {
+      dst[i] = 0x00;
+      dst[i + 1] = 0x01;
+      i++;
+    } else {
+      dst[i] = src[i];
+    }
+  }
+}
+
+static void decode_device_string(const uint8_t* src, int32_t stride, uint8_t* dst, int32_t size) {
+  memset(dst, 0, (size_t)size);
+  for (int32_t i = 0; i < stride && i < size; i++) {
+    if (src[i] == 0x00) {
+      if (i + 1 < stride && src[i + 1] == 0x01 && i + 1 < size) {
+        dst[i] = 0xC0;
+        dst[i + 1] = 0x80;
+        i++;
+        continue;
+      }
+      break;
+    }
+    dst[i] = src[i];
+  }
+}
+
+static int64_t words_for(int64_t nbits) { return (nbits + 63) / 64; }
+
+static int bitmap_new(mbx_ctx* c, int64_t nbits, mbx_bitmap** out) {
+  mbx_bitmap* b = new (std::nothrow) mbx_bitmap();
+  if (!b) return fail(MBX_E_NOMEM, "bitmap: host allocation");
+  b->ctx = c;
+  b->nbits = nbits;
+  b->nwords = words_for(nbits);
+  b->wpb = tiles_per_block_for(nbits) * kWordsPerTile;
+  b->nseg = b->nwords == 0 ? 1 : (b->nwords + b->wpb - 1) / b->wpb;
+  hipError_t e = hipMalloc(&b->words, sizeof(uint64_t) * (size_t)(b->nwords > 0 ? b->nwords : 1));
+  if (e == hipSuccess) e = hipMalloc(&b->segs, sizeof(Partial) * (size_t)b->nseg);
+  if (e == hipSuccess) e = hipMalloc(&b->seg_off, sizeof(int64_t) * (size_t)b->nseg);
+  if (e != hipSuccess) {
+    hipFree(b->words);
+    hipFree(b->segs);
+    hipFree(b->seg_off);
+    delete b;
+    return fail(MBX_E_NOMEM, "bitmap of %lld bits: %s", (long long)nbits, hipGetErrorString(e));
+  }
+  if (b->nwords == 0) hipMemsetAsync(b->segs, 0, sizeof(Partial), c->stream);
+  *out = b;
+  return MBX_OK;
+}
+
+// ----------------------------------------------------------------- library
+
+extern "C" int mbx_abi_version(void) { return MBX_ABI_VERSION; }
+
+extern "C" const char* mbx_last_error(void) { return g_err.c_str(); }
+
+extern "C" int mbx_device_count(int32_t* n) {
+  NOTNULL(n);
+  int k = 0;
+  hipError_t e = hipGetDeviceCount(&k);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail(MBX_E_DEVICE, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  *n = k;
+  return MBX_OK;
+}
+
+extern "C" int mbx_init(int32_t device, mbx_ctx** out) {
+  NOTNULL(out);
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return fail(MBX_E_DEVICE, "mbx_init: no HIP device visible (the executor has no CPU fallback)");
+  if (device < 0 || device >= n) return fail(MBX_E_INVALID, "mbx_init: device %d of %d", device, n);
+  mbx_ctx* c = new (std::nothrow) mbx_ctx();
+  if (!c) return fail(MBX_E_NOMEM, "mbx_init: host allocation");
+  c->device = device;
+  int rc = MBX_OK;
+  do {
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->dagg, sizeof(AggOut));
+    if (e == hipSuccess) e = hipMalloc(&c->dcount, sizeof(int64_t) * 2);
+    if (e == hipSuccess) e = hipMalloc(&c->dnan, sizeof(int32_t) * 2);
+    if (e == hipSuccess) e = hipMalloc(&c->ticket, sizeof(uint32_t) * 4);
+    if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(uint32_t) * 4);
+    if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 256, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      rc = fail(MBX_E_DEVICE, "mbx_init: %s", hipGetErrorString(e));
+      break;
+    }
+    rc = ensure_partials(c, 4096);
+  } while (0);
+  if (rc != MBX_OK) {
+    mbx_free(c);
+    return rc;
+  }
+  *out = c;
+  return MBX_OK;
+}
+
+extern "C" int mbx_free(mbx_ctx* c) {
+  if (!c) return MBX_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  hipFree(c->partials);
+  hipFree(c->dagg);
+  hipFree(c->dcount);
+  hipFree(c->dnan);
+  hipFree(c->ticket);
+  if (c->pinned) hipHostFree(c->pinned);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return MBX_OK;
+}
+
+extern "C" int mbx_sync(mbx_ctx* c) {
+  NOTNULL(c);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MBX_OK;
+}
+
+extern "C" void* mbx_stream(mbx_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// ------------------------------------------------------------------ tables
+
+static int check_cols(const mbx_col_desc* cols, int32_t ncols) {
+  if (ncols <= 0) return fail(MBX_E_INVALID, "table: ncols = %d", ncols);
+  for (int32_t j = 0; j < ncols; j++) {
+    const int32_t t = cols[j].attr_type;
+    if (t != MBX_ATTR_INTEGER && t != MBX_ATTR_REAL && t != MBX_ATTR_STRING)
+      return fail(MBX_E_TYPE, "table: column %d has AttrType %d (only attrInteger/attrReal/attrString are stored)",
+                  j, t);
+    if (t == MBX_ATTR_STRING && (cols[j].size <= 0 || cols[j].size > MBX_MAX_STR_BYTES))
+      return fail(MBX_E_UNSUPPORTED, "table: column %d char(%d) outside 1..%d", j, cols[j].size,
+                  MBX_MAX_STR_BYTES);
+  }
+  return MBX_OK;
+}
+
+static int32_t stride_words(const mbx_col_desc& d) {
+  return d.attr_type == MBX_ATTR_STRING ? (d.size + 3) / 4 : 1;
+}
+
+extern "C" int mbx_table_free(mbx_table* t) {
+  if (!t) return MBX_OK;
+  hipSetDevice(t->ctx->device);
+  hipStreamSynchronize(t->ctx->stream);
+  for (auto& c : t->cols)
+    if (c.owned) hipFree(c.dev);
+  if (t->owns_deleted) hipFree(t->deleted);
+  delete t;
+  return MBX_OK;
+}
+
+extern "C" int mbx_table_stage(mbx_ctx* c, const mbx_col_desc* cols, int32_t ncols, int64_t nrows,
+                               const void* const* host_cols, const uint64_t* deleted_words, int64_t row_offset,
+                               mbx_table** out) {
+  NOTNULL(c);
+  NOTNULL(cols);
+  NOTNULL(host_cols);
+  NOTNULL(out);
+  *out = nullptr;
+  int rc = check_cols(cols, ncols);
+  if (rc) return rc;
+  if (nrows < 0) return fail(MBX_E_INVALID, "table: nrows = %lld", (long long)nrows);
+  if (row_offset < 0 || (row_offset & 63)) return fail(MBX_E_INVALID, "table: row_offset %lld not a multiple of 64",
+                                                      (long long)row_offset);
+  if ((rc = set_device(c))) return rc;
+  mbx_table* t = new (std::nothrow) mbx_table();
+  if (!t) return fail(MBX_E_NOMEM, "table: host allocation");
+  t->ctx = c;
+  t->nrows = nrows;
+  t->row_offset = row_offset;
+  const size_t n = (size_t)(nrows > 0 ? nrows : 1);
+  for (int32_t j = 0; j < ncols; j++) {
+    TCol col;
+    col.attr_type = cols[j].attr_type;
+    col.size = cols[j].attr_type == MBX_ATTR_STRING ? cols[j].size : 4;
+    col.stride_w = stride_words(cols[j]);
+    col.owned = true;
+    const size_t bytes = n * (size_t)col.stride_w * 4;
+    hipError_t e = hipMalloc(&col.dev, bytes);
+    if (e != hipSuccess) {
+      mbx_table_free(t);
+      return fail(MBX_E_NOMEM, "table: column %d (%zu bytes): %s", j, bytes, hipGetErrorString(e));
+    }
+    t->cols.push_back(col);
+    if (nrows == 0) continue;
+    if (!host_cols[j]) {
+      mbx_table_free(t);
+      return fail(MBX_E_INVALID, "table: host_cols[%d] is null", j);
+    }
+    if (col.attr_type != MBX_ATTR_STRING) {
+      e = hipMemcpy(col.dev, host_cols[j], (size_t)nrows * 4, hipMemcpyHostToDevice);
+    } else {
+      const int32_t stride = col.stride_w * 4;
+      std::vector<uint8_t> img((size_t)nrows * (size_t)stride);
+      const uint8_t* src = (const uint8_t*)host_cols[j];
+      for (int64_t r = 0; r < nrows; r++)
+        encode_device_string(src + (size_t)r * (size_t)col.size, col.size, img.data() + (size_t)r * (size_t)stride,
+                             stride);
+      e = hipMemcpy(col.dev, img.data(), img.size(), hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+      mbx_table_free(t);
+      return fail(MBX_E_DEVICE, "table: staging column %d: %s", j, hipGetErrorString(e));
+    }
+  }
+  if (deleted_words && nrows > 0) {
+    const int64_t nw = words_for(nrows);
+    std::vector<uint64_t> d(deleted_words, deleted_words + nw);
+    if (nrows & 63) d[nw - 1] &= (1ull << (nrows & 63)) - 1ull;
+    hipError_t e = hipMalloc(&t->deleted, sizeof(uint64_t) * (size_t)nw);
+    if (e == hipSuccess) e = hipMemcpy(t->deleted, d.data(), sizeof(uint64_t) * (size_t)nw, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      mbx_table_free(t);
+      return fail(MBX_E_DEVICE, "table: staging deleted bitmap: %s", hipGetErrorString(e));
+    }
+    t->owns_deleted = true;
+  }
+  *out = t;
+  return MBX_OK;
+}
+
+extern "C" int mbx_table_wrap(mbx_ctx* c, const mbx_col_desc* cols, int32_t ncols, int64_t nrows,
+                              const void* const* dev_cols, const uint64_t* dev_deleted_words, int64_t row_offset,
+                              mbx_table** out) {
+  NOTNULL(c);
+  NOTNULL(cols);
+  NOTNULL(dev_cols);
+  NOTNULL(out);
+  *out = nullptr;
+  int rc = check_cols(cols, ncols);
+  if (rc) return rc;
+  if (nrows < 0 || row_offset < 0 || (row_offset & 63))
+    return fail(MBX_E_INVALID, "table_wrap: nrows %lld row_offset %lld", (long long)nrows, (long long)row_offset);
+  mbx_table* t = new (std::nothrow) mbx_table();
+  if (!t) return fail(MBX_E_NOMEM, "table: host allocation");
+  t->ctx = c;
+  t->nrows = nrows;
+  t->row_offset = row_offset;
+  for (int32_t j = 0; j < ncols; j++) {
+    if (!dev_cols[j] && nrows > 0) {
+      delete t;
+      return fail(MBX_E_INVALID, "table_wrap: dev_cols[%d] is null", j);
+    }
+    TCol col;
+    col.attr_type = cols[j].attr_type;
+    col.size = cols[j].attr_type == MBX_ATTR_STRING ? cols[j].size : 4;
+    col.stride_w = stride_words(cols[j]);
+    col.dev = const_cast<void*>(dev_cols[j]);
+    col.owned = false;
+    if (((uintptr_t)col.dev) & 15) t->aligned16 = false;
+    t->cols.push_back(col);
+  }
+  t->deleted = const_cast<uint64_t*>(dev_deleted_words);
+  t->owns_deleted = false;
+  *out = t;
+  return MBX_OK;
+}
+
+extern "C" int mbx_table_info(const mbx_table* t, int64_t* nrows, int64_t* row_offset, int32_t* ncols) {
+  NOTNULL(t);
+  if (nrows) *nrows = t->nrows;
+  if (row_offset) *row_offset = t->row_offset;
+  if (ncols) *ncols = (int32_t)t->cols.size();
+  return MBX_OK;
+}
+
+// ------------------------------------------------------------------- plans
+
+static int col_kind(int32_t attr) { return attr == MBX_ATTR_INTEGER ? kInt : (attr == MBX_ATTR_REAL ? kReal : kStr); }
+
+static int slot_for(mbx_plan* p, int32_t col) {
+  for (size_t s = 0; s < p->slot_col.size(); s++)
+    if (p->slot_col[s] == col) return (int)s;
+  if ((int)p->slot_col.size() >= kMaxCols) return -1;
+  const TCol& tc = p->t->cols[(size_t)col];
+  const int s = (int)p->slot_col.size();
+  p->slot_col.push_back(col);
+  p->host.cols[s].base = tc.dev;
+  p->host.cols[s].kind = col_kind(tc.attr_type);
+  p->host.cols[s].stride_w = tc.stride_w;
+  p->host.ncols = s + 1;
+  return s;
+}
+
+// PredEval's op table (R/iterator/PredEval.java:137-162) applied to a constant
+// comparison result.
+static bool op_on(int32_t op, int comp) {
+  switch (op) {
+    case MBX_OP_EQ: return comp == 0;
+    case MBX_OP_LT: return comp < 0;
+    case MBX_OP_GT: return comp > 0;
+    case MBX_OP_NE:
+    case MBX_OP_NOT: return comp != 0;
+    case MBX_OP_LE: return comp <= 0;
+    case MBX_OP_GE: return comp >= 0;
+    default: return false;
+  }
+}
+
+static int32_t cmp_op_of(int32_t op) {
+  switch (op) {
+    case MBX_OP_LT: return kLT;
+    case MBX_OP_LE: return kLE;
+    case MBX_OP_GT: return kGT;
+    case MBX_OP_GE: return kGE;
+    case MBX_OP_EQ: return kEQ;
+    default: return kNE;  // aopNE, aopNOT
+  }
+}
+
+// comp(lit, col) = -comp(col, lit): mirror the operator
+static int32_t flip(int32_t op) {
+  switch (op) {
+    case kLT: return kGT;
+    case kLE: return kGE;
+    case kGT: return kLT;
+    case kGE: return kLE;
+    default: return op;
+  }
+}
+
+static int literal_type_ok(int32_t type) {
+  return type == MBX_ATTR_INTEGER || type == MBX_ATTR_REAL || type == MBX_ATTR_STRING;
+}
+
+static int add_pool_string(mbx_plan* p, const mbx_operand& o, int32_t& words_used, KTerm& kt) {
+  if (o.string_len < 0 || o.string_len > MBX_MAX_STR_BYTES || (o.string_len > 0 && !o.string))
+    return fail(MBX_E_UNSUPPORTED, "plan: string literal of %d bytes (max %d)", o.string_len, MBX_MAX_STR_BYTES);
+  const int32_t w = (o.string_len + 3) / 4;
+  if (words_used + (w > 0 ? w : 1) > kMaxPoolWords)
+    return fail(MBX_E_UNSUPPORTED, "plan: string literals exceed %d bytes", kMaxPoolWords * 4);
+  uint8_t tmp[MBX_MAX_STR_BYTES + 4];
+  encode_device_string((const uint8_t*)o.string, o.string_len, tmp, w * 4);
+  memcpy(&p->host.pool[words_used], tmp, (size_t)w * 4);
+  kt.soff = words_used;
+  kt.swords = w;
+  words_used += w > 0 ? w : 1;
+  return MBX_OK;
+}
+
+static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_plan* p) {
+  p->ctx = c;
+  p->t = t;
+  memset(&p->host, 0, sizeof(KPlan));
+  p->host.agg_slot = -1;
+  const int32_t ncols = (int32_t)t->cols.size();
+  int32_t nconj = cnf ? cnf->nconj : 0;
+  if (nconj < 0) return fail(MBX_E_INVALID, "plan: nconj = %d", nconj);
+  if (nconj > MBX_MAX_CONJ) return fail(MBX_E_UNSUPPORTED, "plan: %d conjuncts (max %d)", nconj, MBX_MAX_CONJ);
+  if (nconj > 0 && (!cnf->conds || !cnf->conj_offsets)) return fail(MBX_E_INVALID, "plan: null conds/conj_offsets");
+  uint32_t all = 0;
+  int32_t nterms = 0, pool_used = 0;
+  for (int32_t ci = 0; ci < nconj; ci++) {
+    const int32_t k0 = cnf->conj_offsets[ci], k1 = cnf->conj_offsets[ci + 1];
+    if (k0 < 0 || k1 < k0) return fail(MBX_E_INVALID, "plan: conj_offsets not ascending at %d", ci);
+    bool always_true = false;
+    const int32_t first_term = nterms;
+    for (int32_t k = k0; k < k1; k++) {
+      const mbx_condexpr& e = cnf->conds[k];
+      const mbx_operand& o1 = e.operand1;
+      const mbx_operand& o2 = e.operand2;
+      if (e.op < MBX_OP_EQ || e.op > MBX_OP_RANGE) return fail(MBX_E_INVALID, "plan: AttrOperator %d", e.op);
+      // comparison type from operand 1 (PredEval.java:54-91)
+      int32_t ctype;
+      if (o1.type == MBX_ATTR_SYMBOL) {
+        if (o1.fld < 1 || o1.fld > ncols)
+          return fail(MBX_E_RANGE, "plan: FldSpec offset %d outside 1..%d", o1.fld, ncols);
+        ctype = t->cols[(size_t)o1.fld - 1].attr_type;
+      } else if (literal_type_ok(o1.type)) {
+        ctype = o1.type;
+      } else {
+        return fail(MBX_E_TYPE, "plan: operand1 AttrType %d", o1.type);
+      }
+      int32_t t2;
+      if (o2.type == MBX_ATTR_SYMBOL) {
+        if (o2.fld < 1 || o2.fld > ncols)
+          return fail(MBX_E_RANGE, "plan: FldSpec offset %d outside 1..%d", o2.fld, ncols);
+        t2 = t->cols[(size_t)o2.fld - 1].attr_type;
+      } else if (literal_type_ok(o2.type)) {
+        t2 = o2.type;
+      } else {
+        return fail(MBX_E_TYPE, "plan: operand2 AttrType %d", o2.type);
+      }
+      if (t2 != ctype)
+        return fail(MBX_E_TYPE, "plan: term %d compares AttrType %d with %d (reference misreads the field)", k,
+                    ctype, t2);
+      const mbx_operand* lit = o2.type == MBX_ATTR_SYMBOL ? (o1.type == MBX_ATTR_SYMBOL ? nullptr : &o1) : &o2;
+      if (lit && lit->type == MBX_ATTR_REAL && std::isnan(lit->real))
+        return fail(MBX_E_TYPE, "plan: NaN literal (TupleUtils falls through to the string compare and raises)");
+      if (e.op == MBX_OP_NOP || e.op == MBX_OP_RANGE) continue;  // never true
+      if (o1.type != MBX_ATTR_SYMBOL && o2.type != MBX_ATTR_SYMBOL) {
+        // two literals share PredEval's `value` tuple: operand 2 vs itself
+        if (op_on(e.op, 0)) always_true = true;
+        continue;
+      }
+      if (nterms >= kMaxTerms) return fail(MBX_E_UNSUPPORTED, "plan: more than %d terms", kMaxTerms);
+      KTerm kt;
+      memset(&kt, 0, sizeof(kt));
+      kt.kind = col_kind(ctype);
+      kt.conj_bit = 1u << ci;
+      kt.rhs = -1;
+      int32_t op = cmp_op_of(e.op);
+      const mbx_operand* coln;
+      if (o1.type == MBX_ATTR_SYMBOL) {
+        coln = &o1;
+        if (o2.type == MBX_ATTR_SYMBOL) {
+          const int s2 = slot_for(p, o2.fld - 1);
+          if (s2 < 0) return fail(MBX_E_UNSUPPORTED, "plan: more than %d distinct columns", kMaxCols);
+          kt.rhs = s2;
+          p->all_4byte_literal = false;
+        }
+      } else {
+        coln = &o2;  // literal on the left: compare column with literal, operator mirrored
+        op = flip(op);
+      }
+      const int s1 = slot_for(p, coln->fld - 1);
+      if (s1 < 0) return fail(MBX_E_UNSUPPORTED, "plan: more than %d distinct columns", kMaxCols);
+      kt.lhs = s1;
+      kt.op = op;
+      if (kt.rhs < 0) {
+        if (ctype == MBX_ATTR_INTEGER) kt.ilit = lit->integer;
+        else if (ctype == MBX_ATTR_REAL) kt.flit = lit->real;
+        else {
+          int rc = add_pool_string(p, *lit, pool_used, kt);
+          if (rc) return rc;
+        }
+      }
+      if (ctype == MBX_ATTR_STRING) p->all_4byte_literal = false;
+      if (ctype == MBX_ATTR_REAL) p->host.has_real = 1;
+      p->host.terms[nterms++] = kt;
+    }
+    if (always_true) {
+      nterms = first_term;  // the conjunct holds for every row: drop it
+      continue;
+    }
+    all |= 1u << ci;  // an empty conjunct stays required and is never satisfied
+  }
+  p->host.nterms = nterms;
+  p->host.all_conj = all;
+  return MBX_OK;
+}
+
+static int plan_variant(mbx_plan* p, int32_t agg_col, PlanVariant** out) {
+  for (auto& v : p->variants)
+    if (v.agg_col == agg_col) {
+      *out = &v;
+      return MBX_OK;
+    }
+  PlanVariant v;
+  v.agg_col = agg_col;
+  KPlan kp = p->host;
+  std::vector<int32_t> slots = p->slot_col;
+  if (agg_col >= 0) {
+    const int32_t at = p->t->cols[(size_t)agg_col].attr_type;
+    if (at != MBX_ATTR_INTEGER && at != MBX_ATTR_REAL)
+      return fail(MBX_E_TYPE, "aggregate: column %d is not attrInteger/attrReal", agg_col);
+    v.agg_kind = at == MBX_ATTR_REAL ? kReal : kInt;
+    int s = -1;
+    for (size_t i = 0; i < slots.size(); i++)
+      if (slots[i] == agg_col) s = (int)i;
+    if (s < 0) {
+      if ((int)slots.size() >= kMaxCols) return fail(MBX_E_UNSUPPORTED, "aggregate: too many columns");
+      s = (int)slots.size();
+      slots.push_back(agg_col);
+      const TCol& tc = p->t->cols[(size_t)agg_col];
+      kp.cols[s].base = tc.dev;
+      kp.cols[s].kind = col_kind(tc.attr_type);
+      kp.cols[s].stride_w = tc.stride_w;
+      kp.ncols = s + 1;
+    }
+    kp.agg_slot = s;
+  }
+  bool four = p->all_4byte_literal && p->t->aligned16;
+  for (size_t i = 0; i < slots.size(); i++)
+    if (p->t->cols[slots[i]].attr_type == MBX_ATTR_STRING) four = false;
+  const char* force = getenv("MBX_FORCE_GENERIC");
+  if (force && force[0] == '1') four = false;
+  v.fast_k = (four && !slots.empty() && slots.size() <= 4) ? (int32_t)slots.size() : 0;
+  if (four && slots.empty()) {
+    // no column referenced (no filter, or only constant terms): slot 0 is
+    // any 4-byte column so the fast kernel has something to stream
+    for (size_t j = 0; j < p->t->cols.size(); j++)
+      if (p->t->cols[j].attr_type != MBX_ATTR_STRING) {
+        kp.cols[0].base = p->t->cols[j].dev;
+        kp.cols[0].kind = col_kind(p->t->cols[j].attr_type);
+        kp.cols[0].stride_w = 1;
+        kp.ncols = 1;
+        v.fast_k = 1;
+        break;
+      }
+  }
+  hipError_t e = hipMalloc(&v.dev, sizeof(KPlan));
+  if (e == hipSuccess) e = hipMemcpy(v.dev, &kp, sizeof(KPlan), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    hipFree(v.dev);
+    return fail(MBX_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
+  }
+  p->variants.push_back(v);
+  *out = &p->variants.back();
+  return MBX_OK;
+}
+
+extern "C" int mbx_plan_compile(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_plan** out) {
+  NOTNULL(c);
+  NOTNULL(t);
+  NOTNULL(out);
+  *out = nullptr;
+  int rc = set_device(c);
+  if (rc) return rc;
+  mbx_plan* p = new (std::nothrow) mbx_plan();
+  if (!p) return fail(MBX_E_NOMEM, "plan: host allocation");
+  rc = compile_into(c, t, cnf, p);
+  PlanVariant* v = nullptr;
+  if (!rc) rc = plan_variant(p, -1, &v);
+  if (rc) {
+    mbx_plan_free(p);
+    return rc;
+  }
+  *out = p;
+  return MBX_OK;
+}
+
+extern "C" int mbx_plan_free(mbx_plan* p) {
+  if (!p) return MBX_OK;
+  hipSetDevice(p->ctx->device);
+  hipStreamSynchronize(p->ctx->stream);
+  for (auto& v : p->variants) hipFree(v.dev);
+  delete p;
+  return MBX_OK;
+}
+
+// ------------------------------------------------------------------- scans
+
+// One launch per scan: the kernel's last block finalizes (count / aggregate /
+// NaN flag) through the context's ticket.
+static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int32_t mode, uint64_t* out_words,
+                        Partial* parts, int64_t tpb, int64_t* count_out, AggOut* agg_out, int32_t* nan_out) {
+  ScanLaunch L;
+  L.plan = v.dev;
+  L.nrows = p->t->nrows;
+  L.tiles_per_block = tpb;
+  L.deleted = p->t->deleted;
+  L.out_words = out_words;
+  L.partials = parts;
+  L.mode = mode;
+  L.fast_k = v.fast_k;
+  L.agg_kind = v.agg_kind;
+  L.ticket = c->ticket;
+  L.count_out = count_out;
+  L.agg_out = agg_out;
+  L.nan_out = nan_out;
+  HIPCHK(launch_scan(L, c->stream));
+  return MBX_OK;
+}
+
+static int scan_to_count(mbx_ctx* c, mbx_plan* p, int64_t* dev_count, int32_t* dev_nan) {
+  PlanVariant* v = nullptr;
+  int rc = plan_variant(p, -1, &v);
+  if (rc) return rc;
+  const int64_t tpb = tiles_per_block_for(p->t->nrows);
+  const int64_t nb = grid_blocks(p->t->nrows, tpb);
+  if ((rc = ensure_partials(c, nb))) return rc;
+  return enqueue_scan(c, p, *v, kModeCount, nullptr, c->partials, tpb, dev_count, nullptr, dev_nan);
+}
+
+static int check_nan(mbx_ctx* c) {
+  const int32_t* h = (const int32_t*)c->pinned;
+  if (h[8]) return fail(MBX_E_TYPE, "NaN in a float comparison (TupleUtils falls through to the string compare and raises)");
+  return MBX_OK;
+}
+
+extern "C" int mbx_scan_count(mbx_ctx* c, const mbx_plan* pc, int64_t* count) {
+  NOTNULL(c);
+  NOTNULL(pc);
+  NOTNULL(count);
+  mbx_plan* p = const_cast<mbx_plan*>(pc);
+  int rc = set_device(c);
+  if (rc) return rc;
+  if ((rc = scan_to_count(c, p, c->dcount, c->dnan))) return rc;
+  int64_t* h = (int64_t*)c->pinned;
+  HIPCHK(hipMemcpyAsync(h, c->dcount, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, c->dnan, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *count = h[0];
+  return check_nan(c);
+}
+
+extern "C" int mbx_scan_count_async(mbx_ctx* c, const mbx_plan* pc, int64_t* dev_count) {
+  NOTNULL(c);
+  NOTNULL(pc);
+  NOTNULL(dev_count);
+  return scan_to_count(c, const_cast<mbx_plan*>(pc), dev_count, c->dnan);
+}
+
+static int scan_bitmap_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b) {
+  if (b->nbits != p->t->nrows)
+    return fail(MBX_E_INVALID, "scan_bitmap: bitmap has %lld bits, table %lld rows", (long long)b->nbits,
+                (long long)p->t->nrows);
+  PlanVariant* v = nullptr;
+  int rc = plan_variant(p, -1, &v);
+  if (rc) return rc;
+  const int64_t tpb = b->wpb / kWordsPerTile;
+  if (grid_blocks(p->t->nrows, tpb) != b->nseg) return fail(MBX_E_INVALID, "scan_bitmap: segment mismatch");
+  return enqueue_scan(c, p, *v, kModeBitmap, b->words, b->segs, tpb, c->dcount, nullptr, c->dnan);
+}
+
+// read back the count + NaN flag the last scan's final block wrote
+static int scan_result_sync(mbx_ctx* c, int64_t* count) {
+  int64_t* h = (int64_t*)c->pinned;
+  HIPCHK(hipMemcpyAsync(h, c->dcount, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, c->dnan, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *count = h[0];
+  return MBX_OK;
+}
+
+extern "C" int mbx_scan_bitmap_async(mbx_ctx* c, const mbx_plan* pc, mbx_bitmap* out) {
+  NOTNULL(c);
+  NOTNULL(pc);
+  NOTNULL(out);
+  out->count = -1;
+  return scan_bitmap_into(c, const_cast<mbx_plan*>(pc), out);
+}
+
+static int bitmap_count_sync(mbx_ctx* c, mbx_bitmap* b, bool with_nan) {
+  HIPCHK(launch_finalize(b->segs, b->nseg, kInt, nullptr, c->dcount, c->dnan, c->stream));
+  int64_t* h = (int64_t*)c->pinned;
+  HIPCHK(hipMemcpyAsync(h, c->dcount, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, c->dnan, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  b->count = h[0];
+  return with_nan ? check_nan(c) : MBX_OK;
+}
+
+extern "C" int mbx_scan_bitmap(mbx_ctx* c, const mbx_plan* pc, mbx_bitmap** out, int64_t* count) {
+  NOTNULL(c);
+  NOTNULL(pc);
+  NOTNULL(out);
+  *out = nullptr;
+  mbx_plan* p = const_cast<mbx_plan*>(pc);
+  int rc = set_device(c);
+  if (rc) return rc;
+  mbx_bitmap* b = nullptr;
+  if ((rc = bitmap_new(c, p->t->nrows, &b))) return rc;
+  if (!(rc = scan_bitmap_into(c, p, b)) && !(rc = scan_result_sync(c, &b->count))) rc = check_nan(c);
+  if (rc) {
+    mbx_bitmap_free(b);
+    return rc;
+  }
+  if (count) *count = b->count;
+  *out = b;
+  return MBX_OK;
+}
+
+static int scan_agg(mbx_ctx* c, mbx_plan* p, int32_t agg_col, AggOut* dev_out, int32_t* dev_nan) {
+  if (agg_col < 0 || agg_col >= (int32_t)p->t->cols.size())
+    return fail(MBX_E_RANGE, "aggregate: column %d outside 0..%zu", agg_col, p->t->cols.size() - 1);
+  PlanVariant* v = nullptr;
+  int rc = plan_variant(p, agg_col, &v);
+  if (rc) return rc;
+  const int64_t tpb = tiles_per_block_for(p->t->nrows);
+  const int64_t nb = grid_blocks(p->t->nrows, tpb);
+  if ((rc = ensure_partials(c, nb))) return rc;
+  return enqueue_scan(c, p, *v, kModeAgg, nullptr, c->partials, tpb, nullptr, dev_out, dev_nan);
+}
+
+extern "C" int mbx_scan_aggregate(mbx_ctx* c, const mbx_plan* pc, int32_t agg_col, mbx_agg* out) {
+  NOTNULL(c);
+  NOTNULL(pc);
+  NOTNULL(out);
+  static_assert(sizeof(mbx_agg) == sizeof(AggOut), "mbx_agg layout");
+  int rc = set_device(c);
+  if (rc) return rc;
+  if ((rc = scan_agg(c, const_cast<mbx_plan*>(pc), agg_col, c->dagg, c->dnan))) return rc;
+  HIPCHK(hipMemcpyAsync(c->pinned, c->dagg, sizeof(AggOut), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 16, c->dnan, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  memcpy(out, c->pinned, sizeof(mbx_agg));
+  if (((const int32_t*)c->pinned)[16])
+    return fail(MBX_E_TYPE, "NaN in a float comparison (TupleUtils falls through to the string compare and raises)");
+  return MBX_OK;
+}
+
+extern "C" int mbx_scan_aggregate_async(mbx_ctx* c, const mbx_plan* pc, int32_t agg_col, mbx_agg* dev_out) {
+  NOTNULL(c);
+  NOTNULL(pc);
+  NOTNULL(dev_out);
+  return scan_agg(c, const_cast<mbx_plan*>(pc), agg_col, (AggOut*)dev_out, c->dnan);
+}
+
+// ----------------------------------------------------------------- bitmaps
+
+extern "C" int mbx_bitmap_alloc(mbx_ctx* c, int64_t nbits, mbx_bitmap** out) {
+  NOTNULL(c);
+  NOTNULL(out);
+  *out = nullptr;
+  if (nbits < 0) return fail(MBX_E_INVALID, "bitmap: nbits %lld", (long long)nbits);
+  int rc = set_device(c);
+  if (rc) return rc;
+  return bitmap_new(c, nbits, out);
+}
+
+extern "C" int mbx_bitmap_free(mbx_bitmap* b) {
+  if (!b) return MBX_OK;
+  hipSetDevice(b->ctx->device);
+  hipStreamSynchronize(b->ctx->stream);
+  hipFree(b->words);
+  hipFree(b->segs);
+  hipFree(b->seg_off);
+  delete b;
+  return MBX_OK;
+}
+
+extern "C" int mbx_bitmap_upload(mbx_ctx* c, int64_t nbits, const uint64_t* host_words, mbx_bitmap** out) {
+  NOTNULL(c);
+  NOTNULL(out);
+  *out = nullptr;
+  if (nbits < 0) return fail(MBX_E_INVALID, "bitmap: nbits %lld", (long long)nbits);
+  if (nbits > 0 && !host_words) return fail(MBX_E_INVALID, "bitmap_upload: null words");
+  int rc = set_device(c);
+  if (rc) return rc;
+  mbx_bitmap* b = nullptr;
+  if ((rc = bitmap_new(c, nbits, &b))) return rc;
+  if (b->nwords > 0) {
+    hipError_t e = hipMemcpy(b->words, host_words, sizeof(uint64_t) * (size_t)b->nwords, hipMemcpyHostToDevice);
+    if (e == hipSuccess && (nbits & 63)) {
+      const uint64_t last = host_words[b->nwords - 1] & ((1ull << (nbits & 63)) - 1ull);
+      e = hipMemcpy(b->words + b->nwords - 1, &last, sizeof(uint64_t), hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) {
+      mbx_bitmap_free(b);
+      return fail(MBX_E_DEVICE, "bitmap_upload: %s", hipGetErrorString(e));
+    }
+  }
+  hipError_t e = launch_seg_popcount(b->words, b->nwords, b->wpb, b->segs, c->stream);
+  if (e != hipSuccess || (rc = bitmap_count_sync(c, b, false))) {
+    mbx_bitmap_free(b);
+    return rc ? rc : fail(MBX_E_DEVICE, "bitmap_upload: %s", hipGetErrorString(e));
+  }
+  *out = b;
+  return MBX_OK;
+}
+
+extern "C" int mbx_bitmap_download(mbx_ctx* c, const mbx_bitmap* b, uint64_t* host_words, int64_t nwords) {
+  NOTNULL(c);
+  NOTNULL(b);
+  if (nwords < b->nwords) return fail(MBX_E_INVALID, "bitmap_download: need %lld words", (long long)b->nwords);
+  if (b->nwords == 0) return MBX_OK;
+  NOTNULL(host_words);
+  int rc = set_device(c);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(host_words, b->words, sizeof(uint64_t) * (size_t)b->nwords, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MBX_OK;
+}
+
+extern "C" int mbx_bitmap_info(const mbx_bitmap* b, int64_t* nbits, int64_t* nwords, int64_t* count) {
+  NOTNULL(b);
+  if (nbits) *nbits = b->nbits;
+  if (nwords) *nwords = b->nwords;
+  if (count) *count = b->count;
+  return MBX_OK;
+}
+
+extern "C" int mbx_bitmap_combine(mbx_ctx* c, int32_t op, const mbx_bitmap* a, const mbx_bitmap* b,
+                                  mbx_bitmap** out, int64_t* count) {
+  NOTNULL(c);
+  NOTNULL(a);
+  NOTNULL(b);
+  NOTNULL(out);
+  *out = nullptr;
+  if (op < MBX_BM_AND || op > MBX_BM_ANDNOT) return fail(MBX_E_INVALID, "bitmap_combine: op %d", op);
+  if (a->nbits != b->nbits) return fail(MBX_E_INVALID, "bitmap_combine: %lld vs %lld bits", (long long)a->nbits,
+                                        (long long)b->nbits);
+  int rc = set_device(c);
+  if (rc) return rc;
+  mbx_bitmap* r = nullptr;
+  if ((rc = bitmap_new(c, a->nbits, &r))) return rc;
+  hipError_t e = launch_bitmap_combine(op, a->words, b->words, r->nwords, r->nbits, r->wpb, r->words, r->segs,
+                                       c->stream);
+  if (e != hipSuccess) {
+    mbx_bitmap_free(r);
+    return fail(MBX_E_DEVICE, "bitmap_combine: %s", hipGetErrorString(e));
+  }
+  if ((rc = bitmap_count_sync(c, r, false))) {
+    mbx_bitmap_free(r);
+    return rc;
+  }
+  if (count) *count = r->count;
+  *out = r;
+  return MBX_OK;
+}
+
+static int cnf_args(int64_t nbits, const mbx_bitmap* const* bms, const int32_t* conj_offsets, int32_t nconj,
+                    const mbx_bitmap* deleted, BitmapCnf* C) {
+  if (nconj < 1 || nconj > 32) return fail(MBX_E_UNSUPPORTED, "bitmap_cnf: %d conjuncts (1..32)", nconj);
+  NOTNULL(conj_offsets);
+  const int32_t nb = conj_offsets[nconj];
+  if (nb < 0 || nb > kMaxBitmaps) return fail(MBX_E_UNSUPPORTED, "bitmap_cnf: %d bitmaps (max %d)", nb, kMaxBitmaps);
+  if (nb > 0) NOTNULL(bms);
+  memset(C, 0, sizeof(*C));
+  C->nconj = nconj;
+  for (int32_t i = 0; i <= nconj; i++) {
+    if (conj_offsets[i] < 0 || conj_offsets[i] > nb || (i > 0 && conj_offsets[i] < conj_offsets[i - 1]))
+      return fail(MBX_E_INVALID, "bitmap_cnf: conj_offsets not ascending");
+    C->conj_off[i] = conj_offsets[i];
+  }
+  for (int32_t k = 0; k < nb; k++) {
+    if (!bms[k]) return fail(MBX_E_INVALID, "bitmap_cnf: bms[%d] null", k);
+    if (bms[k]->nbits != nbits) return fail(MBX_E_INVALID, "bitmap_cnf: bms[%d] has %lld bits, want %lld", k,
+                                            (long long)bms[k]->nbits, (long long)nbits);
+    C->bms[k] = bms[k]->words;
+  }
+  if (deleted && deleted->nbits != nbits) return fail(MBX_E_INVALID, "bitmap_cnf: deleted bitmap size");
+  return MBX_OK;
+}
+
+extern "C" int mbx_bitmap_cnf(mbx_ctx* c, int64_t nbits, const mbx_bitmap* const* bms, const int32_t* conj_offsets,
+                              int32_t nconj, const mbx_bitmap* deleted, mbx_bitmap** out, int64_t* count) {
+  NOTNULL(c);
+  NOTNULL(out);
+  *out = nullptr;
+  BitmapCnf C;
+  int rc = cnf_args(nbits, bms, conj_offsets, nconj, deleted, &C);
+  if (rc) return rc;
+  if ((rc = set_device(c))) return rc;
+  mbx_bitmap* r = nullptr;
+  if ((rc = bitmap_new(c, nbits, &r))) return rc;
+  hipError_t e = launch_bitmap_cnf(C, deleted ? deleted->words : nullptr, r->nwords, r->nbits, r->wpb, r->words,
+                                   r->segs, c->stream);
+  if (e != hipSuccess) {
+    mbx_bitmap_free(r);
+    return fail(MBX_E_DEVICE, "bitmap_cnf: %s", hipGetErrorString(e));
+  }
+  if ((rc = bitmap_count_sync(c, r, false))) {
+    mbx_bitmap_free(r);
+    return rc;
+  }
+  if (count) *count = r->count;
+  *out = r;
+  return MBX_OK;
+}
+
+extern "C" int mbx_bitmap_cnf_async(mbx_ctx* c, const mbx_bitmap* const* bms, const int32_t* conj_offsets,
+                                    int32_t nconj, const mbx_bitmap* deleted, mbx_bitmap* out) {
+  NOTNULL(c);
+  NOTNULL(out);
+  BitmapCnf C;
+  int rc = cnf_args(out->nbits, bms, conj_offsets, nconj, deleted, &C);
+  if (rc) return rc;
+  out->count = -1;
+  HIPCHK(launch_bitmap_cnf(C, deleted ? deleted->words : nullptr, out->nwords, out->nbits, out->wpb, out->words,
+                           out->segs, c->stream));
+  return MBX_OK;
+}
+
+extern "C" int mbx_bitmap_index_build(mbx_ctx* c, const mbx_table* t, int32_t col, const mbx_operand* values,
+                                      int32_t nvalues, mbx_bitmap** out) {
+  NOTNULL(c);
+  NOTNULL(t);
+  NOTNULL(out);
+  if (nvalues <= 0) return fail(MBX_E_INVALID, "index_build: nvalues %d", nvalues);
+  NOTNULL(values);
+  if (col < 0 || col >= (int32_t)t->cols.size()) return fail(MBX_E_RANGE, "index_build: column %d", col);
+  const TCol& tc = t->cols[(size_t)col];
+  int rc = set_device(c);
+  if (rc) return rc;
+  const int32_t vw = tc.attr_type == MBX_ATTR_STRING ? tc.stride_w : 1;
+  std::vector<uint32_t> vals((size_t)nvalues * (size_t)vw, 0u);
+  for (int32_t v = 0; v < nvalues; v++) {
+    const mbx_operand& o = values[v];
+    if (o.type != tc.attr_type) return fail(MBX_E_TYPE, "index_build: value %d has AttrType %d, column %d", v, o.type,
+                                            tc.attr_type);
+    if (o.type == MBX_ATTR_INTEGER) {
+      memcpy(&vals[(size_t)v], &o.integer, 4);
+    } else if (o.type == MBX_ATTR_REAL) {
+      memcpy(&vals[(size_t)v], &o.real, 4);
+    } else {
+      if (o.string_len > tc.size) {
+        // longer than any value the column can hold: the bitmap stays empty
+        vals[(size_t)v * vw] = 0xFFFFFFFFu;  // never equal: 0xFF is not valid modified UTF-8
+        continue;
+      }
+      encode_device_string((const uint8_t*)o.string, o.string_len, (uint8_t*)&vals[(size_t)v * vw], vw * 4);
+    }
+  }
+  for (int32_t v = 0; v < nvalues; v++) out[v] = nullptr;
+  uint32_t* dvals = nullptr;
+  HIPCHK(hipMalloc(&dvals, vals.size() * 4));
+  hipError_t e = hipMemcpy(dvals, vals.data(), vals.size() * 4, hipMemcpyHostToDevice);
+  std::vector<uint64_t*> outs((size_t)nvalues);
+  for (int32_t v = 0; v < nvalues && e == hipSuccess && !rc; v++) {
+    rc = bitmap_new(c, t->nrows, &out[v]);
+    if (!rc) outs[(size_t)v] = out[v]->words;
+  }
+  if (!rc && e == hipSuccess && t->nrows > 0) {
+    KCol kc;
+    kc.base = tc.dev;
+    kc.kind = col_kind(tc.attr_type);
+    kc.stride_w = tc.stride_w;
+    e = launch_index_build(kc, t->nrows, dvals, nvalues, vw, outs.data(), out[0]->wpb, c->stream);
+    for (int32_t v = 0; v < nvalues && e == hipSuccess; v++)
+      e = launch_seg_popcount(out[v]->words, out[v]->nwords, out[v]->wpb, out[v]->segs, c->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(dvals);
+  if (!rc && e != hipSuccess) rc = fail(MBX_E_DEVICE, "index_build: %s", hipGetErrorString(e));
+  for (int32_t v = 0; v < nvalues && !rc; v++) rc = bitmap_count_sync(c, out[v], false);
+  if (rc) {
+    for (int32_t v = 0; v < nvalues; v++) {
+      mbx_bitmap_free(out[v]);
+      out[v] = nullptr;
+    }
+  }
+  return rc;
+}
+
+// ---------------------------------------------------- late materialisation
+
+static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel, const int32_t* proj,
+                           int32_t nproj, int64_t row_offset, int64_t* dev_ids, void* const* dev_out,
+                           int64_t* dev_total) {
+  if (nproj < 0 || nproj > kMaxProj) return fail(MBX_E_UNSUPPORTED, "materialize: %d columns (max %d)", nproj,
+                                                 kMaxProj);
+  ProjCol pc[kMaxProj];
+  for (int32_t j = 0; j < nproj; j++) {
+    if (!t) return fail(MBX_E_INVALID, "materialize: projection without a table");
+    if (proj[j] < 0 || proj[j] >= (int32_t)t->cols.size())
+      return fail(MBX_E_RANGE, "materialize: column %d outside 0..%zu", proj[j], t->cols.size() - 1);
+    pc[j].base = t->cols[(size_t)proj[j]].dev;
+    pc[j].stride_w = t->cols[(size_t)proj[j]].stride_w;
+    pc[j].pad_ = 0;
+  }
+  if (t && sel->nbits != t->nrows) return fail(MBX_E_INVALID, "materialize: bitmap/table size mismatch");
+  HIPCHK(launch_seg_scan(sel->segs, sel->nseg, sel->seg_off, dev_total, c->stream));
+  if (sel->nwords > 0)
+    HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->seg_off, row_offset, dev_ids, pc, dev_out, nproj,
+                              c->stream));
+  return MBX_OK;
+}
+
+static int64_t col_bytes(const mbx_table* t, int32_t j) {
+  const TCol& tc = t->cols[(size_t)j];
+  return (int64_t)tc.stride_w * 4;
+}
+
+static int ensure_count(mbx_ctx* c, mbx_bitmap* b) {
+  if (b->count >= 0) return MBX_OK;
+  return bitmap_count_sync(c, b, false);
+}
+
+// device rows (stride) -> caller layout (size bytes, modified UTF-8)
+static void unpack_rows(const TCol& tc, const uint8_t* dev_img, int64_t n, void* host_out) {
+  if (tc.attr_type != MBX_ATTR_STRING) {
+    memcpy(host_out, dev_img, (size_t)n * 4);
+    return;
+  }
+  const int32_t stride = tc.stride_w * 4;
+  for (int64_t r = 0; r < n; r++)
+    decode_device_string(dev_img + (size_t)r * stride, stride, (uint8_t*)host_out + (size_t)r * tc.size, tc.size);
+}
+
+extern "C" int mbx_cursor_open(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* selc, const int32_t* proj,
+                               int32_t nproj, mbx_cursor** out) {
+  NOTNULL(c);
+  NOTNULL(selc);
+  NOTNULL(out);
+  *out = nullptr;
+  if (nproj > 0) {
+    NOTNULL(t);
+    NOTNULL(proj);
+  }
+  mbx_bitmap* sel = const_cast<mbx_bitmap*>(selc);
+  int rc = set_device(c);
+  if (rc) return rc;
+  if ((rc = ensure_count(c, sel))) return rc;
+  mbx_cursor* k = new (std::nothrow) mbx_cursor();
+  if (!k) return fail(MBX_E_NOMEM, "cursor: host allocation");
+  k->ctx = c;
+  k->t = t;
+  k->count = sel->count;
+  const size_t n = (size_t)(k->count > 0 ? k->count : 1);
+  hipError_t e = hipMalloc(&k->ids, n * sizeof(int64_t));
+  for (int32_t j = 0; j < nproj && e == hipSuccess; j++) {
+    if (proj[j] < 0 || proj[j] >= (int32_t)t->cols.size()) {
+      mbx_cursor_close(k);
+      return fail(MBX_E_RANGE, "cursor: column %d", proj[j]);
+    }
+    void* d = nullptr;
+    e = hipMalloc(&d, n * (size_t)col_bytes(t, proj[j]));
+    k->outs.push_back(d);
+    k->proj.push_back(proj[j]);
+  }
+  if (e != hipSuccess) {
+    mbx_cursor_close(k);
+    return fail(MBX_E_NOMEM, "cursor: %s", hipGetErrorString(e));
+  }
+  rc = materialize_dev(c, t, sel, proj, nproj, t ? t->row_offset : 0, k->ids, k->outs.data(), c->dcount);
+  if (!rc) {
+    hipError_t e2 = hipStreamSynchronize(c->stream);
+    if (e2 != hipSuccess) rc = fail(MBX_E_DEVICE, "cursor: %s", hipGetErrorString(e2));
+  }
+  if (rc) {
+    mbx_cursor_close(k);
+    return rc;
+  }
+  *out = k;
+  return MBX_OK;
+}
+
+extern "C" int mbx_cursor_count(const mbx_cursor* k, int64_t* count) {
+  NOTNULL(k);
+  NOTNULL(count);
+  *count = k->count;
+  return MBX_OK;
+}
+
+extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_ids, void* const* host_out,
+                               int64_t* n) {
+  NOTNULL(k);
+  NOTNULL(n);
+  *n = 0;
+  if (max_rows <= 0) return fail(MBX_E_INVALID, "cursor_next: max_rows %lld", (long long)max_rows);
+  const int64_t take = k->count - k->next < max_rows ? k->count - k->next : max_rows;
+  if (take <= 0) return MBX_OK;  // end of stream: get_next() returns null
+  mbx_ctx* c = k->ctx;
+  int rc = set_device(c);
+  if (rc) return rc;
+  const mbx_table* t = k->t;
+  if (host_ids)
+    HIPCHK(hipMemcpyAsync(host_ids, k->ids + k->next, (size_t)take * sizeof(int64_t), hipMemcpyDeviceToHost,
+                          c->stream));
+  std::vector<std::vector<uint8_t>> imgs(k->outs.size());
+  for (size_t j = 0; j < k->outs.size(); j++) {
+    if (!host_out || !host_out[j]) continue;
+    const TCol& tc = t->cols[(size_t)k->proj[j]];
+    const int64_t w = (int64_t)tc.stride_w * 4;
+    if (tc.attr_type == MBX_ATTR_STRING) {
+      imgs[j].resize((size_t)(take * w));
+      HIPCHK(hipMemcpyAsync(imgs[j].data(), (uint8_t*)k->outs[j] + k->next * w, (size_t)(take * w),
+                            hipMemcpyDeviceToHost, c->stream));
+    } else {
+      HIPCHK(hipMemcpyAsync(host_out[j], (uint8_t*)k->outs[j] + k->next * w, (size_t)(take * w),
+                            hipMemcpyDeviceToHost, c->stream));
+    }
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (size_t j = 0; j < k->outs.size(); j++) {
+    if (!host_out || !host_out[j]) continue;
+    const TCol& tc = t->cols[(size_t)k->proj[j]];
+    if (tc.attr_type == MBX_ATTR_STRING) unpack_rows(tc, imgs[j].data(), take, host_out[j]);
+  }
+  k->next += take;
+  *n = take;
+  return MBX_OK;
+}
+
+extern "C" int mbx_cursor_restart(mbx_cursor* k) {
+  NOTNULL(k);
+  k->next = 0;
+  return MBX_OK;
+}
+
+extern "C" int mbx_cursor_close(mbx_cursor* k) {
+  if (!k) return MBX_OK;
+  hipSetDevice(k->ctx->device);
+  hipStreamSynchronize(k->ctx->stream);
+  hipFree(k->ids);
+  for (void* d : k->outs) hipFree(d);
+  delete k;
+  return MBX_OK;
+}
+
+extern "C" int mbx_bitmap_select(mbx_ctx* c, const mbx_bitmap* b, int64_t row_offset, int64_t* host_ids, int64_t cap,
+                                 int64_t* n) {
+  NOTNULL(c);
+  NOTNULL(b);
+  NOTNULL(n);
+  *n = 0;
+  mbx_bitmap* sel = const_cast<mbx_bitmap*>(b);
+  int rc = set_device(c);
+  if (rc) return rc;
+  if ((rc = ensure_count(c, sel))) return rc;
+  if (sel->count > cap) return fail(MBX_E_INVALID, "bitmap_select: %lld ids, capacity %lld", (long long)sel->count,
+                                    (long long)cap);
+  if (sel->count == 0) return MBX_OK;
+  NOTNULL(host_ids);
+  int64_t* d = nullptr;
+  HIPCHK(hipMalloc(&d, (size_t)sel->count * sizeof(int64_t)));
+  rc = materialize_dev(c, nullptr, sel, nullptr, 0, row_offset, d, nullptr, c->dcount);
+  hipError_t e = hipSuccess;
+  if (!rc) e = hipMemcpyAsync(host_ids, d, (size_t)sel->count * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
+  if (!rc && e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  hipFree(d);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(MBX_E_DEVICE, "bitmap_select: %s", hipGetErrorString(e));
+  *n = sel->count;
+  return MBX_OK;
+}
+
+extern "C" int mbx_materialize(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel, const int32_t* proj,
+                               int32_t nproj, int64_t* host_ids, void* const* host_out, int64_t cap, int64_t* n) {
+  NOTNULL(c);
+  NOTNULL(t);
+  NOTNULL(sel);
+  NOTNULL(n);
+  *n = 0;
+  mbx_cursor* k = nullptr;
+  int rc = mbx_cursor_open(c, t, sel, proj, nproj, &k);
+  if (rc) return rc;
+  if (k->count > cap) {
+    mbx_cursor_close(k);
+    return fail(MBX_E_INVALID, "materialize: %lld rows, capacity %lld", (long long)k->count, (long long)cap);
+  }
+  if (k->count > 0) rc = mbx_cursor_next(k, k->count, host_ids, host_out, n);
+  mbx_cursor_close(k);
+  return rc;
+}
+
+extern "C" int mbx_materialize_async(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel, const int32_t* proj,
+                                     int32_t nproj, int64_t* dev_ids, void* const* dev_out, int64_t* dev_count) {
+  NOTNULL(c);
+  NOTNULL(t);
+  NOTNULL(sel);
+  if (nproj > 0) {
+    NOTNULL(proj);
+    NOTNULL(dev_out);
+  }
+  return materialize_dev(c, t, sel, proj, nproj, t->row_offset, dev_ids, dev_out, dev_count);
+}

@@ -1,0 +1,148 @@
+// mbx_internal.hpp -- device-side plan layout and kernel launchers shared by
+// the C-ABI layer (mbx_api.cpp) and the CDNA4 kernels (mbx_kernels.hip).
+//
+// HBM layout (DESIGN.md "Data layout"):
+//   * int32 / float32 column: nrows contiguous 4-byte values, position order.
+//   * char(n) column: nrows rows of `stride` bytes (n rounded up to 4), the
+//     modified-UTF-8 payload with C0 80 (U+0000) rewritten to 00 01 and zero
+//     padding, so that an unsigned big-endian word compare of two rows equals
+//     the sign of Java String.compareTo (TupleUtils.java:79-82).
+//   * bitmaps: java.util.BitSet words (bit p%64 of uint64 word p/64).
+// Work decomposition: a "tile" is 256 rows = 4 bitmap words = one wave of 64
+// lanes x 4 consecutive rows (one 16-byte load per lane per 4-byte column).
+// A block (4 waves) owns a contiguous "segment" of tiles; per-segment counts
+// feed the compaction scan, so every producer of a bitmap also reports them.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mbx {
+
+constexpr int kTileRows = 256;       // rows per wave tile
+constexpr int kWordsPerTile = 4;     // bitmap words per tile
+constexpr int kBlock = 256;          // threads per block (4 waves)
+constexpr int kWaves = kBlock / 64;
+constexpr int kMaxTerms = 32;
+constexpr int kMaxCols = 8;
+constexpr int kMaxStrWords = 64;     // 256-byte strings
+constexpr int kMaxPoolWords = 512;
+constexpr int kMaxBitmaps = 64;      // bitmaps in one CNF launch
+constexpr int kMaxProj = 16;
+
+enum ColKind : int32_t { kInt = 0, kReal = 1, kStr = 2 };
+
+// normalized comparison: the kernel evaluates `lhs_col OP rhs` where rhs is a
+// literal or another column; literal-on-left terms are flipped on the host.
+enum CmpOp : int32_t { kLT = 0, kLE = 1, kGT = 2, kGE = 3, kEQ = 4, kNE = 5 };
+
+struct KCol {
+  const void* base;
+  int32_t kind;      // ColKind
+  int32_t stride_w;  // 32-bit words per row (1 for int/real)
+};
+
+struct KTerm {
+  int32_t kind;      // comparison type (ColKind)
+  int32_t op;        // CmpOp
+  int32_t lhs;       // column slot
+  int32_t rhs;       // column slot, or -1 for a literal
+  uint32_t conj_bit; // 1u << conjunct
+  int32_t ilit;
+  float flit;
+  int32_t soff;      // string literal: word offset in the pool
+  int32_t swords;    // string literal: words
+};
+
+// The compiled predicate (PredEval over one CNF) + optional aggregate column.
+// Lives in device memory; kernels read it with uniform (scalar) loads.
+struct KPlan {
+  int32_t ncols;
+  int32_t nterms;
+  uint32_t all_conj;  // every conjunct bit that must be set (0: no filter)
+  int32_t agg_slot;   // -1: none
+  int32_t has_real;   // any float comparison (NaN detection)
+  int32_t pad_;
+  KCol cols[kMaxCols];
+  KTerm terms[kMaxTerms];
+  uint32_t pool[kMaxPoolWords];
+};
+
+// per-block partial result of a scan (deterministic finalize, no atomics)
+struct Partial {
+  int64_t count;
+  int64_t isum;
+  double fsum;
+  int32_t imin, imax;
+  float fmin, fmax;
+  int32_t nan_seen;
+  int32_t pad_;
+};
+
+// mirrors mbx_agg (include/mbx.h) field for field
+struct AggOut {
+  int64_t count;
+  int32_t agg_type;
+  int32_t pad_;
+  int64_t isum;
+  int32_t imin, imax;
+  double fsum;
+  float fmin, fmax;
+};
+
+// per-segment counts live in the `count` field of a Partial array
+constexpr int kSegStride = (int)(sizeof(Partial) / sizeof(int64_t));
+
+enum ScanMode : int32_t { kModeCount = 0, kModeBitmap = 1, kModeAgg = 2 };
+
+struct ScanLaunch {
+  const KPlan* plan;          // device
+  int64_t nrows;
+  int64_t tiles_per_block;    // segment = tiles_per_block tiles
+  const uint64_t* deleted;    // device or null
+  uint64_t* out_words;        // device or null
+  Partial* partials;          // device, one per block
+  int32_t mode;
+  int32_t fast_k;             // >0: fast kernel over K 4-byte slots; 0: generic
+  int32_t agg_kind;           // kInt / kReal when mode == kModeAgg
+  // in-launch finalize: the last block to arrive on `ticket` reduces all
+  // partials in block order (release/acquire hand-off, zeroed by that block)
+  uint32_t* ticket;           // device, 0 before the launch; null: no finalize
+  int64_t* count_out;         // device or null
+  AggOut* agg_out;            // device or null
+  int32_t* nan_out;           // device or null
+};
+
+struct ProjCol {
+  const void* base;
+  int32_t stride_w;
+  int32_t pad_;
+};
+
+struct BitmapCnf {
+  const uint64_t* bms[kMaxBitmaps];
+  int32_t conj_off[33];
+  int32_t nconj;
+};
+
+int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block);
+int64_t choose_tiles_per_block(int64_t nrows);
+
+hipError_t launch_scan(const ScanLaunch& L, hipStream_t s);
+hipError_t launch_finalize(const Partial* partials, int64_t nblocks, int32_t agg_kind, AggOut* out,
+                           int64_t* count_out, int32_t* nan_flag, hipStream_t s);
+hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
+                             int64_t words_per_block, uint64_t* out, Partial* seg_parts, hipStream_t s);
+hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* b, int64_t nwords,
+                                 int64_t nbits, int64_t words_per_block, uint64_t* out, Partial* seg_parts,
+                                 hipStream_t s);
+hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t words_per_block,
+                               Partial* seg_parts, hipStream_t s);
+hipError_t launch_seg_scan(const Partial* seg_parts, int64_t nseg, int64_t* seg_offsets, int64_t* total,
+                           hipStream_t s);
+hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
+                              const int64_t* seg_offsets, int64_t row_offset, int64_t* ids,
+                              const ProjCol* proj, void* const* out, int32_t nproj, hipStream_t s);
+hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint32_t* values, int32_t nvalues,
+                              int32_t value_words, uint64_t* const* outs, int64_t words_per_block, hipStream_t s);
+
+}  // namespace mbx

@@ -1,0 +1,805 @@
+// mbx_kernels.hip -- CDNA4 (gfx950) kernels of the columnar scan path.
+//
+//   k_scan_fast      PredEval over 4-byte columns (ColumnarFileScan.get_next,
+//                    R/iterator/ColumnarFileScan.java:156-172): 16-byte loads,
+//                    4 rows per lane, 256-row wave tiles; COUNT / BitSet /
+//                    COUNT+SUM+MIN+MAX outputs.  HBM-read bound.
+//   k_scan_generic   same contract for any CNF (char(n) strings, column-vs-
+//                    column terms): one row per lane, the wave ballot is the
+//                    BitSet word.
+//   k_bitmap_cnf     ColumnarIndexScan OR/AND over index BitSets
+//                    (R/index/ColumnarIndexScan.java:130-181) AND NOT deleted.
+//   k_bitmap_combine BitSet.and / or / andNot.
+//   k_seg_popcount / k_seg_scan / k_materialize
+//                    nextSetBit compaction + late materialisation
+//                    (R/index/ColumnarIndexScan.java:287-308): per-segment
+//                    counts -> exclusive scan -> one wave per word run writes
+//                    ascending positions and the projected values.
+//   k_index_build    Columnarfile.createBitMapIndex (R/columnar/Columnarfile.java:698-753).
+//   k_finalize       deterministic fixed-order reduction of per-block partials.
+//
+// No atomics on the data path: every reduction is per block into a partial
+// slot, then a single-block pass in a fixed order (bit-reproducible sums).
+#include "mbx_internal.hpp"
+
+namespace mbx {
+
+// ----------------------------------------------------------------- helpers
+
+template <typename T>
+__device__ __forceinline__ bool cmp1(int op, T a, T b) {
+  switch (op) {
+    case kLT: return a < b;
+    case kLE: return a <= b;
+    case kGT: return a > b;
+    case kGE: return a >= b;
+    case kEQ: return a == b;
+    default: return a != b;
+  }
+}
+
+// one uniform switch, four rows
+template <typename T>
+__device__ __forceinline__ void cmp4(int op, const T (&a)[4], T b, bool (&r)[4]) {
+  switch (op) {
+    case kLT:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = a[j] < b;
+      break;
+    case kLE:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = a[j] <= b;
+      break;
+    case kGT:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = a[j] > b;
+      break;
+    case kGE:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = a[j] >= b;
+      break;
+    case kEQ:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = a[j] == b;
+      break;
+    default:
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = a[j] != b;
+      break;
+  }
+}
+
+// String.compareTo sign over the device string image: big-endian unsigned
+// word compare, missing words read as zero padding.
+__device__ __forceinline__ int str_cmp(const uint32_t* a, int aw, const uint32_t* b, int bw) {
+  const int n = aw > bw ? aw : bw;
+  for (int i = 0; i < n; ++i) {
+    const uint32_t x = i < aw ? __builtin_bswap32(a[i]) : 0u;
+    const uint32_t y = i < bw ? __builtin_bswap32(b[i]) : 0u;
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+struct Acc {
+  int64_t count;  // meaningful in lane 0 only (scalar ballot counts)
+  int64_t isum;
+  double fsum;
+  int32_t imin, imax;
+  float fmin, fmax;
+  int32_t nan;
+};
+
+__device__ __forceinline__ void acc_init(Acc& a) {
+  a.count = 0;
+  a.isum = 0;
+  a.fsum = 0.0;
+  a.imin = INT32_MAX;
+  a.imax = INT32_MIN;
+  a.fmin = __builtin_inff();
+  a.fmax = -__builtin_inff();
+  a.nan = 0;
+}
+
+__device__ __forceinline__ void acc_merge(Acc& a, const Acc& b) {
+  a.count += b.count;
+  a.isum += b.isum;
+  a.fsum += b.fsum;
+  a.imin = b.imin < a.imin ? b.imin : a.imin;
+  a.imax = b.imax > a.imax ? b.imax : a.imax;
+  a.fmin = b.fmin < a.fmin ? b.fmin : a.fmin;
+  a.fmax = b.fmax > a.fmax ? b.fmax : a.fmax;
+  a.nan |= b.nan;
+}
+
+__device__ __forceinline__ Acc shfl_xor_acc(const Acc& a, int m) {
+  Acc b;
+  b.count = __shfl_xor(a.count, m);
+  b.isum = __shfl_xor(a.isum, m);
+  b.fsum = __shfl_xor(a.fsum, m);
+  b.imin = __shfl_xor(a.imin, m);
+  b.imax = __shfl_xor(a.imax, m);
+  b.fmin = __shfl_xor(a.fmin, m);
+  b.fmax = __shfl_xor(a.fmax, m);
+  b.nan = __shfl_xor(a.nan, m);
+  return b;
+}
+
+__device__ __forceinline__ Acc from_partial(const Partial& p) {
+  Acc b;
+  b.count = p.count;
+  b.isum = p.isum;
+  b.fsum = p.fsum;
+  b.imin = p.imin;
+  b.imax = p.imax;
+  b.fmin = p.fmin;
+  b.fmax = p.fmax;
+  b.nan = p.nan_seen;
+  return b;
+}
+
+// Reduce n partials with one block in a fixed order (thread i folds i, i+256,
+// ... sequentially, then a fixed xor tree and wave order) and write the
+// results.  Bit-reproducible for a given grid.
+__device__ __forceinline__ void finalize_block(const Partial* parts, int64_t n, int32_t agg_kind, AggOut* out,
+                                               int64_t* count_out, int32_t* nan_flag) {
+  __shared__ Acc fsh[kWaves];
+  Acc a;
+  acc_init(a);
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) acc_merge(a, from_partial(parts[i]));
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    Acc b = shfl_xor_acc(a, m);
+    acc_merge(a, b);
+  }
+  if ((threadIdx.x & 63) == 0) fsh[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Acc r = fsh[0];
+    for (int w = 1; w < kWaves; ++w) acc_merge(r, fsh[w]);
+    if (out) {
+      AggOut o;
+      o.count = r.count;
+      o.agg_type = agg_kind == kReal ? 2 : 1;  // MBX_ATTR_REAL / MBX_ATTR_INTEGER
+      o.pad_ = 0;
+      o.isum = r.isum;
+      o.imin = r.imin;
+      o.imax = r.imax;
+      o.fsum = r.fsum;
+      o.fmin = r.fmin;
+      o.fmax = r.fmax;
+      *out = o;
+    }
+    if (count_out) *count_out = r.count;
+    if (nan_flag) *nan_flag = r.nan;
+  }
+}
+
+// Block-wide fixed-order reduction of per-thread accumulators into this
+// block's Partial; with a ticket, the last block to arrive then finalizes all
+// partials inside the same launch.  Hand-off (MI355X: per-XCD L2s are not
+// coherent): the storing thread drains its store, releases at agent scope and
+// takes a relaxed agent-scope ticket; the last arriver acquires at agent scope
+// before the whole block reads the partials with plain loads.
+template <bool FULL>
+__device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
+  __shared__ Acc sh[kWaves];
+  __shared__ int is_last;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  if (FULL) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      Acc b = shfl_xor_acc(a, m);
+      acc_merge(a, b);
+    }
+  } else {
+    int nn = a.nan;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) nn |= __shfl_xor(nn, m);
+    a.nan = nn;
+  }
+  if (lane == 0) sh[wave] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    Acc r = sh[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) acc_merge(r, sh[w]);
+    Partial p;
+    p.count = r.count;
+    p.isum = r.isum;
+    p.fsum = r.fsum;
+    p.imin = r.imin;
+    p.imax = r.imax;
+    p.fmin = r.fmin;
+    p.fmax = r.fmax;
+    p.nan_seen = r.nan;
+    p.pad_ = 0;
+    L.partials[blockIdx.x] = p;
+    if (L.ticket) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t = __hip_atomic_fetch_add(L.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      is_last = (t == gridDim.x - 1);
+      if (is_last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+  }
+  if (!L.ticket) return;
+  __syncthreads();
+  if (is_last) {
+    finalize_block(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
+    if (threadIdx.x == 0) __hip_atomic_store(L.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Pack the 4-row nibbles of 16 consecutive lanes into one BitSet word.
+// Lane l holds rows 4l..4l+3 of the tile; word k of the tile = lanes 16k..16k+15.
+__device__ __forceinline__ uint64_t pack_word16(uint32_t nib, int lane) {
+  uint32_t o = __shfl_xor(nib, 1);
+  uint32_t v8 = (lane & 1) ? (o | (nib << 4)) : (nib | (o << 4));
+  o = __shfl_xor(v8, 2);
+  uint32_t v16 = (lane & 2) ? (o | (v8 << 8)) : (v8 | (o << 8));
+  o = __shfl_xor(v16, 4);
+  uint32_t v32 = (lane & 4) ? (o | (v16 << 16)) : (v16 | (o << 16));
+  o = __shfl_xor(v32, 8);
+  return (lane & 8) ? (((uint64_t)v32 << 32) | o) : ((uint64_t)v32 | ((uint64_t)o << 32));
+}
+
+// ------------------------------------------------------------- fast scan
+//
+// K 4-byte columns in plan slots 0..K-1, every term `slot OP literal`.
+// Each wave streams whole 256-row tiles of its block's segment: one
+// global_load_dwordx4 per column per tile, terms folded into per-row
+// conjunct bitmasks (cb), the CNF holds when cb == all_conj.
+template <int K, int MODE, bool DEL>
+__global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
+  const KPlan* __restrict__ P = L.plan;
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  const int64_t nrows = L.nrows;
+  const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * L.tiles_per_block;
+  const int64_t t1 = min(t0 + L.tiles_per_block, ntiles);
+  const int nterms = P->nterms;
+  const uint32_t all = P->all_conj;
+  const int agg_slot = MODE == kModeAgg ? P->agg_slot : 0;
+  const bool agg_real = L.agg_kind == kReal;
+
+  const int32_t* colp[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) colp[s] = (const int32_t*)P->cols[s].base;
+
+  Acc acc;
+  acc_init(acc);
+  uint64_t wave_count = 0;
+
+  for (int64_t t = t0 + wave; t < t1; t += kWaves) {
+    const int64_t row0 = t * kTileRows + lane * 4;
+    int32_t v[K][4];
+    if ((t + 1) * kTileRows <= nrows) {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const int4 q = *reinterpret_cast<const int4*>(colp[s] + t * kTileRows + lane * 4);
+        v[s][0] = q.x;
+        v[s][1] = q.y;
+        v[s][2] = q.z;
+        v[s][3] = q.w;
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < K; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[s][j] = row0 + j < nrows ? colp[s][row0 + j] : 0;
+    }
+
+    uint32_t cb[4] = {0u, 0u, 0u, 0u};
+    for (int ti = 0; ti < nterms; ++ti) {
+      const KTerm& T = P->terms[ti];
+      const int lhs = T.lhs;
+      int32_t a[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = v[0][j];
+#pragma unroll
+      for (int s = 1; s < K; ++s)
+        if (lhs == s) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = v[s][j];
+        }
+      bool r[4];
+      if (T.kind == kInt) {
+        cmp4<int32_t>(T.op, a, T.ilit, r);
+      } else {
+        float f[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f[j] = __int_as_float(a[j]);
+          acc.nan |= (f[j] != f[j]) && (row0 + j < nrows);
+        }
+        cmp4<float>(T.op, f, T.flit, r);
+      }
+      const uint32_t bit = T.conj_bit;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cb[j] |= r[j] ? bit : 0u;
+    }
+
+    bool p[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = (cb[j] == all) && (row0 + j < nrows);
+    const int64_t word = t * kWordsPerTile + (lane >> 4);
+    if (DEL) {
+      const uint64_t dw = word < nwords ? L.deleted[word] : 0ull;
+      const uint32_t dn = (uint32_t)(dw >> ((lane & 15) * 4)) & 0xFu;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[j] = p[j] && !((dn >> j) & 1u);
+    }
+    if (MODE == kModeBitmap) {
+      const uint32_t nib = (uint32_t)p[0] | ((uint32_t)p[1] << 1) | ((uint32_t)p[2] << 2) | ((uint32_t)p[3] << 3);
+      const uint64_t w = pack_word16(nib, lane);
+      if ((lane & 15) == 0 && word < nwords) L.out_words[word] = w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wave_count += __popcll(__ballot(p[j]));
+    if (MODE == kModeAgg) {
+      int32_t g[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = v[0][j];
+#pragma unroll
+      for (int s = 1; s < K; ++s)
+        if (agg_slot == s) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[j] = v[s][j];
+        }
+      if (agg_real) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float f = __int_as_float(g[j]);
+          acc.fsum += p[j] ? (double)f : 0.0;
+          acc.fmin = p[j] && f < acc.fmin ? f : acc.fmin;
+          acc.fmax = p[j] && f > acc.fmax ? f : acc.fmax;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc.isum += p[j] ? (int64_t)g[j] : 0;
+          acc.imin = p[j] && g[j] < acc.imin ? g[j] : acc.imin;
+          acc.imax = p[j] && g[j] > acc.imax ? g[j] : acc.imax;
+        }
+      }
+    }
+  }
+  acc.count = lane == 0 ? (int64_t)wave_count : 0;
+  block_reduce_store<MODE == kModeAgg>(acc, L);
+}
+
+// ---------------------------------------------------------- generic scan
+//
+// Any CNF the host accepted: char(n) strings, column-vs-column terms, more
+// than 4 columns.  One row per lane; the ballot of a wave is one BitSet word.
+template <int MODE, bool DEL>
+__global__ __launch_bounds__(kBlock) void k_scan_generic(ScanLaunch L) {
+  const KPlan* __restrict__ P = L.plan;
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  const int64_t nrows = L.nrows;
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t w0 = (int64_t)blockIdx.x * L.tiles_per_block * kWordsPerTile;
+  const int64_t w1 = min(w0 + L.tiles_per_block * kWordsPerTile, nwords);
+  const int nterms = P->nterms;
+  const uint32_t all = P->all_conj;
+  const bool agg_real = L.agg_kind == kReal;
+
+  Acc acc;
+  acc_init(acc);
+  uint64_t wave_count = 0;
+
+  for (int64_t w = w0 + wave; w < w1; w += kWaves) {
+    const int64_t row = w * 64 + lane;
+    const bool valid = row < nrows;
+    uint32_t cb = 0;
+    for (int ti = 0; ti < nterms; ++ti) {
+      const KTerm& T = P->terms[ti];
+      bool r = false;
+      if (valid) {
+        const KCol& A = P->cols[T.lhs];
+        if (T.kind == kStr) {
+          const uint32_t* ap = (const uint32_t*)A.base + row * A.stride_w;
+          int c;
+          if (T.rhs >= 0) {
+            const KCol& B = P->cols[T.rhs];
+            c = str_cmp(ap, A.stride_w, (const uint32_t*)B.base + row * B.stride_w, B.stride_w);
+          } else {
+            c = str_cmp(ap, A.stride_w, P->pool + T.soff, T.swords);
+          }
+          r = cmp1<int>(T.op, c, 0);
+        } else if (T.kind == kInt) {
+          const int32_t a = ((const int32_t*)A.base)[row];
+          const int32_t b = T.rhs >= 0 ? ((const int32_t*)P->cols[T.rhs].base)[row] : T.ilit;
+          r = cmp1<int32_t>(T.op, a, b);
+        } else {
+          const float a = ((const float*)A.base)[row];
+          const float b = T.rhs >= 0 ? ((const float*)P->cols[T.rhs].base)[row] : T.flit;
+          acc.nan |= (a != a) || (b != b);
+          r = cmp1<float>(T.op, a, b);
+        }
+      }
+      cb |= r ? T.conj_bit : 0u;
+    }
+    bool p = valid && cb == all;
+    if (DEL) p = p && !((L.deleted[w] >> lane) & 1ull);
+    const uint64_t m = __ballot(p);
+    if (MODE == kModeBitmap && lane == 0) L.out_words[w] = m;
+    wave_count += __popcll(m);
+    if (MODE == kModeAgg && p) {
+      const KCol& G = P->cols[P->agg_slot];
+      if (agg_real) {
+        const float f = ((const float*)G.base)[row];
+        acc.fsum += (double)f;
+        acc.fmin = f < acc.fmin ? f : acc.fmin;
+        acc.fmax = f > acc.fmax ? f : acc.fmax;
+      } else {
+        const int32_t g = ((const int32_t*)G.base)[row];
+        acc.isum += g;
+        acc.imin = g < acc.imin ? g : acc.imin;
+        acc.imax = g > acc.imax ? g : acc.imax;
+      }
+    }
+  }
+  acc.count = lane == 0 ? (int64_t)wave_count : 0;
+  block_reduce_store<MODE == kModeAgg>(acc, L);
+}
+
+// --------------------------------------------------------------- finalize
+
+__global__ __launch_bounds__(kBlock) void k_finalize(const Partial* __restrict__ parts, int64_t n,
+                                                     int32_t agg_kind, AggOut* out, int64_t* count_out,
+                                                     int32_t* nan_flag) {
+  finalize_block(parts, n, agg_kind, out, count_out, nan_flag);
+}
+
+// ---------------------------------------------------------- bitmap kernels
+
+// result = AND_c OR_{k in c} bms[k], AND NOT deleted; two words per thread.
+__global__ __launch_bounds__(kBlock) void k_bitmap_cnf(BitmapCnf C, const uint64_t* __restrict__ del,
+                                                       int64_t nwords, uint64_t tail_mask,
+                                                       int64_t words_per_block, uint64_t* __restrict__ out,
+                                                       Partial* __restrict__ seg_parts) {
+  const int64_t w0 = (int64_t)blockIdx.x * words_per_block;
+  const int64_t w1 = min(w0 + words_per_block, nwords);
+  int64_t cnt = 0;
+  for (int64_t w = w0 + 2 * threadIdx.x; w < w1; w += 2 * kBlock) {
+    const bool two = w + 1 < w1;
+    uint64_t r0 = ~0ull, r1 = ~0ull;
+    for (int c = 0; c < C.nconj; ++c) {
+      uint64_t o0 = 0, o1 = 0;
+      for (int k = C.conj_off[c]; k < C.conj_off[c + 1]; ++k) {
+        const uint64_t* b = C.bms[k];
+        if (two && ((w & 1) == 0)) {
+          const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(b + w);
+          o0 |= q.x;
+          o1 |= q.y;
+        } else {
+          o0 |= b[w];
+          if (two) o1 |= b[w + 1];
+        }
+      }
+      r0 &= o0;
+      r1 &= o1;
+    }
+    if (del) {
+      r0 &= ~del[w];
+      if (two) r1 &= ~del[w + 1];
+    }
+    if (w == nwords - 1) r0 &= tail_mask;
+    if (two && w + 1 == nwords - 1) r1 &= tail_mask;
+    out[w] = r0;
+    cnt += __popcll(r0);
+    if (two) {
+      out[w + 1] = r1;
+      cnt += __popcll(r1);
+    }
+  }
+  // block sum of counts (fixed order)
+  __shared__ int64_t sh[kWaves];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) cnt += __shfl_xor(cnt, m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t s = 0;
+    for (int i = 0; i < kWaves; ++i) s += sh[i];
+    seg_parts[blockIdx.x].count = s;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_bitmap_combine(int32_t op, const uint64_t* __restrict__ a,
+                                                           const uint64_t* __restrict__ b, int64_t nwords,
+                                                           uint64_t tail_mask, int64_t words_per_block,
+                                                           uint64_t* __restrict__ out,
+                                                           Partial* __restrict__ seg_parts) {
+  const int64_t w0 = (int64_t)blockIdx.x * words_per_block;
+  const int64_t w1 = min(w0 + words_per_block, nwords);
+  int64_t cnt = 0;
+  for (int64_t w = w0 + threadIdx.x; w < w1; w += kBlock) {
+    uint64_t r = op == 0 ? (a[w] & b[w]) : (op == 1 ? (a[w] | b[w]) : (a[w] & ~b[w]));
+    if (w == nwords - 1) r &= tail_mask;
+    out[w] = r;
+    cnt += __popcll(r);
+  }
+  __shared__ int64_t sh[kWaves];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) cnt += __shfl_xor(cnt, m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t s = 0;
+    for (int i = 0; i < kWaves; ++i) s += sh[i];
+    seg_parts[blockIdx.x].count = s;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_seg_popcount(const uint64_t* __restrict__ words, int64_t nwords,
+                                                         int64_t words_per_block,
+                                                         Partial* __restrict__ seg_parts) {
+  const int64_t w0 = (int64_t)blockIdx.x * words_per_block;
+  const int64_t w1 = min(w0 + words_per_block, nwords);
+  int64_t cnt = 0;
+  for (int64_t w = w0 + threadIdx.x; w < w1; w += kBlock) cnt += __popcll(words[w]);
+  __shared__ int64_t sh[kWaves];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) cnt += __shfl_xor(cnt, m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t s = 0;
+    for (int i = 0; i < kWaves; ++i) s += sh[i];
+    seg_parts[blockIdx.x].count = s;
+  }
+}
+
+// exclusive scan of the segment counts, one block of 1024 threads
+__global__ __launch_bounds__(1024) void k_seg_scan(const Partial* __restrict__ parts, int64_t n,
+                                                   int64_t* __restrict__ offsets, int64_t* total) {
+  __shared__ int64_t wsum[16];
+  __shared__ int64_t carry_sh;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry_sh = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t x = i < n ? parts[i].count : 0;
+    int64_t inc = x;  // inclusive wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t y = __shfl_up(inc, d);
+      if (lane >= d) inc += y;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    int64_t before = carry_sh;
+    for (int k = 0; k < wave; ++k) before += wsum[k];
+    if (i < n) offsets[i] = before + inc - x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t s = carry_sh;
+      for (int k = 0; k < 16; ++k) s += wsum[k];
+      carry_sh = s;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && total) *total = carry_sh;
+}
+
+// One block per segment; each wave owns a contiguous run of the segment's
+// words and walks it one word at a time with lane == bit: set lanes compute
+// their output slot with mbcnt (set bits below the lane), so positions and
+// projected values are written densely and in ascending order.
+struct MatArgs {
+  ProjCol proj[kMaxProj];
+  void* out[kMaxProj];
+  int32_t nproj;
+};
+
+__global__ __launch_bounds__(kBlock) void k_materialize(const uint64_t* __restrict__ words, int64_t nwords,
+                                                        int64_t words_per_block,
+                                                        const int64_t* __restrict__ seg_offsets,
+                                                        int64_t row_offset, int64_t* __restrict__ ids,
+                                                        MatArgs M) {
+  __shared__ int64_t wcount[kWaves];
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
+  const int64_t s1 = min(s0 + words_per_block, nwords);
+  const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
+  const int64_t a0 = min(s0 + wave * per, s1);
+  const int64_t a1 = min(a0 + per, s1);
+  int64_t c = 0;
+  for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(words[w]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+  if (lane == 0) wcount[wave] = c;
+  __syncthreads();
+  int64_t off = seg_offsets[blockIdx.x];
+  for (int k = 0; k < wave; ++k) off += wcount[k];
+  for (int64_t w = a0; w < a1; ++w) {
+    const uint64_t m = words[w];
+    if (m == 0) continue;
+    const bool bit = (m >> lane) & 1ull;
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (bit) {
+      const int64_t pos = off + below;
+      const int64_t row = w * 64 + lane;
+      if (ids) ids[pos] = row_offset + row;
+      for (int j = 0; j < M.nproj; ++j) {
+        const int sw = M.proj[j].stride_w;
+        const uint32_t* src = (const uint32_t*)M.proj[j].base + row * sw;
+        uint32_t* dst = (uint32_t*)M.out[j] + pos * sw;
+        for (int k = 0; k < sw; ++k) dst[k] = src[k];
+      }
+    }
+    off += __popcll(m);
+  }
+}
+
+// One pass over a column building the BitSet of each listed value.
+struct IndexArgs {
+  uint64_t* out[64];
+};
+
+__global__ __launch_bounds__(kBlock) void k_index_build(KCol col, int64_t nrows, const uint32_t* __restrict__ vals,
+                                                        int32_t nvalues, int32_t vwords, IndexArgs A,
+                                                        int64_t words_per_block) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t w0 = (int64_t)blockIdx.x * words_per_block;
+  const int64_t w1 = min(w0 + words_per_block, nwords);
+  for (int64_t w = w0 + wave; w < w1; w += kWaves) {
+    const int64_t row = w * 64 + lane;
+    const bool valid = row < nrows;
+    uint32_t x0 = 0;
+    if (valid && col.kind != kStr) x0 = ((const uint32_t*)col.base)[row];
+    for (int v = 0; v < nvalues; ++v) {
+      bool eq = false;
+      if (valid) {
+        if (col.kind == kStr) {
+          eq = str_cmp((const uint32_t*)col.base + row * col.stride_w, col.stride_w, vals + v * vwords, vwords) == 0;
+        } else if (col.kind == kInt) {
+          eq = (int32_t)x0 == (int32_t)vals[v];
+        } else {
+          eq = __uint_as_float(x0) == __uint_as_float(vals[v]);
+        }
+      }
+      const uint64_t m = __ballot(eq);
+      if (lane == 0) A.out[v][w] = m;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+
+int64_t choose_tiles_per_block(int64_t nrows) {
+  const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+  // ~2048 blocks (8 per CU on 256 CUs) for large inputs, >= 4 tiles per block
+  int64_t tpb = (ntiles + 2047) / 2048;
+  return tpb < 4 ? 4 : tpb;
+}
+
+int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block) {
+  const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+  const int64_t g = (ntiles + tiles_per_block - 1) / tiles_per_block;
+  return g < 1 ? 1 : g;
+}
+
+template <int K, int MODE>
+static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
+  if (L.deleted)
+    hipLaunchKernelGGL((k_scan_fast<K, MODE, true>), grid, dim3(kBlock), 0, s, L);
+  else
+    hipLaunchKernelGGL((k_scan_fast<K, MODE, false>), grid, dim3(kBlock), 0, s, L);
+}
+
+template <int MODE>
+static void mode_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
+  switch (L.fast_k) {
+    case 1: fast_launch<1, MODE>(L, grid, s); break;
+    case 2: fast_launch<2, MODE>(L, grid, s); break;
+    case 3: fast_launch<3, MODE>(L, grid, s); break;
+    case 4: fast_launch<4, MODE>(L, grid, s); break;
+    default:
+      if (L.deleted)
+        hipLaunchKernelGGL((k_scan_generic<MODE, true>), grid, dim3(kBlock), 0, s, L);
+      else
+        hipLaunchKernelGGL((k_scan_generic<MODE, false>), grid, dim3(kBlock), 0, s, L);
+  }
+}
+
+hipError_t launch_scan(const ScanLaunch& L, hipStream_t s) {
+  const dim3 grid((unsigned)grid_blocks(L.nrows, L.tiles_per_block));
+  switch (L.mode) {
+    case kModeCount: mode_launch<kModeCount>(L, grid, s); break;
+    case kModeBitmap: mode_launch<kModeBitmap>(L, grid, s); break;
+    default: mode_launch<kModeAgg>(L, grid, s); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize(const Partial* partials, int64_t nblocks, int32_t agg_kind, AggOut* out,
+                           int64_t* count_out, int32_t* nan_flag, hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, s, partials, nblocks, agg_kind, out, count_out,
+                     nan_flag);
+  return hipGetLastError();
+}
+
+static uint64_t tail_mask_of(int64_t nbits) {
+  const int r = (int)(nbits & 63);
+  return r == 0 ? ~0ull : ((1ull << r) - 1ull);
+}
+
+hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
+                             int64_t words_per_block, uint64_t* out, Partial* seg_parts, hipStream_t s) {
+  const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
+  hipLaunchKernelGGL(k_bitmap_cnf, dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,
+                     tail_mask_of(nbits), words_per_block, out, seg_parts);
+  return hipGetLastError();
+}
+
+hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* b, int64_t nwords, int64_t nbits,
+                                 int64_t words_per_block, uint64_t* out, Partial* seg_parts, hipStream_t s) {
+  const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
+  hipLaunchKernelGGL(k_bitmap_combine, dim3((unsigned)g), dim3(kBlock), 0, s, op, a, b, nwords,
+                     tail_mask_of(nbits), words_per_block, out, seg_parts);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t words_per_block, Partial* seg_parts,
+                               hipStream_t s) {
+  const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
+  hipLaunchKernelGGL(k_seg_popcount, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
+                     seg_parts);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_scan(const Partial* seg_parts, int64_t nseg, int64_t* seg_offsets, int64_t* total,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(1024), 0, s, seg_parts, nseg, seg_offsets, total);
+  return hipGetLastError();
+}
+
+hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
+                              const int64_t* seg_offsets, int64_t row_offset, int64_t* ids, const ProjCol* proj,
+                              void* const* out, int32_t nproj, hipStream_t s) {
+  MatArgs M;
+  M.nproj = nproj;
+  for (int j = 0; j < nproj && j < kMaxProj; ++j) {
+    M.proj[j] = proj[j];
+    M.out[j] = out[j];
+  }
+  const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
+  hipLaunchKernelGGL(k_materialize, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
+                     seg_offsets, row_offset, ids, M);
+  return hipGetLastError();
+}
+
+hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint32_t* values, int32_t nvalues,
+                              int32_t value_words, uint64_t* const* outs, int64_t words_per_block, hipStream_t s) {
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
+  for (int32_t v0 = 0; v0 < nvalues; v0 += 64) {
+    IndexArgs A;
+    const int32_t nv = nvalues - v0 < 64 ? nvalues - v0 : 64;
+    for (int i = 0; i < nv; ++i) A.out[i] = outs[v0 + i];
+    hipLaunchKernelGGL(k_index_build, dim3((unsigned)g), dim3(kBlock), 0, s, col, nrows,
+                       values + (int64_t)v0 * value_words, nv, value_words, A, words_per_block);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mbx

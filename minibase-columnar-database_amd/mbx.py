@@ -1,0 +1,461 @@
+"""ctypes binding of libmbx.so (include/mbx.h) -- the GPU executor's C-ABI.
+
+This is how Python callers (tests, bench.py) drive the HIP path; it is a thin
+marshalling layer with no compute of its own.  If libmbx.so is missing, or no
+MI355X is visible, the calls raise: there is no CPU fallback anywhere.
+
+CNF spec accepted by Context.compile (the flattened CondExpr[] of the reference):
+    cnf = [conjunct, ...]                      # AND (CondExpr[] array)
+    conjunct = [term, ...]                     # OR (.next chain)
+    term = (op, operand1, operand2[, index_type])
+    operand = ('sym', fld) | ('int', v) | ('real', v) | ('str', text_or_mutf8_bytes)
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmbx.so")
+
+# include/mbx.h constants
+STRING, INTEGER, REAL, SYMBOL = 0, 1, 2, 3
+EQ, LT, GT, NE, LE, GE, NOT, NOP, RANGE = range(9)
+IDX_NONE, IDX_BTREE, IDX_HASH, IDX_BITMAP = range(4)
+BM_AND, BM_OR, BM_ANDNOT = range(3)
+E_INVALID, E_TYPE, E_RANGE, E_DEVICE, E_NOMEM, E_UNSUPPORTED = -1, -2, -3, -4, -5, -6
+
+
+class MbxError(RuntimeError):
+    """A negative status from the C-ABI; .code is the MBX_E_* value."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"mbx error {code}: {msg}")
+        self.code = code
+
+
+class ColDesc(ctypes.Structure):
+    _fields_ = [("attr_type", ctypes.c_int32), ("size", ctypes.c_int32)]
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("fld", ctypes.c_int32), ("integer", ctypes.c_int32),
+                ("real", ctypes.c_float), ("string", ctypes.c_char_p), ("string_len", ctypes.c_int32)]
+
+
+class CondExprC(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("operand1", Operand), ("operand2", Operand),
+                ("index_type", ctypes.c_int32)]
+
+
+class Cnf(ctypes.Structure):
+    _fields_ = [("conds", ctypes.POINTER(CondExprC)), ("conj_offsets", ctypes.POINTER(ctypes.c_int32)),
+                ("nconj", ctypes.c_int32)]
+
+
+class Agg(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int64), ("agg_type", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("isum", ctypes.c_int64), ("imin", ctypes.c_int32), ("imax", ctypes.c_int32),
+                ("fsum", ctypes.c_double), ("fmin", ctypes.c_float), ("fmax", ctypes.c_float)]
+
+
+def java_mutf8(s):
+    """DataOutputStream.writeUTF payload bytes of a str (modified UTF-8)."""
+    if isinstance(s, (bytes, bytearray)):
+        return bytes(s)
+    units = s.encode("utf-16-be", "surrogatepass")
+    out = bytearray()
+    for i in range(0, len(units), 2):
+        cu = (units[i] << 8) | units[i + 1]
+        if 0 < cu < 0x80:
+            out.append(cu)
+        elif cu < 0x800:
+            out += bytes([0xC0 | (cu >> 6), 0x80 | (cu & 0x3F)])
+        else:
+            out += bytes([0xE0 | (cu >> 12), 0x80 | ((cu >> 6) & 0x3F), 0x80 | (cu & 0x3F)])
+    return bytes(out)
+
+
+EXPORTS = [
+    "mbx_abi_version", "mbx_last_error", "mbx_device_count", "mbx_init", "mbx_free", "mbx_sync", "mbx_stream",
+    "mbx_table_stage", "mbx_table_wrap", "mbx_table_free", "mbx_table_info", "mbx_plan_compile", "mbx_plan_free",
+    "mbx_scan_count", "mbx_scan_count_async", "mbx_scan_bitmap", "mbx_scan_bitmap_async", "mbx_scan_aggregate",
+    "mbx_scan_aggregate_async", "mbx_bitmap_alloc", "mbx_bitmap_upload", "mbx_bitmap_download", "mbx_bitmap_info",
+    "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_bitmap_index_build",
+    "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
+    "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libmbx.so (built by `make -C minibase-columnar-database_amd/csrc`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MbxError(E_DEVICE, f"{LIB_PATH} missing: build it with __graft_entry__.build() "
+                                 "(the executor has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, V, I32, I64 = ctypes.POINTER, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    sig = {
+        "mbx_abi_version": ([], ctypes.c_int),
+        "mbx_last_error": ([], ctypes.c_char_p),
+        "mbx_device_count": ([P(I32)], ctypes.c_int),
+        "mbx_init": ([I32, P(V)], ctypes.c_int),
+        "mbx_free": ([V], ctypes.c_int),
+        "mbx_sync": ([V], ctypes.c_int),
+        "mbx_stream": ([V], V),
+        "mbx_table_stage": ([V, P(ColDesc), I32, I64, P(V), V, I64, P(V)], ctypes.c_int),
+        "mbx_table_wrap": ([V, P(ColDesc), I32, I64, P(V), V, I64, P(V)], ctypes.c_int),
+        "mbx_table_free": ([V], ctypes.c_int),
+        "mbx_table_info": ([V, P(I64), P(I64), P(I32)], ctypes.c_int),
+        "mbx_plan_compile": ([V, V, P(Cnf), P(V)], ctypes.c_int),
+        "mbx_plan_free": ([V], ctypes.c_int),
+        "mbx_scan_count": ([V, V, P(I64)], ctypes.c_int),
+        "mbx_scan_count_async": ([V, V, V], ctypes.c_int),
+        "mbx_scan_bitmap": ([V, V, P(V), P(I64)], ctypes.c_int),
+        "mbx_scan_bitmap_async": ([V, V, V], ctypes.c_int),
+        "mbx_scan_aggregate": ([V, V, I32, P(Agg)], ctypes.c_int),
+        "mbx_scan_aggregate_async": ([V, V, I32, V], ctypes.c_int),
+        "mbx_bitmap_alloc": ([V, I64, P(V)], ctypes.c_int),
+        "mbx_bitmap_upload": ([V, I64, V, P(V)], ctypes.c_int),
+        "mbx_bitmap_download": ([V, V, V, I64], ctypes.c_int),
+        "mbx_bitmap_info": ([V, P(I64), P(I64), P(I64)], ctypes.c_int),
+        "mbx_bitmap_free": ([V], ctypes.c_int),
+        "mbx_bitmap_combine": ([V, I32, V, V, P(V), P(I64)], ctypes.c_int),
+        "mbx_bitmap_cnf": ([V, I64, P(V), P(I32), I32, V, P(V), P(I64)], ctypes.c_int),
+        "mbx_bitmap_cnf_async": ([V, P(V), P(I32), I32, V, V], ctypes.c_int),
+        "mbx_bitmap_index_build": ([V, V, I32, P(Operand), I32, P(V)], ctypes.c_int),
+        "mbx_bitmap_select": ([V, V, I64, V, I64, P(I64)], ctypes.c_int),
+        "mbx_materialize": ([V, V, V, P(I32), I32, V, P(V), I64, P(I64)], ctypes.c_int),
+        "mbx_materialize_async": ([V, V, V, P(I32), I32, V, P(V), V], ctypes.c_int),
+        "mbx_cursor_open": ([V, V, V, P(I32), I32, P(V)], ctypes.c_int),
+        "mbx_cursor_count": ([V, P(I64)], ctypes.c_int),
+        "mbx_cursor_next": ([V, I64, V, P(V), P(I64)], ctypes.c_int),
+        "mbx_cursor_restart": ([V], ctypes.c_int),
+        "mbx_cursor_close": ([V], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _chk(rc):
+    if rc < 0:
+        raise MbxError(rc, lib().mbx_last_error().decode(errors="replace"))
+    return rc
+
+
+def device_count():
+    n = ctypes.c_int32(0)
+    rc = lib().mbx_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def _operand(spec, keep):
+    o = Operand()
+    kind, v = spec
+    if kind == "sym":
+        o.type, o.fld = SYMBOL, int(v)
+    elif kind == "int":
+        o.type, o.integer = INTEGER, int(v)
+    elif kind == "real":
+        o.type, o.real = REAL, float(v)
+    elif kind == "str":
+        b = java_mutf8(v)
+        keep.append(b)
+        o.type, o.string, o.string_len = STRING, b, len(b)
+    else:
+        raise ValueError(kind)
+    return o
+
+
+def make_cnf(cnf, keep):
+    c = Cnf()
+    if cnf is None:
+        c.nconj = 0
+        return c
+    terms = [t for conj in cnf for t in conj]
+    conds = (CondExprC * max(1, len(terms)))()
+    for i, term in enumerate(terms):
+        op, a, b = term[:3]
+        conds[i].op = op
+        conds[i].operand1 = _operand(a, keep)
+        conds[i].operand2 = _operand(b, keep)
+        conds[i].index_type = term[3] if len(term) > 3 else IDX_BITMAP
+    offs = (ctypes.c_int32 * (len(cnf) + 1))()
+    k = 0
+    for i, conj in enumerate(cnf):
+        offs[i] = k
+        k += len(conj)
+    offs[len(cnf)] = k
+    keep += [conds, offs]
+    c.conds = conds
+    c.conj_offsets = offs
+    c.nconj = len(cnf)
+    return c
+
+
+class Context:
+    """mbx_ctx: one GPU, one HIP stream."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_init(device, ctypes.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().mbx_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return lib().mbx_stream(self.h)
+
+    def sync(self):
+        _chk(lib().mbx_sync(self.h))
+
+    # -- tables ---------------------------------------------------------
+    def stage(self, columns, deleted_words=None, row_offset=0):
+        """columns: list of (attr_type, size, ndarray); strings as uint8 [n, size]."""
+        arrs, descs = [], (ColDesc * len(columns))()
+        nrows = None
+        for j, (t, size, a) in enumerate(columns):
+            if t == INTEGER:
+                a = np.ascontiguousarray(a, dtype=np.int32)
+                size = 4
+            elif t == REAL:
+                a = np.ascontiguousarray(a, dtype=np.float32)
+                size = 4
+            else:
+                a = np.ascontiguousarray(a, dtype=np.uint8).reshape(-1, size)
+            descs[j].attr_type, descs[j].size = t, size
+            arrs.append(a)
+            nrows = a.shape[0] if nrows is None else nrows
+        ptrs = (ctypes.c_void_p * len(columns))(*[a.ctypes.data for a in arrs])
+        dw = None if deleted_words is None else np.ascontiguousarray(deleted_words, dtype=np.uint64)
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_table_stage(self.h, descs, len(columns), nrows, ptrs,
+                                   None if dw is None else dw.ctypes.data, row_offset, ctypes.byref(h)))
+        return Table(self, h, nrows, [(t, s) for t, s, _ in columns], row_offset)
+
+    def wrap(self, col_descs, dev_ptrs, nrows, dev_deleted=None, row_offset=0):
+        """Zero-copy table over device buffers (e.g. torch tensors' data_ptr())."""
+        descs = (ColDesc * len(col_descs))()
+        for j, (t, s) in enumerate(col_descs):
+            descs[j].attr_type, descs[j].size = t, s
+        ptrs = (ctypes.c_void_p * len(col_descs))(*dev_ptrs)
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_table_wrap(self.h, descs, len(col_descs), nrows, ptrs, dev_deleted, row_offset,
+                                  ctypes.byref(h)))
+        return Table(self, h, nrows, list(col_descs), row_offset, keep=[descs, ptrs])
+
+    # -- plans / scans ---------------------------------------------------
+    def compile(self, table, cnf):
+        keep = []
+        c = make_cnf(cnf, keep)
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_plan_compile(self.h, table.h, ctypes.byref(c), ctypes.byref(h)))
+        return Plan(self, h, table)
+
+    def scan_count(self, plan):
+        n = ctypes.c_int64()
+        _chk(lib().mbx_scan_count(self.h, plan.h, ctypes.byref(n)))
+        return n.value
+
+    def scan_count_async(self, plan, dev_ptr):
+        _chk(lib().mbx_scan_count_async(self.h, plan.h, dev_ptr))
+
+    def scan_bitmap(self, plan):
+        h = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        _chk(lib().mbx_scan_bitmap(self.h, plan.h, ctypes.byref(h), ctypes.byref(n)))
+        return Bitmap(self, h, plan.table.nrows)
+
+    def scan_bitmap_async(self, plan, bitmap):
+        _chk(lib().mbx_scan_bitmap_async(self.h, plan.h, bitmap.h))
+
+    def scan_aggregate(self, plan, col):
+        a = Agg()
+        _chk(lib().mbx_scan_aggregate(self.h, plan.h, col, ctypes.byref(a)))
+        if a.agg_type == INTEGER:
+            return dict(count=a.count, sum=a.isum, min=a.imin, max=a.imax)
+        return dict(count=a.count, sum=a.fsum, min=a.fmin, max=a.fmax)
+
+    def scan_aggregate_async(self, plan, col, dev_ptr):
+        _chk(lib().mbx_scan_aggregate_async(self.h, plan.h, col, dev_ptr))
+
+    # -- bitmaps ---------------------------------------------------------
+    def bitmap_alloc(self, nbits):
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_bitmap_alloc(self.h, nbits, ctypes.byref(h)))
+        return Bitmap(self, h, nbits)
+
+    def bitmap_upload(self, nbits, words):
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_bitmap_upload(self.h, nbits, w.ctypes.data if w.size else None, ctypes.byref(h)))
+        return Bitmap(self, h, nbits)
+
+    def bitmap_combine(self, op, a, b):
+        h = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        _chk(lib().mbx_bitmap_combine(self.h, op, a.h, b.h, ctypes.byref(h), ctypes.byref(n)))
+        return Bitmap(self, h, a.nbits)
+
+    def bitmap_cnf(self, nbits, conjuncts, deleted=None):
+        """conjuncts: list of lists of Bitmap (OR within, AND across)."""
+        flat = [b for conj in conjuncts for b in conj]
+        bms = (ctypes.c_void_p * max(1, len(flat)))(*[b.h.value for b in flat])
+        offs = (ctypes.c_int32 * (len(conjuncts) + 1))()
+        k = 0
+        for i, conj in enumerate(conjuncts):
+            offs[i] = k
+            k += len(conj)
+        offs[len(conjuncts)] = k
+        h = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        _chk(lib().mbx_bitmap_cnf(self.h, nbits, bms, offs, len(conjuncts), None if deleted is None else deleted.h,
+                                  ctypes.byref(h), ctypes.byref(n)))
+        return Bitmap(self, h, nbits)
+
+    def bitmap_cnf_async(self, conjuncts, out, deleted=None):
+        flat = [b for conj in conjuncts for b in conj]
+        bms = (ctypes.c_void_p * max(1, len(flat)))(*[b.h.value for b in flat])
+        offs = (ctypes.c_int32 * (len(conjuncts) + 1))()
+        k = 0
+        for i, conj in enumerate(conjuncts):
+            offs[i] = k
+            k += len(conj)
+        offs[len(conjuncts)] = k
+        _chk(lib().mbx_bitmap_cnf_async(self.h, bms, offs, len(conjuncts),
+                                        None if deleted is None else deleted.h, out.h))
+
+    def index_build(self, table, col, values):
+        keep = []
+        ops = (Operand * len(values))(*[_operand(v, keep) for v in values])
+        hs = (ctypes.c_void_p * len(values))()
+        _chk(lib().mbx_bitmap_index_build(self.h, table.h, col, ops, len(values), hs))
+        return [Bitmap(self, ctypes.c_void_p(hs[i]), table.nrows) for i in range(len(values))]
+
+    def select(self, bitmap, row_offset=0):
+        n = ctypes.c_int64()
+        cap = max(1, bitmap.count)
+        ids = np.zeros(cap, dtype=np.int64)
+        _chk(lib().mbx_bitmap_select(self.h, bitmap.h, row_offset, ids.ctypes.data, cap, ctypes.byref(n)))
+        return ids[:n.value]
+
+    def materialize(self, table, bitmap, proj):
+        """(ids, [column arrays]) of every selected row, ascending positions."""
+        n = ctypes.c_int64()
+        cap = max(1, bitmap.count)
+        ids = np.zeros(cap, dtype=np.int64)
+        outs = [table.empty_column(j, cap) for j in proj]
+        ptrs = (ctypes.c_void_p * max(1, len(proj)))(*[o.ctypes.data for o in outs])
+        pj = (ctypes.c_int32 * max(1, len(proj)))(*proj)
+        _chk(lib().mbx_materialize(self.h, table.h, bitmap.h, pj, len(proj), ids.ctypes.data, ptrs, cap,
+                                   ctypes.byref(n)))
+        return ids[:n.value], [o[:n.value] for o in outs]
+
+    def cursor(self, table, bitmap, proj):
+        h = ctypes.c_void_p()
+        pj = (ctypes.c_int32 * max(1, len(proj)))(*proj)
+        _chk(lib().mbx_cursor_open(self.h, table.h, bitmap.h, pj, len(proj), ctypes.byref(h)))
+        return Cursor(self, h, table, list(proj))
+
+
+class _Handle:
+    _free = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            getattr(lib(), self._free)(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Table(_Handle):
+    _free = "mbx_table_free"
+
+    def __init__(self, ctx, h, nrows, descs, row_offset, keep=None):
+        self.ctx, self.h, self.nrows, self.descs, self.row_offset = ctx, h, nrows, descs, row_offset
+        self._keep = keep
+
+    def empty_column(self, j, n):
+        t, size = self.descs[j]
+        if t == STRING:
+            return np.zeros((n, size), dtype=np.uint8)
+        return np.zeros(n, dtype=np.int32 if t == INTEGER else np.float32)
+
+
+class Plan(_Handle):
+    _free = "mbx_plan_free"
+
+    def __init__(self, ctx, h, table):
+        self.ctx, self.h, self.table = ctx, h, table
+
+
+class Bitmap(_Handle):
+    _free = "mbx_bitmap_free"
+
+    def __init__(self, ctx, h, nbits):
+        self.ctx, self.h, self.nbits = ctx, h, nbits
+
+    @property
+    def nwords(self):
+        return (self.nbits + 63) // 64
+
+    @property
+    def count(self):
+        c = ctypes.c_int64()
+        _chk(lib().mbx_bitmap_info(self.h, None, None, ctypes.byref(c)))
+        return c.value
+
+    def download(self):
+        w = np.zeros(max(1, self.nwords), dtype=np.uint64)
+        _chk(lib().mbx_bitmap_download(self.ctx.h, self.h, w.ctypes.data, len(w)))
+        return w[:self.nwords]
+
+
+class Cursor(_Handle):
+    """iterator.Iterator over a materialised selection: next() hands out batches."""
+    _free = "mbx_cursor_close"
+
+    def __init__(self, ctx, h, table, proj):
+        self.ctx, self.h, self.table, self.proj = ctx, h, table, proj
+
+    @property
+    def count(self):
+        c = ctypes.c_int64()
+        _chk(lib().mbx_cursor_count(self.h, ctypes.byref(c)))
+        return c.value
+
+    def next(self, max_rows):
+        ids = np.zeros(max_rows, dtype=np.int64)
+        outs = [self.table.empty_column(j, max_rows) for j in self.proj]
+        ptrs = (ctypes.c_void_p * max(1, len(outs)))(*[o.ctypes.data for o in outs])
+        n = ctypes.c_int64()
+        _chk(lib().mbx_cursor_next(self.h, max_rows, ids.ctypes.data, ptrs, ctypes.byref(n)))
+        k = n.value
+        return ids[:k], [o[:k] for o in outs]
+
+    def restart(self):
+        _chk(lib().mbx_cursor_restart(self.h))

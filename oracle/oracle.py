@@ -204,6 +204,14 @@ def filescan(table, cnf):
     return n, words[:table.nwords], ids[:n]
 
 
+def filescan_count(table, cnf):
+    """ColumnarFileScan COUNT only (Query.java:147 resultCount), no outputs."""
+    keep = []
+    c = _cnf(cnf, keep)
+    return _check(lib().orc_filescan(table._c, len(table.columns), table.nrows, table._del_ptr(),
+                                     ctypes.byref(c), None, None), "filescan")
+
+
 def pred_eval(table, cnf, row):
     keep = []
     c = _cnf(cnf, keep)

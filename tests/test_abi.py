@@ -1,0 +1,58 @@
+"""The C-ABI boundary: libmbx.so loads and exports every entry point that
+include/mbx.h declares; no compute is attempted without a GPU."""
+import os
+import re
+
+import pytest
+
+import helpers
+import mbx_pkg
+
+HEADER = os.path.join(helpers.ROOT, "include", "mbx.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(mbx_[a-z_0-9]+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for must in ["mbx_init", "mbx_table_stage", "mbx_plan_compile", "mbx_scan_count", "mbx_scan_bitmap",
+                 "mbx_bitmap_cnf", "mbx_materialize", "mbx_cursor_next", "mbx_scan_aggregate"]:
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol():
+    m = mbx_pkg.load()
+    L = m.lib()
+    missing = [f for f in declared_functions() if not hasattr(L, f)]
+    assert not missing, missing
+    assert sorted(m.mbx.EXPORTS) == declared_functions()
+    assert L.mbx_abi_version() == 1
+
+
+def test_library_is_built_for_gfx950():
+    so = os.path.join(mbx_pkg.PKG_DIR, "libmbx.so")
+    data = open(so, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_no_gpu_fails_loudly():
+    """Without a visible MI355X the executor refuses to run (no CPU fallback)."""
+    m = mbx_pkg.load()
+    if m.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(m.MbxError) as e:
+        m.Context(0)
+    assert e.value.code == m.mbx.E_DEVICE
+    assert "no CPU fallback" in str(e.value)
+
+
+def test_null_arguments_are_rejected_without_a_device():
+    m = mbx_pkg.load()
+    L = m.lib()
+    assert L.mbx_sync(None) == m.mbx.E_INVALID
+    assert b"null" in L.mbx_last_error()
+    assert L.mbx_table_free(None) == 0 and L.mbx_bitmap_free(None) == 0

@@ -1,0 +1,367 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and
+the reference's golden vectors.  Bit-exact for selections, counts, row ids and
+integer aggregates; float SUM within 1e-6 relative (BASELINE.json north_star).
+"""
+import numpy as np
+import pytest
+
+import helpers
+import mbx_pkg
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLD = helpers.load_golden()
+
+
+@pytest.fixture(scope="module")
+def m():
+    return mbx_pkg.load()
+
+
+@pytest.fixture(scope="module")
+def ctx(m):
+    c = m.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def mini(ctx):
+    rows = helpers.load_minidata()
+    cols = helpers.minidata_columns(rows)
+    return rows, cols, oracle.Table(cols), ctx.stage(cols)
+
+
+def gpu_select(ctx, table, cnf):
+    plan = ctx.compile(table, cnf)
+    bm = ctx.scan_bitmap(plan)
+    return bm, bm.download()
+
+
+# ------------------------------------------------------------------ goldens
+
+@pytest.mark.parametrize("g", GOLD["bitsets"], ids=lambda g: f"line{g['line']}")
+def test_golden_bitsets_filescan(ctx, mini, g):
+    _, _, _, t = mini
+    bm, words = gpu_select(ctx, t, helpers.golden_cnf(g["cnf"]))
+    assert list(oracle.words_to_positions(words)) == g["positions"]
+    assert bm.count == len(g["positions"])
+    assert list(ctx.select(bm)) == g["positions"]
+
+
+@pytest.mark.parametrize("g", GOLD["full_constraint_counts"], ids=lambda g: f"line{g['line']}")
+def test_golden_counts(ctx, mini, g):
+    _, _, _, t = mini
+    assert ctx.scan_count(ctx.compile(t, helpers.golden_cnf(g["cnf"]))) == g["count"]
+
+
+def index_registry(ctx, ocols, t, col):
+    """`index db cf <col> bitmap`: one BitMapFile per distinct value, built on
+    the GPU in one pass; the registry maps value -> device bitmap."""
+    typ, size, arr = ocols[col]
+    if typ == oracle.STRING:
+        vals = sorted({bytes(r).rstrip(b"\0") for r in arr})
+        specs = [("str", v) for v in vals]
+    else:
+        vals = sorted(set(int(x) for x in arr))
+        specs = [("int", v) for v in vals]
+    bms = ctx.index_build(t, col, specs)
+    return dict(zip(vals, bms))
+
+
+def value_set(reg, typ, op, lit):
+    """ColumnIndexScan.getBitSet value selection (R/index/ColumnIndexScan.java:656-740)."""
+    if typ == oracle.STRING:
+        key = lambda v: oracle.java_mutf8(v).decode("utf-8", "surrogatepass").encode("utf-16-be", "surrogatepass")
+        litb = oracle.java_mutf8(lit)
+        cmp = lambda other: (key(litb) > key(other)) - (key(litb) < key(other))
+        lit_key = litb
+    else:
+        cmp = lambda other: (lit > other) - (lit < other)
+        lit_key = lit
+    out = []
+    if op in (oracle.EQ, oracle.LE, oracle.GE) and lit_key in reg:
+        out.append(reg[lit_key])
+    for v, bm in reg.items():
+        c = cmp(v)
+        if (op in (oracle.LT, oracle.LE) and c > 0) or (op in (oracle.GT, oracle.GE) and c < 0) or \
+                (op == oracle.NE and c != 0):
+            out.append(bm)
+    return out
+
+
+@pytest.mark.parametrize("g", GOLD["bitsets"] + GOLD["indexes_query"],
+                         ids=lambda g: f"line{g['line']}")
+def test_golden_index_scan_cnf(ctx, mini, g):
+    """ColumnarIndexScan: value-set OR per term, OR within a conjunct, AND
+    across conjuncts -- one k_bitmap_cnf launch over the index bitmaps."""
+    rows, ocols, _, t = mini
+    regs = {c: index_registry(ctx, ocols, t, c) for c in range(4)}
+    conjuncts = []
+    for conj in helpers.golden_cnf(g["cnf"]):
+        lst = []
+        for op, (_, fld), (_, lit), *_ in conj:
+            lst += value_set(regs[fld - 1], helpers.MINI_TYPES[fld - 1], op, lit)
+        conjuncts.append(lst)
+    bm = ctx.bitmap_cnf(len(rows), conjuncts)
+    pos = list(oracle.words_to_positions(bm.download()))
+    if "positions" in g:
+        assert pos == g["positions"]
+    else:
+        ids, (a, b, c, d) = ctx.materialize(t, bm, [0, 1, 2, 3])
+        got = [[bytes(x).rstrip(b"\0").decode(), bytes(y).rstrip(b"\0").decode(), int(z), int(w)]
+               for x, y, z, w in zip(a, b, c, d)]
+        assert got == g["rows"] and bm.count == g["count"]
+
+
+# ------------------------------------------------------- synthetic parity
+
+def int_table(n, seed=42, hi=1 << 20, ncols=4, deleted_frac=None):
+    cols = [(oracle.INTEGER, 4, c) for c in helpers.synthetic_int_table(n, ncols, hi, seed)]
+    dele = None if deleted_frac is None else helpers.random_deleted(n, deleted_frac)
+    return cols, dele
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 255, 256, 257, 1000, 4099, 70001])
+@pytest.mark.parametrize("generic", [False, True])
+def test_ragged_sizes(ctx, n, generic, monkeypatch):
+    if generic:
+        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+    cols, _ = int_table(n, hi=100)
+    ot = oracle.Table(cols)
+    t = ctx.stage(cols)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", 50))], [(oracle.GE, ("sym", 2), ("int", 10)),
+                                                      (oracle.EQ, ("sym", 3), ("int", 7))]]
+    n_o, w_o, ids_o = oracle.filescan(ot, cnf)
+    bm, words = gpu_select(ctx, t, cnf)
+    assert bm.count == n_o
+    assert np.array_equal(words, w_o)
+    assert np.array_equal(ctx.select(bm), ids_o)
+    assert ctx.scan_count(ctx.compile(t, cnf)) == n_o
+
+
+@pytest.mark.parametrize("generic", [False, True])
+def test_c2_range_filter_full_size(ctx, generic, monkeypatch):
+    """C2: 10M rows x 4 int32, `c0 < 104858` -> BitSet + positions + COUNT, bit-exact."""
+    if generic:
+        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+    n = 10_000_000
+    cols, _ = int_table(n)
+    ot = oracle.Table(cols)
+    t = ctx.stage(cols)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", 104858))]]
+    n_o, w_o, ids_o = oracle.filescan(ot, cnf)
+    bm, words = gpu_select(ctx, t, cnf)
+    assert bm.count == n_o
+    assert np.array_equal(words, w_o)
+    assert np.array_equal(ctx.select(bm), ids_o)
+
+
+def test_c3_conjunction_count_full_size(ctx):
+    """C3: 100M rows x 4 int32, (c0 < 2^19) AND (c1 >= 2^19) -> COUNT."""
+    n = 100_000_000
+    cols, _ = int_table(n)
+    t = ctx.stage(cols)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", 1 << 19))], [(oracle.GE, ("sym", 2), ("int", 1 << 19))]]
+    got = ctx.scan_count(ctx.compile(t, cnf))
+    ref = int(np.count_nonzero((cols[0][2] < (1 << 19)) & (cols[1][2] >= (1 << 19))))
+    assert got == ref
+    assert got == oracle.filescan(oracle.Table(cols), cnf)[0]
+    # complement identity over the full table (size-independent property)
+    neg = [[(oracle.GE, ("sym", 1), ("int", 1 << 19)), (oracle.LT, ("sym", 2), ("int", 1 << 19))]]
+    assert got + ctx.scan_count(ctx.compile(t, neg)) == n
+
+
+@pytest.mark.parametrize("generic", [False, True])
+def test_deleted_rows(ctx, generic, monkeypatch):
+    if generic:
+        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+    n = 1_000_003
+    cols, dele = int_table(n, hi=1000, deleted_frac=0.1)
+    ot = oracle.Table(cols, dele)
+    t = ctx.stage(cols, dele)
+    cnf = [[(oracle.NE, ("sym", 4), ("int", 3))], [(oracle.LE, ("sym", 2), ("int", 500))]]
+    n_o, w_o, _ = oracle.filescan(ot, cnf)
+    bm, words = gpu_select(ctx, t, cnf)
+    assert np.array_equal(words, w_o) and bm.count == n_o
+    assert ctx.scan_count(ctx.compile(t, None)) == n - int(sum(bin(int(x)).count("1") for x in dele))
+
+
+@pytest.mark.parametrize("op", [oracle.EQ, oracle.LT, oracle.GT, oracle.NE, oracle.LE, oracle.GE, oracle.NOT,
+                                oracle.NOP, oracle.RANGE])
+@pytest.mark.parametrize("lit_left", [False, True])
+def test_operator_table(ctx, op, lit_left):
+    cols, _ = int_table(5000, hi=20)
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    term = (op, ("int", 9), ("sym", 2)) if lit_left else (op, ("sym", 2), ("int", 9))
+    cnf = [[term]]
+    n_o, w_o, _ = oracle.filescan(ot, cnf)
+    bm, words = gpu_select(ctx, t, cnf)
+    assert np.array_equal(words, w_o) and bm.count == n_o
+
+
+def test_column_vs_column_and_constant_terms(ctx):
+    cols, _ = int_table(9999, hi=30)
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    for cnf in ([[(oracle.LE, ("sym", 1), ("sym", 2))]],
+                [[(oracle.EQ, ("int", 1), ("int", 2))], [(oracle.GT, ("sym", 3), ("int", 20))]],
+                [[(oracle.LT, ("int", 1), ("int", 2))]],
+                [[(oracle.LT, ("int", 1), ("int", 2)), (oracle.EQ, ("sym", 4), ("int", 5))]]):
+        n_o, w_o, _ = oracle.filescan(ot, cnf)
+        bm, words = gpu_select(ctx, t, cnf)
+        assert np.array_equal(words, w_o) and bm.count == n_o, cnf
+
+
+def test_errors_follow_the_reference(ctx, m):
+    cols, _ = int_table(100)
+    t = ctx.stage(cols)
+    with pytest.raises(m.MbxError) as e:
+        ctx.compile(t, [[(oracle.EQ, ("sym", 9), ("int", 1))]])
+    assert e.value.code == m.mbx.E_RANGE           # FieldNumberOutOfBoundException
+    with pytest.raises(m.MbxError) as e:
+        ctx.compile(t, [[(oracle.EQ, ("sym", 1), ("str", "x"))]])
+    assert e.value.code == m.mbx.E_TYPE            # mismatched operand types
+
+
+def mixed_table(n, seed=5):
+    """C5 schema: i32 c0 uniform [0,2^20); f32 c1 uniform [0,1); char(16) c2
+    from a 50-name dictionary."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    names = [f"{chr(65 + (i * 7) % 26)}{'abcdefghijklmnop'[:(i % 15) + 1]}"[:16] for i in range(50)]
+    c0 = rng.integers(0, 1 << 20, size=n, dtype=np.int32)
+    c1 = rng.random(n, dtype=np.float32)
+    idx = rng.integers(0, 50, size=n)
+    dic = helpers.encode_strings(names, 16)
+    c2 = dic[idx]
+    return [(oracle.INTEGER, 4, c0), (oracle.REAL, 4, c1), (oracle.STRING, 16, c2)], names
+
+
+C5_CNF = [[(oracle.LT, ("sym", 1), ("int", 1 << 19))], [(oracle.GE, ("sym", 2), ("real", 0.25))],
+          [(oracle.GE, ("sym", 3), ("str", "M"))]]
+
+
+def test_c5_mixed_filter_and_aggregates(ctx):
+    cols, _ = mixed_table(2_000_000)
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    n_o, w_o, _ = oracle.filescan(ot, C5_CNF)
+    bm, words = gpu_select(ctx, t, C5_CNF)
+    assert np.array_equal(words, w_o) and bm.count == n_o
+    a_o = oracle.aggregate(ot, C5_CNF, 1)
+    a_g = ctx.scan_aggregate(ctx.compile(t, C5_CNF), 1)
+    assert a_g["count"] == a_o["count"]
+    assert a_g["min"] == a_o["min"] and a_g["max"] == a_o["max"]
+    assert abs(a_g["sum"] - a_o["sum"]) <= 1e-6 * abs(a_o["sum"])
+    i_o = oracle.aggregate(ot, C5_CNF, 0)
+    i_g = ctx.scan_aggregate(ctx.compile(t, C5_CNF), 0)
+    assert i_g == i_o
+
+
+@pytest.mark.parametrize("generic", [False, True])
+def test_fast_path_aggregates(ctx, generic, monkeypatch):
+    if generic:
+        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+    n = 3_000_017
+    rng = np.random.Generator(np.random.PCG64(11))
+    cols = [(oracle.INTEGER, 4, rng.integers(-1000, 1000, n, dtype=np.int32)),
+            (oracle.REAL, 4, (rng.random(n, dtype=np.float32) - 0.5) * 100)]
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    cnf = [[(oracle.GT, ("sym", 1), ("int", -100))], [(oracle.LT, ("sym", 2), ("real", 10.0))]]
+    for col in (0, 1):
+        a_o = oracle.aggregate(ot, cnf, col)
+        a_g = ctx.scan_aggregate(ctx.compile(t, cnf), col)
+        assert a_g["count"] == a_o["count"] and a_g["min"] == a_o["min"] and a_g["max"] == a_o["max"]
+        assert abs(a_g["sum"] - a_o["sum"]) <= 1e-6 * max(1.0, abs(a_o["sum"]))
+    # empty selection: identities
+    empty = ctx.scan_aggregate(ctx.compile(t, [[(oracle.LT, ("sym", 1), ("int", -5000))]]), 0)
+    assert empty["count"] == 0 and empty["sum"] == 0
+
+
+def test_nan_raises_like_the_reference(ctx, m):
+    cols = [(oracle.REAL, 4, np.array([1.0, np.nan, 3.0], dtype=np.float32))]
+    t = ctx.stage(cols)
+    with pytest.raises(m.MbxError) as e:
+        ctx.scan_count(ctx.compile(t, [[(oracle.LT, ("sym", 1), ("real", 2.0))]]))
+    assert e.value.code == m.mbx.E_TYPE
+
+
+def test_strings_java_order(ctx):
+    vals = ["", "a", "ab", "b", "South_Dakota", "South", "é", "€", "\U0001F600", "a\u0000b", "a\u0000",
+            "zzzzzzzzzzzzzzzz"]
+    arr = helpers.encode_strings(vals, 16)
+    cols = [(oracle.STRING, 16, arr)]
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    for lit in vals + ["a\u0000a", "zzzzzzzzzzzzzzzzz", "Sout"]:
+        for op in (oracle.LT, oracle.EQ, oracle.GE, oracle.NE):
+            cnf = [[(op, ("sym", 1), ("str", lit))]]
+            n_o, w_o, _ = oracle.filescan(ot, cnf)
+            bm, words = gpu_select(ctx, t, cnf)
+            assert np.array_equal(words, w_o), (lit, op)
+    # materialised strings come back as the caller's modified UTF-8
+    bm, _ = gpu_select(ctx, t, None)
+    ids, (out,) = ctx.materialize(t, bm, [0])
+    assert np.array_equal(out, arr)
+
+
+def test_bitmap_ops_and_materialize(ctx):
+    n = 1_234_567
+    rng = np.random.Generator(np.random.PCG64(3))
+    a_bits, b_bits = rng.random(n) < 0.3, rng.random(n) < 0.5
+    pack = lambda bits: np.packbits(bits, bitorder="little").view(np.uint8)
+    words = lambda bits: np.frombuffer(np.pad(pack(bits), (0, (-len(pack(bits))) % 8)).tobytes(), dtype=np.uint64)
+    wa, wb = words(a_bits), words(b_bits)
+    A, B = ctx.bitmap_upload(n, wa), ctx.bitmap_upload(n, wb)
+    assert A.count == int(a_bits.sum())
+    m = mbx_pkg.load().mbx
+    for op, ref in ((m.BM_AND, wa & wb), (m.BM_OR, wa | wb), (m.BM_ANDNOT, wa & ~wb)):
+        r = ctx.bitmap_combine(op, A, B)
+        assert np.array_equal(r.download(), ref)
+    r = ctx.bitmap_cnf(n, [[A], [B]], deleted=ctx.bitmap_upload(n, words(rng.random(n) < 0.1)))
+    cols, _ = int_table(n)
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    ids, (c0, c3) = ctx.materialize(t, r, [0, 3])
+    assert np.array_equal(ids, oracle.words_to_positions(r.download()))
+    g0, g3 = oracle.gather(ot, ids, [0, 3])
+    assert np.array_equal(c0, g0) and np.array_equal(c3, g3)
+    cur = ctx.cursor(t, r, [0, 3])
+    parts = []
+    while True:
+        i, (x, y) = cur.next(100_000)
+        if len(i) == 0:
+            break
+        parts.append((i, x, y))
+    assert np.array_equal(np.concatenate([p[0] for p in parts]), ids)
+    assert np.array_equal(np.concatenate([p[1] for p in parts]), c0)
+
+
+def test_index_build_matches_oracle(ctx):
+    cols, _ = mixed_table(300_001)
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    _, names = mixed_table(1)
+    bms = ctx.index_build(t, 2, [("str", s) for s in names[:10]] + [("str", "nope")])
+    for s, bm in zip(names[:10] + ["nope"], bms):
+        n_o, w_o = oracle.bitmap_eq(ot, 2, ("str", s))
+        assert bm.count == n_o and np.array_equal(bm.download(), w_o)
+    cols2, _ = int_table(300_001, hi=10)
+    ot2, t2 = oracle.Table(cols2), ctx.stage(cols2)
+    for v, bm in zip(range(10), ctx.index_build(t2, 2, [("int", v) for v in range(10)])):
+        n_o, w_o = oracle.bitmap_eq(ot2, 2, ("int", v))
+        assert np.array_equal(bm.download(), w_o)
+
+
+def test_row_range_shards_concatenate(ctx):
+    """Sharding: row ranges on 64-row boundaries; per-shard
+    BitSets and global positions concatenate to the unsharded answer."""
+    n = 2_000_000
+    cols, dele = int_table(n, hi=1000, deleted_frac=0.05)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", 300))], [(oracle.GE, ("sym", 2), ("int", 100))]]
+    n_o, w_o, ids_o = oracle.filescan(oracle.Table(cols, dele), cnf)
+    bounds = [0, 64 * 7001, 64 * 20000, n]
+    words, ids = [], []
+    for s, e in zip(bounds[:-1], bounds[1:]):
+        sh = [(ty, sz, a[s:e]) for ty, sz, a in cols]
+        t = ctx.stage(sh, dele[s // 64:(e + 63) // 64].copy(), row_offset=s)
+        bm, w = gpu_select(ctx, t, cnf)
+        words.append(w)
+        ids.append(ctx.select(bm, row_offset=s))
+    assert np.array_equal(np.concatenate(words), w_o)
+    assert np.array_equal(np.concatenate(ids), ids_o)
