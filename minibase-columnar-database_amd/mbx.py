@@ -10,8 +10,10 @@ CNF spec accepted by Context.compile (the flattened CondExpr[] of the reference)
     term = (op, operand1, operand2[, index_type])
     operand = ('sym', fld) | ('int', v) | ('real', v) | ('str', text_or_mutf8_bytes)
 """
+import atexit
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -201,17 +203,38 @@ def make_cnf(cnf, keep):
     return c
 
 
+_live_contexts = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    """Free every library object before the HIP runtime tears down."""
+    for c in list(_live_contexts):
+        c.close()
+
+
 class Context:
-    """mbx_ctx: one GPU, one HIP stream."""
+    """mbx_ctx: one GPU, one HIP stream.  Objects created through a context
+    (tables, plans, bitmaps, cursors) are freed before it (C-ABI rule)."""
 
     def __init__(self, device=0):
         h = ctypes.c_void_p()
         _chk(lib().mbx_init(device, ctypes.byref(h)))
         self.h = h
         self.device = device
+        self._children = weakref.WeakSet()
+        _live_contexts.add(self)
+
+    def _own(self, obj):
+        self._children.add(obj)
+        return obj
 
     def close(self):
         if self.h:
+            # cursors and bitmaps first, then plans, then tables
+            order = {"mbx_cursor_close": 0, "mbx_bitmap_free": 1, "mbx_plan_free": 2, "mbx_table_free": 3}
+            for ch in sorted(list(self._children), key=lambda o: order.get(o._free, 9)):
+                ch.close()
             lib().mbx_free(self.h)
             self.h = None
 
@@ -398,6 +421,7 @@ class Table(_Handle):
     def __init__(self, ctx, h, nrows, descs, row_offset, keep=None):
         self.ctx, self.h, self.nrows, self.descs, self.row_offset = ctx, h, nrows, descs, row_offset
         self._keep = keep
+        ctx._own(self)
 
     def empty_column(self, j, n):
         t, size = self.descs[j]
@@ -411,6 +435,7 @@ class Plan(_Handle):
 
     def __init__(self, ctx, h, table):
         self.ctx, self.h, self.table = ctx, h, table
+        ctx._own(self)
 
 
 class Bitmap(_Handle):
@@ -418,6 +443,7 @@ class Bitmap(_Handle):
 
     def __init__(self, ctx, h, nbits):
         self.ctx, self.h, self.nbits = ctx, h, nbits
+        ctx._own(self)
 
     @property
     def nwords(self):
@@ -441,6 +467,7 @@ class Cursor(_Handle):
 
     def __init__(self, ctx, h, table, proj):
         self.ctx, self.h, self.table, self.proj = ctx, h, table, proj
+        ctx._own(self)
 
     @property
     def count(self):
