@@ -710,6 +710,8 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.count_out = count_out;
   L.agg_out = agg_out;
   L.nan_out = nan_out;
+  const char* var = getenv("MBX_SCAN_VARIANT");
+  L.variant = var ? atoi(var) : 0;
   HIPCHK(launch_scan(L, c->stream));
   return MBX_OK;
 }

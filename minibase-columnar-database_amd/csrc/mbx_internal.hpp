@@ -110,6 +110,7 @@ struct ScanLaunch {
   int64_t* count_out;         // device or null
   AggOut* agg_out;            // device or null
   int32_t* nan_out;           // device or null
+  int32_t variant;            // 0: default kernel; >0: tuning variant (MBX_SCAN_VARIANT)
 };
 
 struct ProjCol {

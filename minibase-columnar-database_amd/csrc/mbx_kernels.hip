@@ -257,14 +257,111 @@ __device__ __forceinline__ uint64_t pack_word16(uint32_t nib, int lane) {
 // Each wave streams whole 256-row tiles of its block's segment: one
 // global_load_dwordx4 per column per tile, terms folded into per-row
 // conjunct bitmasks (cb), the CNF holds when cb == all_conj.
+// per-tile body shared by every unroll depth: v holds the tile's K columns
+// (4 rows per lane); folds the CNF, applies deleted rows and emits the
+// requested output.
 template <int K, int MODE, bool DEL>
+__device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const int32_t (&v)[K][4],
+                                          int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
+                                          Acc& acc, uint64_t& wave_count) {
+  const int64_t nrows = L.nrows;
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t row0 = t * kTileRows + lane * 4;
+  uint32_t cb[4] = {0u, 0u, 0u, 0u};
+  for (int ti = 0; ti < nterms; ++ti) {
+    const KTerm& T = P->terms[ti];
+    const int lhs = T.lhs;
+    int32_t a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = v[0][j];
+#pragma unroll
+    for (int s = 1; s < K; ++s)
+      if (lhs == s) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = v[s][j];
+      }
+    bool r[4];
+    if (T.kind == kInt) {
+      cmp4<int32_t>(T.op, a, T.ilit, r);
+    } else {
+      float f[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[j] = __int_as_float(a[j]);
+        acc.nan |= (f[j] != f[j]) && (row0 + j < nrows);
+      }
+      cmp4<float>(T.op, f, T.flit, r);
+    }
+    const uint32_t bit = T.conj_bit;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cb[j] |= r[j] ? bit : 0u;
+  }
+
+  bool p[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) p[j] = (cb[j] == all) && (row0 + j < nrows);
+  const int64_t word = t * kWordsPerTile + (lane >> 4);
+  if (DEL) {
+    const uint64_t dw = word < nwords ? L.deleted[word] : 0ull;
+    const uint32_t dn = (uint32_t)(dw >> ((lane & 15) * 4)) & 0xFu;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = p[j] && !((dn >> j) & 1u);
+  }
+  if (MODE == kModeBitmap) {
+    const uint32_t nib = (uint32_t)p[0] | ((uint32_t)p[1] << 1) | ((uint32_t)p[2] << 2) | ((uint32_t)p[3] << 3);
+    const uint64_t w = pack_word16(nib, lane);
+    if ((lane & 15) == 0 && word < nwords) L.out_words[word] = w;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wave_count += __popcll(__ballot(p[j]));
+  if (MODE == kModeAgg) {
+    int32_t g[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = v[0][j];
+#pragma unroll
+    for (int s = 1; s < K; ++s)
+      if (agg_slot == s) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) g[j] = v[s][j];
+      }
+    if (agg_real) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float f = __int_as_float(g[j]);
+        acc.fsum += p[j] ? (double)f : 0.0;
+        acc.fmin = p[j] && f < acc.fmin ? f : acc.fmin;
+        acc.fmax = p[j] && f > acc.fmax ? f : acc.fmax;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc.isum += p[j] ? (int64_t)g[j] : 0;
+        acc.imin = p[j] && g[j] < acc.imin ? g[j] : acc.imin;
+        acc.imax = p[j] && g[j] > acc.imax ? g[j] : acc.imax;
+      }
+    }
+  }
+}
+
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ v4i load16(const int32_t* p) {
+  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
+  return *reinterpret_cast<const v4i*>(p);
+}
+
+// U tiles per wave iteration: all U x K 16-byte loads are issued before the
+// first compare, so each wave keeps U*K*1 KiB in flight.  Tiles of a block's
+// segment are dealt round-robin to its 4 waves (the block streams one
+// contiguous run of U*4 tiles per iteration).
+template <int K, int MODE, bool DEL, int U, bool NT>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
   const int64_t nrows = L.nrows;
   const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
-  const int64_t nwords = (nrows + 63) >> 6;
   const int64_t t0 = (int64_t)blockIdx.x * L.tiles_per_block;
   const int64_t t1 = min(t0 + L.tiles_per_block, ntiles);
   const int nterms = P->nterms;
@@ -280,98 +377,32 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   acc_init(acc);
   uint64_t wave_count = 0;
 
-  for (int64_t t = t0 + wave; t < t1; t += kWaves) {
-    const int64_t row0 = t * kTileRows + lane * 4;
-    int32_t v[K][4];
-    if ((t + 1) * kTileRows <= nrows) {
+  for (int64_t base = t0 + wave; base < t1; base += kWaves * U) {
+    int32_t v[U][K][4];
 #pragma unroll
-      for (int s = 0; s < K; ++s) {
-        const int4 q = *reinterpret_cast<const int4*>(colp[s] + t * kTileRows + lane * 4);
-        v[s][0] = q.x;
-        v[s][1] = q.y;
-        v[s][2] = q.z;
-        v[s][3] = q.w;
-      }
-    } else {
+    for (int u = 0; u < U; ++u) {
+      const int64_t t = base + (int64_t)u * kWaves;
+      const int64_t row0 = t * kTileRows + lane * 4;
+      if (t < t1 && (t + 1) * kTileRows <= nrows) {
 #pragma unroll
-      for (int s = 0; s < K; ++s)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[s][j] = row0 + j < nrows ? colp[s][row0 + j] : 0;
-    }
-
-    uint32_t cb[4] = {0u, 0u, 0u, 0u};
-    for (int ti = 0; ti < nterms; ++ti) {
-      const KTerm& T = P->terms[ti];
-      const int lhs = T.lhs;
-      int32_t a[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] = v[0][j];
-#pragma unroll
-      for (int s = 1; s < K; ++s)
-        if (lhs == s) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) a[j] = v[s][j];
-        }
-      bool r[4];
-      if (T.kind == kInt) {
-        cmp4<int32_t>(T.op, a, T.ilit, r);
-      } else {
-        float f[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f[j] = __int_as_float(a[j]);
-          acc.nan |= (f[j] != f[j]) && (row0 + j < nrows);
-        }
-        cmp4<float>(T.op, f, T.flit, r);
-      }
-      const uint32_t bit = T.conj_bit;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cb[j] |= r[j] ? bit : 0u;
-    }
-
-    bool p[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) p[j] = (cb[j] == all) && (row0 + j < nrows);
-    const int64_t word = t * kWordsPerTile + (lane >> 4);
-    if (DEL) {
-      const uint64_t dw = word < nwords ? L.deleted[word] : 0ull;
-      const uint32_t dn = (uint32_t)(dw >> ((lane & 15) * 4)) & 0xFu;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) p[j] = p[j] && !((dn >> j) & 1u);
-    }
-    if (MODE == kModeBitmap) {
-      const uint32_t nib = (uint32_t)p[0] | ((uint32_t)p[1] << 1) | ((uint32_t)p[2] << 2) | ((uint32_t)p[3] << 3);
-      const uint64_t w = pack_word16(nib, lane);
-      if ((lane & 15) == 0 && word < nwords) L.out_words[word] = w;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wave_count += __popcll(__ballot(p[j]));
-    if (MODE == kModeAgg) {
-      int32_t g[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) g[j] = v[0][j];
-#pragma unroll
-      for (int s = 1; s < K; ++s)
-        if (agg_slot == s) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) g[j] = v[s][j];
-        }
-      if (agg_real) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float f = __int_as_float(g[j]);
-          acc.fsum += p[j] ? (double)f : 0.0;
-          acc.fmin = p[j] && f < acc.fmin ? f : acc.fmin;
-          acc.fmax = p[j] && f > acc.fmax ? f : acc.fmax;
+        for (int s = 0; s < K; ++s) {
+          const v4i q = load16<NT>(colp[s] + row0);
+          v[u][s][0] = q.x;
+          v[u][s][1] = q.y;
+          v[u][s][2] = q.z;
+          v[u][s][3] = q.w;
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc.isum += p[j] ? (int64_t)g[j] : 0;
-          acc.imin = p[j] && g[j] < acc.imin ? g[j] : acc.imin;
-          acc.imax = p[j] && g[j] > acc.imax ? g[j] : acc.imax;
-        }
+        for (int s = 0; s < K; ++s)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[u][s][j] = (t < t1 && row0 + j < nrows) ? colp[s][row0 + j] : 0;
       }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t t = base + (int64_t)u * kWaves;
+      if (t < t1) fast_tile<K, MODE, DEL>(L, P, v[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count);
     }
   }
   acc.count = lane == 0 ? (int64_t)wave_count : 0;
@@ -685,6 +716,9 @@ __global__ __launch_bounds__(kBlock) void k_index_build(KCol col, int64_t nrows,
 
 // ---------------------------------------------------------------- launchers
 
+constexpr int kDefaultU = 2;
+constexpr bool kDefaultNT = false;
+
 int64_t choose_tiles_per_block(int64_t nrows) {
   const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
   // ~2048 blocks (8 per CU on 256 CUs) for large inputs, >= 4 tiles per block
@@ -700,10 +734,22 @@ int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block) {
 
 template <int K, int MODE>
 static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
-  if (L.deleted)
-    hipLaunchKernelGGL((k_scan_fast<K, MODE, true>), grid, dim3(kBlock), 0, s, L);
-  else
-    hipLaunchKernelGGL((k_scan_fast<K, MODE, false>), grid, dim3(kBlock), 0, s, L);
+  if (L.deleted) {
+    hipLaunchKernelGGL((k_scan_fast<K, MODE, true, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
+    return;
+  }
+  if (K == 2 && MODE == kModeCount && L.variant) {  // tuning variants of the C3 kernel
+    switch (L.variant) {
+      case 1: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, false>), grid, dim3(kBlock), 0, s, L); return;
+      case 2: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, false>), grid, dim3(kBlock), 0, s, L); return;
+      case 3: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, false>), grid, dim3(kBlock), 0, s, L); return;
+      case 4: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 5: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 6: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, true>), grid, dim3(kBlock), 0, s, L); return;
+      default: break;
+    }
+  }
+  hipLaunchKernelGGL((k_scan_fast<K, MODE, false, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
 }
 
 template <int MODE>
