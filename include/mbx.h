@@ -208,8 +208,9 @@ int mbx_bitmap_cnf_async(mbx_ctx *ctx, const mbx_bitmap *const *bms, const int32
                          int32_t nconj, const mbx_bitmap *deleted, mbx_bitmap *out);
 /* Columnarfile.createBitMapIndex (R/columnar/Columnarfile.java:698-753): one
  * BitMapFile per value, bit p set where column `col` (0-based) equals
- * values[v]; deleted rows included, as in the reference.  One pass over the
- * column for all values. */
+ * values[v]; deleted positions stay clear (the reference builds the index
+ * from a ColumnScan, which skips them).  One pass over the column for all
+ * values. */
 int mbx_bitmap_index_build(mbx_ctx *ctx, const mbx_table *t, int32_t col, const mbx_operand *values,
                            int32_t nvalues, mbx_bitmap **out);
 

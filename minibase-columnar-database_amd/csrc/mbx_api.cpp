@@ -1061,7 +1061,7 @@ extern "C" int mbx_bitmap_index_build(mbx_ctx* c, const mbx_table* t, int32_t co
     kc.base = tc.dev;
     kc.kind = col_kind(tc.attr_type);
     kc.stride_w = tc.stride_w;
-    e = launch_index_build(kc, t->nrows, dvals, nvalues, vw, outs.data(), out[0]->wpb, c->stream);
+    e = launch_index_build(kc, t->nrows, t->deleted, dvals, nvalues, vw, outs.data(), out[0]->wpb, c->stream);
     for (int32_t v = 0; v < nvalues && e == hipSuccess; v++)
       e = launch_seg_popcount(out[v]->words, out[v]->nwords, out[v]->wpb, out[v]->segs, c->stream);
   }

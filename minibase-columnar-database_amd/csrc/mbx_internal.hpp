@@ -143,7 +143,8 @@ hipError_t launch_seg_scan(const Partial* seg_parts, int64_t nseg, int64_t* seg_
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                               const int64_t* seg_offsets, int64_t row_offset, int64_t* ids,
                               const ProjCol* proj, void* const* out, int32_t nproj, hipStream_t s);
-hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint32_t* values, int32_t nvalues,
+hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
+                              int32_t nvalues,
                               int32_t value_words, uint64_t* const* outs, int64_t words_per_block, hipStream_t s);
 
 }  // namespace mbx

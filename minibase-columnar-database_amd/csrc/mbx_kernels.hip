@@ -352,18 +352,22 @@ __device__ __forceinline__ v4i load16(const int32_t* p) {
 }
 
 // U tiles per wave iteration: all U x K 16-byte loads are issued before the
-// first compare, so each wave keeps U*K*1 KiB in flight.  Tiles of a block's
-// segment are dealt round-robin to its 4 waves (the block streams one
-// contiguous run of U*4 tiles per iteration).
-template <int K, int MODE, bool DEL, int U, bool NT>
+// first compare, so each wave keeps U*K*1 KiB in flight.
+// IL = false: a block owns a contiguous segment of tiles, dealt round-robin
+//   to its 4 waves (per-segment counts feed compaction).
+// IL = true:  grid-stride interleave -- at any moment the whole grid reads one
+//   contiguous window of each column (DRAM row-buffer friendly); partial
+//   counts are then per block, not per segment (COUNT / aggregate only).
+template <int K, int MODE, bool DEL, int U, bool NT, bool IL = false>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
   const int64_t nrows = L.nrows;
   const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
-  const int64_t t0 = (int64_t)blockIdx.x * L.tiles_per_block;
-  const int64_t t1 = min(t0 + L.tiles_per_block, ntiles);
+  const int64_t t0 = IL ? (int64_t)blockIdx.x * kWaves : (int64_t)blockIdx.x * L.tiles_per_block;
+  const int64_t t1 = IL ? ntiles : min(t0 + L.tiles_per_block, ntiles);
+  const int64_t ustep = IL ? (int64_t)gridDim.x * kWaves : kWaves;  // between the U tiles of one wave
   const int nterms = P->nterms;
   const uint32_t all = P->all_conj;
   const int agg_slot = MODE == kModeAgg ? P->agg_slot : 0;
@@ -377,11 +381,11 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   acc_init(acc);
   uint64_t wave_count = 0;
 
-  for (int64_t base = t0 + wave; base < t1; base += kWaves * U) {
+  for (int64_t base = t0 + wave; base < t1; base += ustep * U) {
     int32_t v[U][K][4];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t t = base + (int64_t)u * kWaves;
+      const int64_t t = base + (int64_t)u * ustep;
       const int64_t row0 = t * kTileRows + lane * 4;
       if (t < t1 && (t + 1) * kTileRows <= nrows) {
 #pragma unroll
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t t = base + (int64_t)u * kWaves;
+      const int64_t t = base + (int64_t)u * ustep;
       if (t < t1) fast_tile<K, MODE, DEL>(L, P, v[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count);
     }
   }
@@ -679,14 +683,16 @@ __global__ __launch_bounds__(kBlock) void k_materialize(const uint64_t* __restri
   }
 }
 
-// One pass over a column building the BitSet of each listed value.
+// One pass over a column building the BitSet of each listed value.  Deleted
+// positions stay clear: createBitMapIndex walks a ColumnScan, which skips them
+// (R/columnar/ColumnScan.java:49-65).
 struct IndexArgs {
   uint64_t* out[64];
 };
 
-__global__ __launch_bounds__(kBlock) void k_index_build(KCol col, int64_t nrows, const uint32_t* __restrict__ vals,
-                                                        int32_t nvalues, int32_t vwords, IndexArgs A,
-                                                        int64_t words_per_block) {
+__global__ __launch_bounds__(kBlock) void k_index_build(KCol col, int64_t nrows, const uint64_t* __restrict__ del,
+                                                        const uint32_t* __restrict__ vals, int32_t nvalues,
+                                                        int32_t vwords, IndexArgs A, int64_t words_per_block) {
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
   const int64_t nwords = (nrows + 63) >> 6;
@@ -694,7 +700,7 @@ __global__ __launch_bounds__(kBlock) void k_index_build(KCol col, int64_t nrows,
   const int64_t w1 = min(w0 + words_per_block, nwords);
   for (int64_t w = w0 + wave; w < w1; w += kWaves) {
     const int64_t row = w * 64 + lane;
-    const bool valid = row < nrows;
+    const bool valid = row < nrows && !(del && ((del[w] >> lane) & 1ull));
     uint32_t x0 = 0;
     if (valid && col.kind != kStr) x0 = ((const uint32_t*)col.base)[row];
     for (int v = 0; v < nvalues; ++v) {
@@ -746,6 +752,12 @@ static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
       case 4: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, true>), grid, dim3(kBlock), 0, s, L); return;
       case 5: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, true>), grid, dim3(kBlock), 0, s, L); return;
       case 6: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 7: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, false, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 8: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, false, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 9: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, false, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 10: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, true, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 11: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, true, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 12: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, true, true>), grid, dim3(kBlock), 0, s, L); return;
       default: break;
     }
   }
@@ -834,15 +846,16 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
   return hipGetLastError();
 }
 
-hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint32_t* values, int32_t nvalues,
-                              int32_t value_words, uint64_t* const* outs, int64_t words_per_block, hipStream_t s) {
+hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
+                              int32_t nvalues, int32_t value_words, uint64_t* const* outs, int64_t words_per_block,
+                              hipStream_t s) {
   const int64_t nwords = (nrows + 63) >> 6;
   const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
   for (int32_t v0 = 0; v0 < nvalues; v0 += 64) {
     IndexArgs A;
     const int32_t nv = nvalues - v0 < 64 ? nvalues - v0 : 64;
     for (int i = 0; i < nv; ++i) A.out[i] = outs[v0 + i];
-    hipLaunchKernelGGL(k_index_build, dim3((unsigned)g), dim3(kBlock), 0, s, col, nrows,
+    hipLaunchKernelGGL(k_index_build, dim3((unsigned)g), dim3(kBlock), 0, s, col, nrows, deleted,
                        values + (int64_t)v0 * value_words, nv, value_words, A, words_per_block);
   }
   return hipGetLastError();

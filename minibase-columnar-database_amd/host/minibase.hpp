@@ -1,0 +1,353 @@
+// minibase.hpp -- C++ mirror of the reference's scan/index operator surface,
+// executed by the MI355X kernels behind include/mbx.h.
+//
+// Class and method names, argument meaning and error behaviour follow the
+// Java reference (R/ = minijava/src): a caller of
+//   iterator::ColumnarFileScan   (R/iterator/ColumnarFileScan.java:51-188)
+//   iterator::ColumnarColumnScan (R/iterator/ColumnarColumnScan.java:39-211)
+//   index::ColumnIndexScan       (R/index/ColumnIndexScan.java:76-741, Bitmap branch)
+//   index::ColumnarIndexScan     (R/index/ColumnarIndexScan.java:79-370)
+// builds the same CondExpr[] / FldSpec[] and drives get_next() / close() /
+// restart() exactly as with the Java classes.  Rows are never evaluated here:
+// every predicate, BitSet operation and projection is a kernel launch.
+//
+// The storage layer below the scans (DB file, BufMgr, heap files) is out of
+// scope for the GPU build: columnar::Columnarfile holds the decoded columns
+// of a file in a process-wide registry (the stand-in for SystemDefs'
+// JavabaseDB) and stages them to HBM once.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/mbx.h"
+
+namespace chainexception {
+// R/chainexception/ChainException.java:11 -- every checked exception's root.
+class ChainException : public std::runtime_error {
+ public:
+  explicit ChainException(const std::string& msg, int code = 0) : std::runtime_error(msg), code(code) {}
+  int code;  // MBX_E_* when raised from the device layer
+};
+}  // namespace chainexception
+
+namespace global {
+struct AttrType {  // R/global/AttrType.java:45-49
+  enum { attrString = 0, attrInteger = 1, attrReal = 2, attrSymbol = 3, attrNull = 4 };
+  int attrType;
+  AttrType(int t = attrNull) : attrType(t) {}
+};
+struct AttrOperator {  // R/global/AttrOperator.java:98-106
+  enum { aopEQ = 0, aopLT = 1, aopGT = 2, aopNE = 3, aopLE = 4, aopGE = 5, aopNOT = 6, aopNOP = 7, opRANGE = 8 };
+  int attrOperator;
+  AttrOperator(int o = aopEQ) : attrOperator(o) {}
+  static AttrOperator findOperator(const std::string& op);  // :154-172
+  std::string toString() const;
+};
+struct IndexType {  // R/global/IndexType.java:10-13
+  enum { None = 0, B_Index = 1, Hash = 2, Bitmap = 3 };
+  int indexType;
+  IndexType(int t = None) : indexType(t) {}
+  std::string toString() const;
+};
+struct TID {  // R/global/TID.java: numRIDs + position
+  int numRIDs = 0;
+  int64_t position = -1;
+};
+// SystemDefs (R/global/SystemDefs.java:6-9): the process-wide engine state;
+// here the GPU context every operator launches on.
+class SystemDefs {
+ public:
+  static mbx_ctx* ctx();
+  static void shutdown();
+};
+}  // namespace global
+
+namespace heap {
+// The projected output tuple (iterator's Jtuple).  Field accessors mirror
+// R/heap/Tuple.java:194-343 (1-based field numbers).
+class Tuple {
+ public:
+  void setHdr(const std::vector<global::AttrType>& types, const std::vector<short>& str_sizes);
+  int getIntFld(int fldNo) const;
+  float getFloFld(int fldNo) const;
+  std::string getStrFld(int fldNo) const;
+  void setIntFld(int fldNo, int v);
+  void setFloFld(int fldNo, float v);
+  void setStrFld(int fldNo, const std::string& v);
+  short noOfFlds() const { return (short)types_.size(); }
+  int size() const;  // header + fields, as Tuple.size() with setHdr's layout
+ private:
+  void check(int fldNo, int type) const;
+  std::vector<global::AttrType> types_;
+  std::vector<short> str_sizes_;
+  std::vector<int32_t> ints_;
+  std::vector<float> reals_;
+  std::vector<std::string> strs_;
+};
+}  // namespace heap
+
+namespace iterator {
+using global::AttrOperator;
+using global::AttrType;
+using global::IndexType;
+
+class FileScanException : public chainexception::ChainException {
+  using ChainException::ChainException;
+};
+class PredEvalException : public chainexception::ChainException {
+  using ChainException::ChainException;
+};
+class UnknowAttrType : public chainexception::ChainException {
+  using ChainException::ChainException;
+};
+class FieldNumberOutOfBoundException : public chainexception::ChainException {
+  using ChainException::ChainException;
+};
+class InvalidRelation : public chainexception::ChainException {
+  using ChainException::ChainException;
+};
+
+struct RelSpec {  // R/iterator/RelSpec.java
+  enum { outer = 0, innerRel = 1 };
+  int key;
+  RelSpec(int k = outer) : key(k) {}
+};
+struct FldSpec {  // R/iterator/FldSpec.java
+  RelSpec relation;
+  int offset;  // 1-based
+  FldSpec(RelSpec r = RelSpec(), int off = 1) : relation(r), offset(off) {}
+};
+struct Operand {  // R/iterator/Operand.java
+  FldSpec symbol;
+  std::string string;  // modified UTF-8 bytes (ASCII text is its own encoding)
+  int integer = 0;
+  float real = 0.0f;
+};
+// R/iterator/CondExpr.java:12-57: one OR-linked disjunct list element.
+struct CondExpr {
+  AttrOperator op;
+  AttrType type1, type2;
+  Operand operand1, operand2;
+  IndexType indexType;
+  CondExpr* next = nullptr;
+};
+
+// CondExpr[] (null-terminated array of OR-chains) -> the C-ABI's flat CNF.
+struct CnfImage {
+  std::vector<mbx_condexpr> conds;
+  std::vector<int32_t> offsets;
+  mbx_cnf view() const;
+};
+CnfImage flatten(CondExpr* const* filter, int fld_remap_from = 0, int fld_remap_to = 0);
+
+// R/iterator/Iterator.java:12-141
+class Iterator {
+ public:
+  virtual ~Iterator() = default;
+  virtual heap::Tuple* get_next() = 0;
+  virtual void close() = 0;
+  virtual void restart() = 0;
+  virtual int getTupleSize() = 0;
+
+ protected:
+  bool closeFlag = false;
+};
+}  // namespace iterator
+
+namespace columnar {
+using global::AttrType;
+
+// A device BitSet handle (java.util.BitSet on the GPU).
+class DeviceBitSet {
+ public:
+  DeviceBitSet() = default;
+  explicit DeviceBitSet(mbx_bitmap* b) : b_(b) {}
+  ~DeviceBitSet();
+  DeviceBitSet(const DeviceBitSet&) = delete;
+  DeviceBitSet& operator=(const DeviceBitSet&) = delete;
+  mbx_bitmap* get() const { return b_; }
+  int64_t cardinality() const;
+  std::vector<uint64_t> toLongArray() const;  // BitSet.toLongArray()
+  std::vector<int64_t> positions(int64_t row_offset = 0) const;
+
+ private:
+  mbx_bitmap* b_ = nullptr;
+};
+using BitSetPtr = std::shared_ptr<DeviceBitSet>;
+
+// R/columnar/Columnarfile.java: the file's schema + its HBM image.
+class Columnarfile {
+ public:
+  // open an existing file (:239-359)
+  explicit Columnarfile(const std::string& name);
+  // create (:49-231) from decoded column values; strings as modified UTF-8
+  Columnarfile(const std::string& name, int numColumns, const std::vector<std::string>& colNames,
+               const std::vector<AttrType>& types, const std::vector<short>& sizes);
+
+  void insertColumns(const std::vector<std::vector<int32_t>>& ints, const std::vector<std::vector<float>>& reals,
+                     const std::vector<std::vector<std::string>>& strs, int64_t nrows);
+  int64_t getTupleCnt() const;
+  int getFieldCount() const;
+  std::vector<AttrType> getAttributeTypes() const;
+  std::vector<short> getStringSizes() const;  // sizes of the string columns, in order
+  std::vector<short> getAttrSizes() const;
+  int colNameToIndex(const std::string& name) const;
+  std::string indexToColName(int idx) const;
+  const std::string& get_fileName() const { return name_; }
+  mbx_table* table() const;  // staged on first use
+
+  // bitmap index registry (createBitMapIndex :698-753, getBitmapIndex :1103-1127,
+  // getBitmapValues :1138)
+  void createBitMapIndex(int colNo);
+  bool bitmapIndexExists(int colNo) const;
+  std::vector<std::string> getBitmapValues(int colNo) const;  // registered value keys
+  BitSetPtr getBitmapIndex(int colNo, const std::string& key) const;  // empty BitSet if absent
+  BitSetPtr getMarkedDeleted() const;  // may be null (nothing deleted)
+  void markTupleDeleted(int64_t position);
+
+  struct Impl;
+
+ private:
+  std::string name_;
+  std::shared_ptr<Impl> impl_;
+};
+
+std::string int_key(int v);
+}  // namespace columnar
+
+namespace iterator {
+
+// R/iterator/ColumnarFileScan.java:51-99 (+ get_next :156-172, get_next_tid :174-188)
+class ColumnarFileScan : public Iterator {
+ public:
+  ColumnarFileScan(const std::string& file_name, const std::vector<AttrType>& in1,
+                   const std::vector<short>& s1_sizes, short len_in1, int n_out_flds,
+                   const std::vector<FldSpec>& proj_list, CondExpr* const* outFilter);
+  heap::Tuple* get_next() override;
+  global::TID get_next_tid();
+  void close() override;
+  void restart() override;
+  int getTupleSize() override;
+  int64_t resultCount() const;  // COUNT of the whole selection (one kernel)
+  columnar::BitSetPtr selection() const { return sel_; }
+
+ private:
+  void fill(int64_t row);
+  void next_batch();
+  columnar::Columnarfile f_;
+  std::vector<AttrType> in1_;
+  std::vector<FldSpec> perm_mat_;
+  heap::Tuple Jtuple_;
+  mbx_plan* plan_ = nullptr;
+  columnar::BitSetPtr sel_;
+  mbx_cursor* cur_ = nullptr;
+  std::vector<int32_t> proj_cols_;
+  std::vector<std::vector<uint8_t>> batch_;
+  std::vector<int64_t> batch_ids_;
+  int64_t batch_n_ = 0, batch_i_ = 0;
+};
+
+// R/iterator/ColumnarColumnScan.java:39-88: predicate on one column (field 1
+// of the CondExpr refers to column colNo), late-materialised out_indexes.
+class ColumnarColumnScan : public Iterator {
+ public:
+  ColumnarColumnScan(columnar::Columnarfile* cf, int colNo, int n_out_flds, const std::vector<int>& out_indexes,
+                     const std::vector<FldSpec>& proj_list, CondExpr* const* outFilter);
+  heap::Tuple* get_next() override;
+  global::TID get_next_tid();
+  void close() override;
+  void restart() override;
+  int getTupleSize() override;
+
+ private:
+  std::unique_ptr<ColumnarFileScan> inner_;
+};
+}  // namespace iterator
+
+namespace index {
+using global::AttrType;
+using global::IndexType;
+using iterator::CondExpr;
+using iterator::FldSpec;
+
+class IndexException : public chainexception::ChainException {
+  using ChainException::ChainException;
+};
+class UnknownIndexTypeException : public chainexception::ChainException {
+  using ChainException::ChainException;
+};
+
+// R/index/ColumnIndexScan.java:76-272 (Bitmap branch): `col op literal`
+// over the bitmap indexes; positions skip deleted rows.
+class ColumnIndexScan : public iterator::Iterator {
+ public:
+  ColumnIndexScan(IndexType index, columnar::Columnarfile* cf, const std::string& indName,
+                  const std::vector<AttrType>& types, const std::vector<short>& str_sizes, int noInFlds, int noOutFlds,
+                  const std::vector<int>& outIndexes, const std::vector<FldSpec>& outFlds, CondExpr* const* selects,
+                  int fldNum, bool indexOnly);
+  // the short form ColumnarIndexScan uses (:185-272): positions only
+  ColumnIndexScan(IndexType index, columnar::Columnarfile* cf, const std::string& indName,
+                  const std::vector<AttrType>& types, const std::vector<short>& str_sizes, int noInFlds,
+                  CondExpr* const* selects, int fldNum);
+  heap::Tuple* get_next() override;
+  global::TID get_next_tid();
+  columnar::BitSetPtr getPositionsOfIndexScan();  // :647-654
+  void close() override;
+  void restart() override;
+  int getTupleSize() override;
+
+  // getBitSet's value selection (:656-740): the bitmaps whose value v
+  // satisfies `v op literal`
+  static std::vector<columnar::BitSetPtr> valueBitmaps(const columnar::Columnarfile& cf, int colNo,
+                                                       const CondExpr& e);
+
+ private:
+  void materialize();
+  columnar::Columnarfile* f_;
+  int colNo_;
+  std::vector<int> outIndexes_;
+  std::vector<AttrType> types_;
+  bool index_only_ = false;
+  CondExpr sel_{};
+  columnar::BitSetPtr positions_;
+  heap::Tuple Jtuple_;
+  std::vector<int64_t> ids_;
+  std::vector<std::vector<uint8_t>> vals_;
+  int64_t next_ = 0;
+  bool ready_ = false;
+};
+
+// R/index/ColumnarIndexScan.java:79-182 (+ getOutputPositions :270, get_next :287-308)
+class ColumnarIndexScan : public iterator::Iterator {
+ public:
+  ColumnarIndexScan(columnar::Columnarfile* cf, const std::vector<int>& fldNums,
+                    const std::vector<IndexType>& indexTypes, const std::vector<std::string>& indNames,
+                    const std::vector<AttrType>& types, const std::vector<short>& str_sizes, int noInFlds,
+                    int noOutFlds, const std::vector<int>& out_indexes, const std::vector<FldSpec>& outFlds,
+                    CondExpr* const* selects, bool indexOnly);
+  columnar::BitSetPtr getOutputPositions() const { return output_; }
+  heap::Tuple* get_next() override;
+  void close() override;
+  void restart() override;
+  int getTupleSize() override;
+  bool usedFusedCnf() const { return fused_; }
+
+ private:
+  columnar::Columnarfile* f_;
+  std::vector<int> outIndexes_;
+  std::vector<AttrType> types_;
+  columnar::BitSetPtr output_;
+  heap::Tuple Jtuple_;
+  std::vector<int64_t> ids_;
+  std::vector<std::vector<uint8_t>> vals_;
+  int64_t next_ = 0;
+  bool ready_ = false;
+  bool fused_ = false;
+};
+}  // namespace index

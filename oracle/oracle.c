@@ -263,11 +263,12 @@ static int equal_value(const orc_column *col, int64_t row, const orc_operand *va
   return ORC_OK;
 }
 
-int64_t orc_bitmap_eq(const orc_column *col, int64_t nrows, const orc_operand *value,
-                      uint64_t *out_words) {
+int64_t orc_bitmap_eq(const orc_column *col, int64_t nrows, const uint64_t *deleted_words,
+                      const orc_operand *value, uint64_t *out_words) {
   memset(out_words, 0, (size_t)((nrows + 63) / 64) * sizeof(uint64_t));
   int64_t n = 0;
   for (int64_t pos = 0; pos < nrows; pos++) {
+    if (deleted(deleted_words, pos)) continue; /* ColumnScan.getNext skips it */
     int eq = 0;
     int rc = equal_value(col, pos, value, &eq);
     if (rc) return rc;
@@ -279,15 +280,17 @@ int64_t orc_bitmap_eq(const orc_column *col, int64_t nrows, const orc_operand *v
   return n;
 }
 
-/* getBitmapValues: the distinct values the index registered (Columnarfile.java:1138).
- * Returned as row indices of first occurrences. */
-static int64_t distinct_rows(const orc_column *col, int64_t nrows, int64_t **out) {
+/* getBitmapValues: the distinct values the index registered while scanning
+ * the live rows (Columnarfile.java:698-753, :1138).  Returned as row indices
+ * of first occurrences. */
+static int64_t distinct_rows(const orc_column *col, int64_t nrows, const uint64_t *deleted_words, int64_t **out) {
   int64_t *first = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nrows > 0 ? nrows : 1));
   int64_t nd = 0;
   if (col->attr_type == ORC_INTEGER) {
     /* sort-free O(n * distinct) -- fine for an oracle on low-cardinality columns */
     const int32_t *d = (const int32_t *)col->data;
     for (int64_t r = 0; r < nrows; r++) {
+      if (deleted(deleted_words, r)) continue;
       int seen = 0;
       for (int64_t k = 0; k < nd && !seen; k++) seen = d[first[k]] == d[r];
       if (!seen) first[nd++] = r;
@@ -295,6 +298,7 @@ static int64_t distinct_rows(const orc_column *col, int64_t nrows, int64_t **out
   } else {
     const char *d = (const char *)col->data;
     for (int64_t r = 0; r < nrows; r++) {
+      if (deleted(deleted_words, r)) continue;
       int seen = 0;
       for (int64_t k = 0; k < nd && !seen; k++)
         seen = memcmp(d + (size_t)first[k] * col->size, d + (size_t)r * col->size, (size_t)col->size) == 0;
@@ -316,13 +320,13 @@ int64_t orc_column_index_scan(const orc_column *col, int64_t nrows, const uint64
   /* symbol = value (EQ, LE, GE include the literal itself; :660-668).  A
    * literal with no bitmap file yields an empty BitSet (Columnarfile.java:1124). */
   if (op == ORC_EQ || op == ORC_LE || op == ORC_GE) {
-    rc = orc_bitmap_eq(col, nrows, value, tmp);
+    rc = orc_bitmap_eq(col, nrows, deleted_words, value, tmp);
     if (rc < 0) goto done;
     for (int64_t w = 0; w < nw; w++) out_words[w] |= tmp[w];
   }
   if (op == ORC_LT || op == ORC_LE || op == ORC_GT || op == ORC_GE || op == ORC_NE) {
     int64_t *first = NULL;
-    int64_t nd = distinct_rows(col, nrows, &first);
+    int64_t nd = distinct_rows(col, nrows, deleted_words, &first);
     for (int64_t k = 0; k < nd; k++) {
       fieldval other, lit;
       read_column(col, 1, 1, first[k], &other);
@@ -340,7 +344,7 @@ int64_t orc_column_index_scan(const orc_column *col, int64_t nrows, const uint64
       ov.type = col->attr_type;
       if (col->attr_type == ORC_INTEGER) ov.integer = other.i;
       else { ov.string = other.s; ov.string_len = other.slen; }
-      rc = orc_bitmap_eq(col, nrows, &ov, tmp);
+      rc = orc_bitmap_eq(col, nrows, deleted_words, &ov, tmp);
       if (rc < 0) { free(first); goto done; }
       for (int64_t w = 0; w < nw; w++) out_words[w] |= tmp[w];
     }

@@ -113,11 +113,12 @@ int orc_aggregate(const orc_column *cols, int32_t ncols, int64_t nrows,
                   int32_t agg_col, orc_agg *out);
 
 /* BitMapFile contents for one distinct value: Columnarfile.createBitMapIndex
- * (R/columnar/Columnarfile.java:698-753) sets bit `position` of the value's
- * bitmap for every row holding that value (deleted rows included).
- * Returns the number of set bits. */
-int64_t orc_bitmap_eq(const orc_column *col, int64_t nrows, const orc_operand *value,
-                      uint64_t *out_words);
+ * (R/columnar/Columnarfile.java:698-753) walks a ColumnScan (which skips
+ * deleted positions, R/columnar/ColumnScan.java:49-65) and sets bit
+ * `position` of the value's bitmap for every row holding that value.
+ * deleted_words may be NULL.  Returns the number of set bits. */
+int64_t orc_bitmap_eq(const orc_column *col, int64_t nrows, const uint64_t *deleted_words,
+                      const orc_operand *value, uint64_t *out_words);
 
 /* ColumnIndexScan(Bitmap) positions for the single term `col op value`:
  * getBitSet (R/index/ColumnIndexScan.java:656-740) ORs the bitmaps of every

@@ -90,7 +90,7 @@ def lib():
         L.orc_filescan.restype = ctypes.c_int64
         L.orc_aggregate.argtypes = [P(_Column), ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, P(_Cnf),
                                     ctypes.c_int32, P(_Agg)]
-        L.orc_bitmap_eq.argtypes = [P(_Column), ctypes.c_int64, P(_Operand), ctypes.c_void_p]
+        L.orc_bitmap_eq.argtypes = [P(_Column), ctypes.c_int64, ctypes.c_void_p, P(_Operand), ctypes.c_void_p]
         L.orc_bitmap_eq.restype = ctypes.c_int64
         L.orc_column_index_scan.argtypes = [P(_Column), ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                             P(_Operand), ctypes.c_void_p]
@@ -233,7 +233,7 @@ def bitmap_eq(table, col, value):
     keep = []
     o = _operand(value, keep)
     words = np.zeros(max(1, table.nwords), dtype=np.uint64)
-    n = _check(lib().orc_bitmap_eq(ctypes.byref(table._c[col]), table.nrows, ctypes.byref(o),
+    n = _check(lib().orc_bitmap_eq(ctypes.byref(table._c[col]), table.nrows, table._del_ptr(), ctypes.byref(o),
                                    words.ctypes.data), "bitmap_eq")
     return n, words[:table.nwords]
 
