@@ -712,7 +712,12 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.nan_out = nan_out;
   const char* var = getenv("MBX_SCAN_VARIANT");
   L.variant = var ? atoi(var) : 0;
+  const char* fm = getenv("MBX_FIN_MODE");
+  L.fin_mode = fm ? atoi(fm) : kFinWriteThrough;
+  if (L.fin_mode == kFinSeparate) L.ticket = nullptr;
   HIPCHK(launch_scan(L, c->stream));
+  if (L.fin_mode == kFinSeparate)
+    HIPCHK(launch_finalize(parts, grid_blocks(L.nrows, tpb), L.agg_kind, agg_out, count_out, nan_out, c->stream));
   return MBX_OK;
 }
 

@@ -111,6 +111,13 @@ struct ScanLaunch {
   AggOut* agg_out;            // device or null
   int32_t* nan_out;           // device or null
   int32_t variant;            // 0: default kernel; >0: tuning variant (MBX_SCAN_VARIANT)
+  int32_t fin_mode;           // FinMode (MBX_FIN_MODE): how the last block sees the partials
+};
+
+enum FinMode : int32_t {
+  kFinWriteThrough = 0,  // sc1 partial stores + ticket, sc1 loads by the last block
+  kFinFences = 1,        // plain stores + agent release / acquire fences
+  kFinSeparate = 2,      // no ticket: a separate k_finalize launch
 };
 
 struct ProjCol {

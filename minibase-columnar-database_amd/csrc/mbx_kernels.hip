@@ -140,15 +140,35 @@ __device__ __forceinline__ Acc from_partial(const Partial& p) {
   return b;
 }
 
+// write-through (sc1) store / load of one Partial, 8 bytes at a time
+__device__ __forceinline__ void store_partial_sc1(Partial* dst, const Partial& p) {
+  const uint64_t* s = reinterpret_cast<const uint64_t*>(&p);
+  uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+#pragma unroll
+  for (int i = 0; i < kSegStride; ++i) __hip_atomic_store(d + i, s[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ Partial load_partial_sc1(const Partial* src) {
+  Partial p;
+  uint64_t* d = reinterpret_cast<uint64_t*>(&p);
+  uint64_t* s = reinterpret_cast<uint64_t*>(const_cast<Partial*>(src));
+#pragma unroll
+  for (int i = 0; i < kSegStride; ++i) d[i] = __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return p;
+}
+
 // Reduce n partials with one block in a fixed order (thread i folds i, i+256,
 // ... sequentially, then a fixed xor tree and wave order) and write the
-// results.  Bit-reproducible for a given grid.
+// results.  Bit-reproducible for a given grid.  SC1: the partials were
+// stored write-through in this launch and are read with sc1 loads.
+template <bool SC1>
 __device__ __forceinline__ void finalize_block(const Partial* parts, int64_t n, int32_t agg_kind, AggOut* out,
                                                int64_t* count_out, int32_t* nan_flag) {
   __shared__ Acc fsh[kWaves];
   Acc a;
   acc_init(a);
-  for (int64_t i = threadIdx.x; i < n; i += kBlock) acc_merge(a, from_partial(parts[i]));
+  for (int64_t i = threadIdx.x; i < n; i += kBlock)
+    acc_merge(a, from_partial(SC1 ? load_partial_sc1(parts + i) : parts[i]));
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
     Acc b = shfl_xor_acc(a, m);
@@ -217,8 +237,15 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
     p.fmax = r.fmax;
     p.nan_seen = r.nan;
     p.pad_ = 0;
-    L.partials[blockIdx.x] = p;
-    if (L.ticket) {
+    if (L.ticket && L.fin_mode == kFinWriteThrough) {
+      // write-through (sc1) partial, drained, then the ticket: no L2
+      // write-back fence needed (MI355X_MICROARCH.md, Valid forms row 1)
+      store_partial_sc1(L.partials + blockIdx.x, p);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t t = __hip_atomic_fetch_add(L.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      is_last = (t == gridDim.x - 1);
+    } else if (L.ticket) {
+      L.partials[blockIdx.x] = p;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -228,12 +255,17 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+    } else {
+      L.partials[blockIdx.x] = p;
     }
   }
   if (!L.ticket) return;
   __syncthreads();
   if (is_last) {
-    finalize_block(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
+    if (L.fin_mode == kFinWriteThrough)
+      finalize_block<true>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
+    else
+      finalize_block<false>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
     if (threadIdx.x == 0) __hip_atomic_store(L.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -495,7 +527,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_generic(ScanLaunch L) {
 __global__ __launch_bounds__(kBlock) void k_finalize(const Partial* __restrict__ parts, int64_t n,
                                                      int32_t agg_kind, AggOut* out, int64_t* count_out,
                                                      int32_t* nan_flag) {
-  finalize_block(parts, n, agg_kind, out, count_out, nan_flag);
+  finalize_block<false>(parts, n, agg_kind, out, count_out, nan_flag);
 }
 
 // ---------------------------------------------------------- bitmap kernels
@@ -723,12 +755,17 @@ __global__ __launch_bounds__(kBlock) void k_index_build(KCol col, int64_t nrows,
 // ---------------------------------------------------------------- launchers
 
 constexpr int kDefaultU = 2;
-constexpr bool kDefaultNT = false;
+// measured on MI355X (profiles/r01/sweep3.log, C3 100M rows): U=2 tiles in
+// flight per wave with non-temporal loads, 4 blocks per CU, write-through
+// partials -> 135 us = 5.9 TB/s; plain loads +3 %, 8 blocks/CU +7 %,
+// 2 blocks/CU +56 %, release-fence partials +22 %.
+constexpr bool kDefaultNT = true;
 
 int64_t choose_tiles_per_block(int64_t nrows) {
   const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
-  // ~2048 blocks (8 per CU on 256 CUs) for large inputs, >= 4 tiles per block
-  int64_t tpb = (ntiles + 2047) / 2048;
+  // ~1024 blocks (4 per CU on 256 CUs, 16 waves/CU) for large inputs,
+  // >= 4 tiles per block
+  int64_t tpb = (ntiles + 1023) / 1024;
   return tpb < 4 ? 4 : tpb;
 }
 

@@ -1,0 +1,949 @@
+// minibase.cpp -- implementation of the C++ operator mirror (minibase.hpp).
+// Every row-level computation is a libmbx kernel; this file only translates
+// the reference's objects (CondExpr chains, FldSpec lists, Columnarfile
+// metadata) into C-ABI calls and walks result batches for get_next().
+#include "minibase.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <sstream>
+
+namespace minibase {
+
+namespace {
+
+template <class E>
+void chk(int rc, const std::string& what) {
+  if (rc < 0) throw E(what + ": " + mbx_last_error(), rc);
+}
+
+// Java String.compareTo over modified UTF-8 payloads: decode to UTF-16 code
+// units and compare (used only for value-dictionary decisions, never rows).
+std::vector<uint16_t> utf16_of(const std::string& s) {
+  std::vector<uint16_t> u;
+  const unsigned char* p = (const unsigned char*)s.data();
+  size_t i = 0, n = s.size();
+  while (i < n) {
+    unsigned c = p[i];
+    if (c < 0x80) {
+      u.push_back((uint16_t)c);
+      i += 1;
+    } else if ((c & 0xE0) == 0xC0 && i + 1 < n) {
+      u.push_back((uint16_t)(((c & 0x1F) << 6) | (p[i + 1] & 0x3F)));
+      i += 2;
+    } else if (i + 2 < n) {
+      u.push_back((uint16_t)(((c & 0x0F) << 12) | ((p[i + 1] & 0x3F) << 6) | (p[i + 2] & 0x3F)));
+      i += 3;
+    } else {
+      break;
+    }
+  }
+  return u;
+}
+
+int java_compare(const std::string& a, const std::string& b) {
+  const auto x = utf16_of(a), y = utf16_of(b);
+  const size_t lim = std::min(x.size(), y.size());
+  for (size_t k = 0; k < lim; k++)
+    if (x[k] != y[k]) return x[k] < y[k] ? -1 : 1;
+  return x.size() == y.size() ? 0 : (x.size() < y.size() ? -1 : 1);
+}
+
+mbx_ctx* g_ctx = nullptr;
+
+}  // namespace
+
+// ------------------------------------------------------------------ global
+
+namespace global {
+
+mbx_ctx* SystemDefs::ctx() {
+  if (!g_ctx) {
+    const char* d = getenv("MBX_DEVICE");
+    chk<chainexception::ChainException>(mbx_init(d ? atoi(d) : 0, &g_ctx), "SystemDefs: GPU context");
+  }
+  return g_ctx;
+}
+
+}  // namespace global
+namespace columnar {
+void close_all_files();
+}
+namespace global {
+
+// flushAllPages + close: every device object goes before the context
+void SystemDefs::shutdown() {
+  columnar::close_all_files();
+  if (g_ctx) mbx_free(g_ctx);
+  g_ctx = nullptr;
+}
+
+AttrOperator AttrOperator::findOperator(const std::string& op) {
+  if (op == "=") return AttrOperator(aopEQ);
+  if (op == "<") return AttrOperator(aopLT);
+  if (op == ">") return AttrOperator(aopGT);
+  if (op == "!=") return AttrOperator(aopNE);
+  if (op == ">=") return AttrOperator(aopGE);
+  if (op == "<=") return AttrOperator(aopLE);
+  throw chainexception::ChainException("unsupported or invalid operator");
+}
+
+std::string AttrOperator::toString() const {
+  static const char* n[] = {"aopEQ", "aopLT", "aopGT", "aopNE", "aopLE", "aopGE", "aopNOT", "aopNOP", "opRANGE"};
+  if (attrOperator >= 0 && attrOperator <= 8) return n[attrOperator];
+  return "Unexpected AttrOperator " + std::to_string(attrOperator);
+}
+
+std::string IndexType::toString() const {
+  switch (indexType) {
+    case None: return "None";
+    case B_Index: return "B_Index";
+    case Hash: return "Hash";
+    case Bitmap: return "Bitmap";
+  }
+  return "Unexpected IndexType " + std::to_string(indexType);
+}
+
+}  // namespace global
+
+// ------------------------------------------------------------------- heap
+
+namespace heap {
+
+void Tuple::setHdr(const std::vector<global::AttrType>& types, const std::vector<short>& str_sizes) {
+  types_ = types;
+  str_sizes_ = str_sizes;
+  ints_.assign(types.size(), 0);
+  reals_.assign(types.size(), 0.0f);
+  strs_.assign(types.size(), std::string());
+}
+
+void Tuple::check(int fldNo, int type) const {
+  if (fldNo < 1 || fldNo > (int)types_.size())
+    throw iterator::FieldNumberOutOfBoundException("Tuple: field number " + std::to_string(fldNo) + " out of bound");
+  if (types_[(size_t)fldNo - 1].attrType != type)
+    throw iterator::UnknowAttrType("Tuple: field " + std::to_string(fldNo) + " has another type");
+}
+
+int Tuple::getIntFld(int f) const {
+  check(f, global::AttrType::attrInteger);
+  return ints_[(size_t)f - 1];
+}
+float Tuple::getFloFld(int f) const {
+  check(f, global::AttrType::attrReal);
+  return reals_[(size_t)f - 1];
+}
+std::string Tuple::getStrFld(int f) const {
+  check(f, global::AttrType::attrString);
+  return strs_[(size_t)f - 1];
+}
+void Tuple::setIntFld(int f, int v) {
+  check(f, global::AttrType::attrInteger);
+  ints_[(size_t)f - 1] = v;
+}
+void Tuple::setFloFld(int f, float v) {
+  check(f, global::AttrType::attrReal);
+  reals_[(size_t)f - 1] = v;
+}
+void Tuple::setStrFld(int f, const std::string& v) {
+  check(f, global::AttrType::attrString);
+  strs_[(size_t)f - 1] = v;
+}
+
+int Tuple::size() const {
+  // Tuple.setHdr layout (R/heap/Tuple.java:369-411): 2 + 2*(n+1) header bytes
+  int sz = 2 + 2 * ((int)types_.size() + 1);
+  size_t k = 0;
+  for (const auto& t : types_) {
+    if (t.attrType == global::AttrType::attrString) sz += str_sizes_.size() > k ? str_sizes_[k++] + 2 : 2;
+    else sz += 4;
+  }
+  return sz;
+}
+
+}  // namespace heap
+
+// --------------------------------------------------------------- columnar
+
+namespace columnar {
+
+std::string int_key(int v) { return std::to_string(v); }
+
+struct Columnarfile::Impl {
+  std::vector<std::string> names;
+  std::vector<AttrType> types;
+  std::vector<short> sizes;  // attrSizes: 4 or char(n)
+  int64_t nrows = 0;
+  std::vector<std::vector<uint8_t>> host;  // staging image per column
+  std::vector<uint64_t> deleted;
+  bool any_deleted = false;
+  mbx_table* table = nullptr;
+  bool dirty = true;
+  std::map<int, std::map<std::string, BitSetPtr>> bitmaps;  // col -> value key -> BitMapFile
+  BitSetPtr deleted_bm;
+  ~Impl() {
+    bitmaps.clear();
+    deleted_bm.reset();
+    if (table) mbx_table_free(table);
+  }
+};
+
+static std::map<std::string, std::shared_ptr<Columnarfile::Impl>>& registry() {
+  static std::map<std::string, std::shared_ptr<Columnarfile::Impl>> r;
+  return r;
+}
+
+void close_all_files() { registry().clear(); }
+
+DeviceBitSet::~DeviceBitSet() {
+  if (b_) mbx_bitmap_free(b_);
+}
+
+int64_t DeviceBitSet::cardinality() const {
+  int64_t c = 0;
+  mbx_bitmap_info(b_, nullptr, nullptr, &c);
+  if (c < 0) {
+    std::vector<int64_t> p = positions();
+    c = (int64_t)p.size();
+  }
+  return c;
+}
+
+std::vector<uint64_t> DeviceBitSet::toLongArray() const {
+  int64_t nw = 0;
+  mbx_bitmap_info(b_, nullptr, &nw, nullptr);
+  std::vector<uint64_t> w((size_t)nw);
+  if (nw) chk<chainexception::ChainException>(mbx_bitmap_download(global::SystemDefs::ctx(), b_, w.data(), nw),
+                                              "BitSet download");
+  return w;
+}
+
+std::vector<int64_t> DeviceBitSet::positions(int64_t row_offset) const {
+  int64_t nbits = 0;
+  mbx_bitmap_info(b_, &nbits, nullptr, nullptr);
+  std::vector<int64_t> ids((size_t)(nbits > 0 ? nbits : 1));
+  int64_t n = 0;
+  chk<chainexception::ChainException>(
+      mbx_bitmap_select(global::SystemDefs::ctx(), b_, row_offset, ids.data(), (int64_t)ids.size(), &n),
+      "BitSet nextSetBit");
+  ids.resize((size_t)n);
+  return ids;
+}
+
+Columnarfile::Columnarfile(const std::string& name) : name_(name) {
+  auto it = registry().find(name);
+  if (it == registry().end()) throw chainexception::ChainException("Columnarfile " + name + " does not exist");
+  impl_ = it->second;
+}
+
+Columnarfile::Columnarfile(const std::string& name, int numColumns, const std::vector<std::string>& colNames,
+                           const std::vector<AttrType>& types, const std::vector<short>& sizes)
+    : name_(name) {
+  if ((int)colNames.size() != numColumns || (int)types.size() != numColumns || (int)sizes.size() != numColumns)
+    throw chainexception::ChainException("Columnarfile: schema arity mismatch");
+  impl_ = std::make_shared<Impl>();
+  impl_->names = colNames;
+  impl_->types = types;
+  impl_->sizes = sizes;
+  impl_->host.resize((size_t)numColumns);
+  registry()[name] = impl_;
+}
+
+void Columnarfile::insertColumns(const std::vector<std::vector<int32_t>>& ints,
+                                 const std::vector<std::vector<float>>& reals,
+                                 const std::vector<std::vector<std::string>>& strs, int64_t nrows) {
+  Impl& I = *impl_;
+  size_t ki = 0, kr = 0, ks = 0;
+  for (size_t j = 0; j < I.types.size(); j++) {
+    std::vector<uint8_t>& h = I.host[j];
+    const size_t old = h.size();
+    if (I.types[j].attrType == AttrType::attrInteger) {
+      const auto& v = ints.at(ki++);
+      h.resize(old + (size_t)nrows * 4);
+      memcpy(h.data() + old, v.data(), (size_t)nrows * 4);
+    } else if (I.types[j].attrType == AttrType::attrReal) {
+      const auto& v = reals.at(kr++);
+      h.resize(old + (size_t)nrows * 4);
+      memcpy(h.data() + old, v.data(), (size_t)nrows * 4);
+    } else {
+      const auto& v = strs.at(ks++);
+      const size_t sz = (size_t)I.sizes[j];
+      h.resize(old + (size_t)nrows * sz, 0);
+      for (int64_t r = 0; r < nrows; r++) {
+        if (v[(size_t)r].size() > sz) throw chainexception::ChainException("column value exceeds size limit");
+        memcpy(h.data() + old + (size_t)r * sz, v[(size_t)r].data(), v[(size_t)r].size());
+      }
+    }
+  }
+  I.nrows += nrows;
+  I.deleted.resize((size_t)((I.nrows + 63) / 64), 0);
+  I.dirty = true;
+}
+
+int64_t Columnarfile::getTupleCnt() const { return impl_->nrows; }
+int Columnarfile::getFieldCount() const { return (int)impl_->types.size(); }
+std::vector<AttrType> Columnarfile::getAttributeTypes() const { return impl_->types; }
+std::vector<short> Columnarfile::getAttrSizes() const { return impl_->sizes; }
+
+std::vector<short> Columnarfile::getStringSizes() const {
+  std::vector<short> s;
+  for (size_t j = 0; j < impl_->types.size(); j++)
+    if (impl_->types[j].attrType == AttrType::attrString) s.push_back(impl_->sizes[j]);
+  return s;
+}
+
+int Columnarfile::colNameToIndex(const std::string& name) const {
+  for (size_t j = 0; j < impl_->names.size(); j++)
+    if (impl_->names[j] == name) return (int)j;
+  throw chainexception::ChainException("Column " + name + " does not exist");
+}
+
+std::string Columnarfile::indexToColName(int idx) const { return impl_->names.at((size_t)idx); }
+
+mbx_table* Columnarfile::table() const {
+  Impl& I = *impl_;
+  if (I.table && !I.dirty) return I.table;
+  mbx_ctx* c = global::SystemDefs::ctx();
+  if (I.table) {
+    // cached index bitmaps and the deleted BitSet refer to the old image
+    I.bitmaps.clear();
+    I.deleted_bm.reset();
+    mbx_table_free(I.table);
+    I.table = nullptr;
+  }
+  std::vector<mbx_col_desc> d(I.types.size());
+  std::vector<const void*> p(I.types.size());
+  for (size_t j = 0; j < I.types.size(); j++) {
+    d[j].attr_type = I.types[j].attrType;
+    d[j].size = I.sizes[j];
+    p[j] = I.host[j].data();
+  }
+  chk<chainexception::ChainException>(
+      mbx_table_stage(c, d.data(), (int32_t)d.size(), I.nrows, p.data(), I.any_deleted ? I.deleted.data() : nullptr,
+                      0, &I.table),
+      "Columnarfile " + name_ + ": staging to HBM");
+  I.dirty = false;
+  return I.table;
+}
+
+static std::string value_key(const Columnarfile::Impl& I, int col, int64_t row) {
+  const auto& h = I.host[(size_t)col];
+  if (I.types[(size_t)col].attrType == AttrType::attrString) {
+    const size_t sz = (size_t)I.sizes[(size_t)col];
+    const char* s = (const char*)h.data() + (size_t)row * sz;
+    return std::string(s, strnlen(s, sz));
+  }
+  int32_t v;
+  memcpy(&v, h.data() + (size_t)row * 4, 4);
+  return int_key(v);
+}
+
+void Columnarfile::createBitMapIndex(int colNo) {
+  Impl& I = *impl_;
+  if (colNo < 0 || colNo >= (int)I.types.size()) throw chainexception::ChainException("createBitMapIndex: column");
+  if (I.types[(size_t)colNo].attrType == AttrType::attrReal)
+    throw chainexception::ChainException("createBitMapIndex: attrReal columns are not indexed by the reference");
+  mbx_table* t = table();
+  // the value dictionary (the `.hdr` "col.value" registry): distinct values
+  // of the live rows, in first-seen position order
+  std::vector<std::string> keys;
+  std::set<std::string> seen;
+  for (int64_t r = 0; r < I.nrows; r++) {
+    if (I.any_deleted && ((I.deleted[(size_t)(r >> 6)] >> (r & 63)) & 1ull)) continue;
+    std::string k = value_key(I, colNo, r);
+    if (seen.insert(k).second) keys.push_back(k);
+  }
+  std::vector<mbx_operand> vals(keys.size());
+  for (size_t v = 0; v < keys.size(); v++) {
+    memset(&vals[v], 0, sizeof(mbx_operand));
+    vals[v].type = I.types[(size_t)colNo].attrType;
+    if (vals[v].type == AttrType::attrInteger) vals[v].integer = atoi(keys[v].c_str());
+    else {
+      vals[v].string = keys[v].data();
+      vals[v].string_len = (int32_t)keys[v].size();
+    }
+  }
+  auto& reg = I.bitmaps[colNo];
+  reg.clear();
+  for (size_t v0 = 0; v0 < vals.size(); v0 += 256) {
+    const size_t nv = std::min<size_t>(256, vals.size() - v0);
+    std::vector<mbx_bitmap*> out(nv, nullptr);
+    chk<chainexception::ChainException>(
+        mbx_bitmap_index_build(global::SystemDefs::ctx(), t, colNo, vals.data() + v0, (int32_t)nv, out.data()),
+        "createBitMapIndex");
+    for (size_t v = 0; v < nv; v++) reg[keys[v0 + v]] = std::make_shared<DeviceBitSet>(out[v]);
+  }
+}
+
+bool Columnarfile::bitmapIndexExists(int colNo) const { return impl_->bitmaps.count(colNo) > 0; }
+
+std::vector<std::string> Columnarfile::getBitmapValues(int colNo) const {
+  std::vector<std::string> v;
+  auto it = impl_->bitmaps.find(colNo);
+  if (it != impl_->bitmaps.end())
+    for (const auto& kv : it->second) v.push_back(kv.first);
+  return v;
+}
+
+BitSetPtr Columnarfile::getBitmapIndex(int colNo, const std::string& key) const {
+  auto it = impl_->bitmaps.find(colNo);
+  if (it != impl_->bitmaps.end()) {
+    auto jt = it->second.find(key);
+    if (jt != it->second.end()) return jt->second;
+  }
+  // a value without a BitMapFile reads as an empty BitSet (Columnarfile.java:1124),
+  // made on the device as a CNF with one empty OR-conjunct
+  mbx_bitmap* z = nullptr;
+  int64_t cnt = 0;
+  int32_t offs[2] = {0, 0};
+  chk<chainexception::ChainException>(
+      mbx_bitmap_cnf(global::SystemDefs::ctx(), impl_->nrows, nullptr, offs, 1, nullptr, &z, &cnt), "empty BitSet");
+  return std::make_shared<DeviceBitSet>(z);
+}
+
+BitSetPtr Columnarfile::getMarkedDeleted() const {
+  Impl& I = *impl_;
+  if (!I.any_deleted) return nullptr;
+  if (!I.deleted_bm) {
+    mbx_bitmap* b = nullptr;
+    chk<chainexception::ChainException>(
+        mbx_bitmap_upload(global::SystemDefs::ctx(), I.nrows, I.deleted.data(), &b), "markedDeleted");
+    I.deleted_bm = std::make_shared<DeviceBitSet>(b);
+  }
+  return I.deleted_bm;
+}
+
+void Columnarfile::markTupleDeleted(int64_t position) {
+  Impl& I = *impl_;
+  if (position < 0 || position >= I.nrows) throw chainexception::ChainException("markTupleDeleted: position");
+  I.deleted[(size_t)(position >> 6)] |= 1ull << (position & 63);
+  I.any_deleted = true;
+  I.dirty = true;
+}
+
+}  // namespace columnar
+
+// --------------------------------------------------------------- iterator
+
+namespace iterator {
+
+mbx_cnf CnfImage::view() const {
+  mbx_cnf c;
+  c.conds = conds.data();
+  c.conj_offsets = offsets.data();
+  c.nconj = (int32_t)offsets.size() - 1;
+  return c;
+}
+
+static mbx_operand operand_of(const AttrType& t, const Operand& o, int remap_from, int remap_to) {
+  mbx_operand m;
+  memset(&m, 0, sizeof(m));
+  m.type = t.attrType;
+  if (t.attrType == AttrType::attrSymbol) {
+    if (o.symbol.relation.key != RelSpec::outer) throw InvalidRelation("Invalid relation -innerRel");
+    m.fld = (remap_from && o.symbol.offset == remap_from) ? remap_to : o.symbol.offset;
+  } else if (t.attrType == AttrType::attrInteger) {
+    m.integer = o.integer;
+  } else if (t.attrType == AttrType::attrReal) {
+    m.real = o.real;
+  } else if (t.attrType == AttrType::attrString) {
+    m.string = o.string.data();
+    m.string_len = (int32_t)o.string.size();
+  }
+  return m;
+}
+
+CnfImage flatten(CondExpr* const* filter, int remap_from, int remap_to) {
+  CnfImage img;
+  img.offsets.push_back(0);
+  if (!filter) {
+    img.offsets.clear();
+    img.offsets.push_back(0);
+    return img;  // nconj = 0: p == null
+  }
+  for (int i = 0; filter[i] != nullptr; i++) {
+    for (const CondExpr* e = filter[i]; e; e = e->next) {
+      mbx_condexpr c;
+      memset(&c, 0, sizeof(c));
+      c.op = e->op.attrOperator;
+      c.operand1 = operand_of(e->type1, e->operand1, remap_from, remap_to);
+      c.operand2 = operand_of(e->type2, e->operand2, remap_from, remap_to);
+      c.index_type = e->indexType.indexType;
+      img.conds.push_back(c);
+    }
+    img.offsets.push_back((int32_t)img.conds.size());
+  }
+  return img;
+}
+
+// ---- result batches shared by the scans: project `proj` columns of the
+// selection on the GPU, hand them out row by row
+
+struct Batch {
+  static constexpr int64_t kRows = 8192;
+};
+
+static void setup_jtuple(heap::Tuple& J, const std::vector<AttrType>& in1, const std::vector<short>& s_sizes,
+                         const std::vector<FldSpec>& proj) {
+  // TupleUtils.setup_op_tuple (R/iterator/TupleUtils.java:295-341)
+  std::vector<short> sizesT1(in1.size(), 0);
+  size_t k = 0;
+  for (size_t i = 0; i < in1.size(); i++)
+    if (in1[i].attrType == AttrType::attrString) sizesT1[i] = k < s_sizes.size() ? s_sizes[k++] : 0;
+  std::vector<AttrType> res;
+  std::vector<short> res_sizes;
+  for (const auto& f : proj) {
+    if (f.relation.key != RelSpec::outer) throw InvalidRelation("Invalid relation -innerRel");
+    if (f.offset < 1 || f.offset > (int)in1.size())
+      throw FieldNumberOutOfBoundException("projection offset " + std::to_string(f.offset));
+    res.push_back(in1[(size_t)f.offset - 1]);
+    if (in1[(size_t)f.offset - 1].attrType == AttrType::attrString) res_sizes.push_back(sizesT1[(size_t)f.offset - 1]);
+  }
+  J.setHdr(res, res_sizes);
+}
+
+static int64_t col_width(const std::vector<AttrType>& types, const std::vector<short>& sizes, int col) {
+  return types[(size_t)col].attrType == AttrType::attrString ? sizes[(size_t)col] : 4;
+}
+
+static void fill_row(heap::Tuple& J, const std::vector<AttrType>& types, const std::vector<short>& sizes,
+                     const std::vector<int32_t>& cols, const std::vector<std::vector<uint8_t>>& batch, int64_t i) {
+  for (size_t j = 0; j < cols.size(); j++) {
+    const int c = cols[j];
+    const int64_t w = col_width(types, sizes, c);
+    const uint8_t* p = batch[j].data() + i * w;
+    switch (types[(size_t)c].attrType) {
+      case AttrType::attrInteger: {
+        int32_t v;
+        memcpy(&v, p, 4);
+        J.setIntFld((int)j + 1, v);
+        break;
+      }
+      case AttrType::attrReal: {
+        float v;
+        memcpy(&v, p, 4);
+        J.setFloFld((int)j + 1, v);
+        break;
+      }
+      default:
+        J.setStrFld((int)j + 1, std::string((const char*)p, strnlen((const char*)p, (size_t)w)));
+    }
+  }
+}
+
+ColumnarFileScan::ColumnarFileScan(const std::string& file_name, const std::vector<AttrType>& in1,
+                                   const std::vector<short>& s1_sizes, short len_in1, int n_out_flds,
+                                   const std::vector<FldSpec>& proj_list, CondExpr* const* outFilter)
+    : f_(file_name), in1_(in1), perm_mat_(proj_list) {
+  if ((int)in1.size() != len_in1 || len_in1 != f_.getFieldCount())
+    throw FileScanException("ColumnarFileScan: in1/len_in1 do not match " + file_name);
+  if ((int)proj_list.size() != n_out_flds) throw FileScanException("ColumnarFileScan: n_out_flds");
+  setup_jtuple(Jtuple_, in1, s1_sizes, proj_list);
+  for (const auto& p : proj_list) proj_cols_.push_back(p.offset - 1);
+  CnfImage img = flatten(outFilter);
+  mbx_cnf cnf = img.view();
+  mbx_ctx* c = global::SystemDefs::ctx();
+  chk<PredEvalException>(mbx_plan_compile(c, f_.table(), &cnf, &plan_), "ColumnarFileScan: predicate");
+  mbx_bitmap* b = nullptr;
+  int64_t n = 0;
+  chk<FileScanException>(mbx_scan_bitmap(c, plan_, &b, &n), "ColumnarFileScan: scan");
+  sel_ = std::make_shared<columnar::DeviceBitSet>(b);
+}
+
+int64_t ColumnarFileScan::resultCount() const {
+  int64_t n = 0;
+  chk<FileScanException>(mbx_scan_count(global::SystemDefs::ctx(), plan_, &n), "ColumnarFileScan: count");
+  return n;
+}
+
+void ColumnarFileScan::next_batch() {
+  mbx_ctx* c = global::SystemDefs::ctx();
+  if (!cur_)
+    chk<FileScanException>(mbx_cursor_open(c, f_.table(), sel_->get(), proj_cols_.data(), (int32_t)proj_cols_.size(),
+                                           &cur_),
+                           "ColumnarFileScan: materialise");
+  const auto types = f_.getAttributeTypes();
+  const auto sizes = f_.getAttrSizes();
+  batch_.resize(proj_cols_.size());
+  std::vector<void*> ptrs(proj_cols_.size());
+  for (size_t j = 0; j < proj_cols_.size(); j++) {
+    batch_[j].resize((size_t)(Batch::kRows * col_width(types, sizes, proj_cols_[j])));
+    ptrs[j] = batch_[j].data();
+  }
+  batch_ids_.resize((size_t)Batch::kRows);
+  chk<FileScanException>(mbx_cursor_next(cur_, Batch::kRows, batch_ids_.data(), ptrs.data(), &batch_n_),
+                         "ColumnarFileScan: get_next");
+  batch_i_ = 0;
+}
+
+heap::Tuple* ColumnarFileScan::get_next() {
+  if (batch_i_ >= batch_n_) {
+    next_batch();
+    if (batch_n_ == 0) return nullptr;
+  }
+  fill_row(Jtuple_, f_.getAttributeTypes(), f_.getAttrSizes(), proj_cols_, batch_, batch_i_);
+  batch_i_++;
+  return &Jtuple_;
+}
+
+global::TID ColumnarFileScan::get_next_tid() {
+  global::TID tid;
+  tid.numRIDs = f_.getFieldCount();
+  if (batch_i_ >= batch_n_) {
+    next_batch();
+    if (batch_n_ == 0) return tid;  // position -1: end of scan (null in Java)
+  }
+  tid.position = batch_ids_[(size_t)batch_i_++];
+  return tid;
+}
+
+void ColumnarFileScan::close() {
+  if (!closeFlag) {
+    if (cur_) mbx_cursor_close(cur_);
+    cur_ = nullptr;
+    sel_.reset();
+    if (plan_) mbx_plan_free(plan_);
+    plan_ = nullptr;
+    closeFlag = true;
+  }
+}
+
+void ColumnarFileScan::restart() {
+  if (cur_) chk<FileScanException>(mbx_cursor_restart(cur_), "restart");
+  batch_n_ = batch_i_ = 0;
+}
+
+int ColumnarFileScan::getTupleSize() { return Jtuple_.size(); }
+
+ColumnarColumnScan::ColumnarColumnScan(columnar::Columnarfile* cf, int colNo, int n_out_flds,
+                                       const std::vector<int>& out_indexes, const std::vector<FldSpec>& proj_list,
+                                       CondExpr* const* outFilter) {
+  (void)proj_list;
+  // the CondExpr refers to the scanned column as field 1
+  // (Query.buildQueryCondExprColscan, R/input/Query.java:337-360)
+  std::vector<FldSpec> proj;
+  for (int i = 0; i < n_out_flds; i++) proj.push_back(FldSpec(RelSpec(RelSpec::outer), out_indexes.at((size_t)i) + 1));
+  // remap field 1 -> colNo + 1 by rewriting a copy of the chain
+  std::vector<std::vector<CondExpr>> copies;
+  std::vector<CondExpr*> heads;
+  for (int i = 0; outFilter && outFilter[i]; i++) {
+    std::vector<CondExpr> chain;
+    for (const CondExpr* e = outFilter[i]; e; e = e->next) chain.push_back(*e);
+    copies.push_back(chain);
+  }
+  for (auto& chain : copies) {
+    for (size_t k = 0; k < chain.size(); k++) {
+      if (chain[k].type1.attrType == AttrType::attrSymbol && chain[k].operand1.symbol.offset == 1)
+        chain[k].operand1.symbol.offset = colNo + 1;
+      if (chain[k].type2.attrType == AttrType::attrSymbol && chain[k].operand2.symbol.offset == 1)
+        chain[k].operand2.symbol.offset = colNo + 1;
+      chain[k].next = k + 1 < chain.size() ? &chain[k + 1] : nullptr;
+    }
+    heads.push_back(chain.empty() ? nullptr : &chain[0]);
+  }
+  heads.push_back(nullptr);
+  inner_.reset(new ColumnarFileScan(cf->get_fileName(), cf->getAttributeTypes(), cf->getStringSizes(),
+                                    (short)cf->getFieldCount(), n_out_flds, proj,
+                                    outFilter ? heads.data() : nullptr));
+}
+
+heap::Tuple* ColumnarColumnScan::get_next() { return inner_->get_next(); }
+global::TID ColumnarColumnScan::get_next_tid() { return inner_->get_next_tid(); }
+void ColumnarColumnScan::close() {
+  if (!closeFlag) {
+    inner_->close();
+    closeFlag = true;
+  }
+}
+void ColumnarColumnScan::restart() { inner_->restart(); }
+int ColumnarColumnScan::getTupleSize() { return inner_->getTupleSize(); }
+
+}  // namespace iterator
+
+// ------------------------------------------------------------------ index
+
+namespace index {
+
+using columnar::BitSetPtr;
+
+std::vector<BitSetPtr> ColumnIndexScan::valueBitmaps(const columnar::Columnarfile& cf, int colNo, const CondExpr& e) {
+  const auto types = cf.getAttributeTypes();
+  const bool str = types.at((size_t)colNo).attrType == AttrType::attrString;
+  const std::string lit = str ? e.operand2.string : columnar::int_key(e.operand2.integer);
+  const int op = e.op.attrOperator;
+  std::vector<BitSetPtr> out;
+  using O = global::AttrOperator;
+  // symbol = value (R/index/ColumnIndexScan.java:660-668)
+  if (op == O::aopEQ || op == O::aopLE || op == O::aopGE) out.push_back(cf.getBitmapIndex(colNo, lit));
+  if (op == O::aopLT || op == O::aopLE || op == O::aopGT || op == O::aopGE || op == O::aopNE) {
+    for (const std::string& other : cf.getBitmapValues(colNo)) {
+      int c;  // sign(value.compareTo(other))
+      if (str) c = java_compare(lit, other);
+      else {
+        const int a = e.operand2.integer, b = atoi(other.c_str());
+        c = a == b ? 0 : (a < b ? -1 : 1);
+      }
+      bool take = false;
+      if ((op == O::aopLT || op == O::aopLE) && c > 0) take = true;   // :671-688
+      if ((op == O::aopGT || op == O::aopGE) && c < 0) take = true;   // :691-709
+      if (op == O::aopNE && c != 0) take = true;                      // :712-730
+      if (take) out.push_back(cf.getBitmapIndex(colNo, other));
+    }
+  }
+  return out;  // aopNOT / aopNOP / opRANGE: no value, an empty BitSet
+}
+
+// OR of value bitmaps AND NOT deleted, as one device CNF launch
+static BitSetPtr or_bitmaps(const columnar::Columnarfile& cf, const std::vector<std::vector<BitSetPtr>>& conjuncts) {
+  std::vector<mbx_bitmap*> bms;
+  std::vector<int32_t> offs{0};
+  for (const auto& conj : conjuncts) {
+    for (const auto& b : conj) bms.push_back(b->get());
+    offs.push_back((int32_t)bms.size());
+  }
+  mbx_bitmap* out = nullptr;
+  int64_t n = 0;
+  BitSetPtr del = cf.getMarkedDeleted();
+  chk<IndexException>(mbx_bitmap_cnf(global::SystemDefs::ctx(), cf.getTupleCnt(), bms.data(), offs.data(),
+                                     (int32_t)conjuncts.size(), del ? del->get() : nullptr, &out, &n),
+                      "index BitSet CNF");
+  return std::make_shared<columnar::DeviceBitSet>(out);
+}
+
+static void materialize_all(const columnar::Columnarfile& cf, const BitSetPtr& sel, const std::vector<int>& cols,
+                            std::vector<int64_t>& ids, std::vector<std::vector<uint8_t>>& vals) {
+  const auto types = cf.getAttributeTypes();
+  const auto sizes = cf.getAttrSizes();
+  const int64_t n = sel->cardinality();
+  ids.assign((size_t)(n > 0 ? n : 1), 0);
+  vals.assign(cols.size(), {});
+  std::vector<void*> ptrs(cols.size());
+  std::vector<int32_t> pc(cols.begin(), cols.end());
+  for (size_t j = 0; j < cols.size(); j++) {
+    vals[j].resize((size_t)((n > 0 ? n : 1) * iterator::col_width(types, sizes, cols[j])));
+    ptrs[j] = vals[j].data();
+  }
+  int64_t got = 0;
+  chk<IndexException>(mbx_materialize(global::SystemDefs::ctx(), cf.table(), sel->get(), pc.data(), (int32_t)pc.size(),
+                                      ids.data(), ptrs.data(), (int64_t)ids.size(), &got),
+                      "late materialisation");
+  ids.resize((size_t)got);
+}
+
+ColumnIndexScan::ColumnIndexScan(IndexType index, columnar::Columnarfile* cf, const std::string& indName,
+                                 const std::vector<AttrType>& types, const std::vector<short>& str_sizes,
+                                 int noInFlds, int noOutFlds, const std::vector<int>& outIndexes,
+                                 const std::vector<FldSpec>& outFlds, CondExpr* const* selects, int fldNum,
+                                 bool indexOnly)
+    : f_(cf), colNo_(fldNum - 1), outIndexes_(outIndexes), types_(types), index_only_(indexOnly) {
+  (void)indName;
+  (void)noInFlds;
+  if (index.indexType != IndexType::Bitmap)
+    throw UnknownIndexTypeException("only the Bitmap branch of ColumnIndexScan runs on the GPU (B-tree: out of scope)");
+  if (!selects || !selects[0]) throw IndexException("ColumnIndexScan: no selection");
+  if ((int)outFlds.size() != noOutFlds) throw IndexException("ColumnIndexScan: noOutFlds");
+  sel_ = *selects[0];
+  sel_.next = nullptr;
+  std::vector<AttrType> otypes;
+  std::vector<short> osizes;
+  const auto sizes = cf->getAttrSizes();
+  for (int c : outIndexes) {
+    otypes.push_back(types.at((size_t)c));
+    if (types[(size_t)c].attrType == AttrType::attrString) osizes.push_back(sizes[(size_t)c]);
+  }
+  (void)str_sizes;
+  Jtuple_.setHdr(otypes, osizes);
+  positions_ = or_bitmaps(*cf, {valueBitmaps(*cf, colNo_, sel_)});
+}
+
+ColumnIndexScan::ColumnIndexScan(IndexType index, columnar::Columnarfile* cf, const std::string& indName,
+                                 const std::vector<AttrType>& types, const std::vector<short>& str_sizes, int noInFlds,
+                                 CondExpr* const* selects, int fldNum)
+    : ColumnIndexScan(index, cf, indName, types, str_sizes, noInFlds, 0, {}, {}, selects, fldNum, false) {}
+
+BitSetPtr ColumnIndexScan::getPositionsOfIndexScan() { return positions_; }
+
+void ColumnIndexScan::materialize() {
+  if (ready_) return;
+  materialize_all(*f_, positions_, outIndexes_, ids_, vals_);
+  ready_ = true;
+}
+
+heap::Tuple* ColumnIndexScan::get_next() {
+  materialize();
+  if (next_ >= (int64_t)ids_.size()) return nullptr;
+  if (index_only_) {
+    // only the key is returned (R/index/ColumnIndexScan.java:512-565)
+    std::vector<AttrType> t{types_.at((size_t)colNo_)};
+    std::vector<short> s;
+    if (t[0].attrType == AttrType::attrString) s.push_back(f_->getAttrSizes()[(size_t)colNo_]);
+    Jtuple_.setHdr(t, s);
+    if (t[0].attrType == AttrType::attrString) Jtuple_.setStrFld(1, sel_.operand2.string);
+    else Jtuple_.setIntFld(1, sel_.operand2.integer);
+    next_++;
+    return &Jtuple_;
+  }
+  std::vector<int32_t> cols(outIndexes_.begin(), outIndexes_.end());
+  iterator::fill_row(Jtuple_, f_->getAttributeTypes(), f_->getAttrSizes(), cols, vals_, next_);
+  next_++;
+  return &Jtuple_;
+}
+
+global::TID ColumnIndexScan::get_next_tid() {
+  materialize();
+  global::TID tid;
+  tid.numRIDs = f_->getFieldCount();
+  if (next_ < (int64_t)ids_.size()) tid.position = ids_[(size_t)next_++];
+  return tid;
+}
+
+void ColumnIndexScan::close() { closeFlag = true; }
+void ColumnIndexScan::restart() { next_ = 0; }
+int ColumnIndexScan::getTupleSize() { return Jtuple_.size(); }
+
+ColumnarIndexScan::ColumnarIndexScan(columnar::Columnarfile* cf, const std::vector<int>& fldNums,
+                                     const std::vector<IndexType>& indexTypes,
+                                     const std::vector<std::string>& indNames, const std::vector<AttrType>& types,
+                                     const std::vector<short>& str_sizes, int noInFlds, int noOutFlds,
+                                     const std::vector<int>& out_indexes, const std::vector<FldSpec>& outFlds,
+                                     CondExpr* const* selects, bool indexOnly)
+    : f_(cf), outIndexes_(out_indexes), types_(types) {
+  (void)fldNums;
+  (void)indexTypes;
+  (void)indNames;
+  (void)str_sizes;
+  (void)noInFlds;
+  (void)indexOnly;
+  if ((int)outFlds.size() != noOutFlds) throw IndexException("ColumnarIndexScan: noOutFlds");
+  if (!selects || !selects[0]) throw IndexException("ColumnarIndexScan: no selection");
+  std::vector<AttrType> otypes;
+  std::vector<short> osizes;
+  const auto sizes = cf->getAttrSizes();
+  for (int c : out_indexes) {
+    otypes.push_back(types.at((size_t)c));
+    if (types[(size_t)c].attrType == AttrType::attrString) osizes.push_back(sizes[(size_t)c]);
+  }
+  Jtuple_.setHdr(otypes, osizes);
+
+  // constraint keys (column + op + literal + index type), as the reference's
+  // duplicate-constraint string (:137-141)
+  struct Term {
+    const CondExpr* e;
+    int col;
+    std::string key;
+  };
+  std::vector<std::vector<Term>> conj;
+  std::map<std::string, int> occurrences;
+  for (int i = 0; selects[i]; i++) {
+    std::vector<Term> ts;
+    for (const CondExpr* e = selects[i]; e; e = e->next) {
+      int col;
+      if (e->type1.attrType == AttrType::attrSymbol && e->type2.attrType != AttrType::attrSymbol)
+        col = e->operand1.symbol.offset - 1;
+      else if (e->type2.attrType == AttrType::attrSymbol && e->type1.attrType != AttrType::attrSymbol)
+        col = e->operand2.symbol.offset - 1;
+      else
+        throw IndexException("IndexScan.java: invalid constraint");
+      const std::string lit = e->type2.attrType == AttrType::attrInteger ? std::to_string(e->operand2.integer)
+                                                                          : e->operand2.string;
+      Term t{e, col, cf->indexToColName(col) + e->op.toString() + lit + e->indexType.toString()};
+      occurrences[t.key]++;
+      ts.push_back(t);
+    }
+    conj.push_back(ts);
+  }
+  auto term_bitmaps = [&](const Term& t) -> std::vector<BitSetPtr> {
+    if (t.e->indexType.indexType == IndexType::B_Index) {
+      // B-tree branch: same positions as the predicate itself; evaluated by
+      // the scan kernel (the B-tree access path is out of scope)
+      CondExpr one = *t.e;
+      one.next = nullptr;
+      CondExpr* arr[2] = {&one, nullptr};
+      iterator::CnfImage img = iterator::flatten(arr);
+      mbx_cnf cnf = img.view();
+      mbx_plan* p = nullptr;
+      chk<IndexException>(mbx_plan_compile(global::SystemDefs::ctx(), cf->table(), &cnf, &p), "B_Index term");
+      mbx_bitmap* b = nullptr;
+      int64_t n = 0;
+      const int rc = mbx_scan_bitmap(global::SystemDefs::ctx(), p, &b, &n);
+      mbx_plan_free(p);
+      chk<IndexException>(rc, "B_Index term scan");
+      return {std::make_shared<columnar::DeviceBitSet>(b)};
+    }
+    if (!cf->bitmapIndexExists(t.col))
+      throw IndexException("Bitmap index does not exist on column " + cf->indexToColName(t.col));
+    return ColumnIndexScan::valueBitmaps(*cf, t.col, *t.e);
+  };
+
+  bool dup = false;
+  for (const auto& kv : occurrences) dup = dup || kv.second > 1;
+  size_t total = 0;
+  std::vector<std::vector<BitSetPtr>> lists;
+  if (!dup) {
+    for (const auto& ts : conj) {
+      std::vector<BitSetPtr> l;
+      for (const auto& t : ts) {
+        auto v = term_bitmaps(t);
+        l.insert(l.end(), v.begin(), v.end());
+      }
+      total += l.size();
+      lists.push_back(l);
+    }
+  }
+  if (!dup && total <= 64) {
+    // one k_bitmap_cnf launch: AND_c OR_k bitmaps AND NOT deleted
+    output_ = or_bitmaps(*cf, lists);
+    fused_ = true;
+    return;
+  }
+  // Step-wise form, keeping the reference's object semantics (:130-181):
+  // one positions BitSet per conjunct (conjunct 0's is outputPositions and
+  // is AND-ed in place); a repeated constraint ORs in the cached *object*.
+  std::vector<BitSetPtr> objs;
+  std::map<std::string, size_t> cache;
+  mbx_ctx* c = global::SystemDefs::ctx();
+  auto combine = [&](int op, const BitSetPtr& a, const BitSetPtr& b) {
+    mbx_bitmap* r = nullptr;
+    int64_t n = 0;
+    chk<IndexException>(mbx_bitmap_combine(c, op, a->get(), b->get(), &r, &n), "BitSet combine");
+    return std::make_shared<columnar::DeviceBitSet>(r);
+  };
+  for (size_t i = 0; i < conj.size(); i++) {
+    BitSetPtr positions = cf->getBitmapIndex(-1, "");  // empty BitSet
+    objs.push_back(positions);
+    for (const auto& t : conj[i]) {
+      const bool in_cache = cache.count(t.key) > 0;
+      const bool dflag = in_cache ? true : occurrences[t.key] > 1;
+      if (!dflag || !in_cache) {
+        BitSetPtr term = or_bitmaps(*cf, {term_bitmaps(t)});  // getPositionsOfIndexScan
+        objs[i] = combine(MBX_BM_OR, objs[i], term);
+        if (dflag) cache[t.key] = i;
+      } else {
+        objs[i] = combine(MBX_BM_OR, objs[i], objs[cache[t.key]]);
+      }
+    }
+    if (i > 0) objs[0] = combine(MBX_BM_AND, objs[0], objs[i]);
+  }
+  output_ = objs[0];
+}
+
+heap::Tuple* ColumnarIndexScan::get_next() {
+  if (!ready_) {
+    materialize_all(*f_, output_, outIndexes_, ids_, vals_);
+    ready_ = true;
+  }
+  if (next_ >= (int64_t)ids_.size()) return nullptr;
+  std::vector<int32_t> cols(outIndexes_.begin(), outIndexes_.end());
+  iterator::fill_row(Jtuple_, f_->getAttributeTypes(), f_->getAttrSizes(), cols, vals_, next_);
+  next_++;
+  return &Jtuple_;
+}
+
+void ColumnarIndexScan::close() { closeFlag = true; }
+void ColumnarIndexScan::restart() { next_ = 0; }
+int ColumnarIndexScan::getTupleSize() { return Jtuple_.size(); }
+
+}  // namespace index
+
+}  // namespace minibase

@@ -27,6 +27,10 @@
 
 #include "../../include/mbx.h"
 
+// Everything lives in `minibase::` (the Java packages become nested
+// namespaces; `index` would otherwise collide with POSIX index(3)).
+namespace minibase {
+
 namespace chainexception {
 // R/chainexception/ChainException.java:11 -- every checked exception's root.
 class ChainException : public std::runtime_error {
@@ -351,3 +355,5 @@ class ColumnarIndexScan : public iterator::Iterator {
   bool fused_ = false;
 };
 }  // namespace index
+
+}  // namespace minibase

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3,4,5,6")
     ap.add_argument("--tpb", default="0,24,48,96,191,382")
     ap.add_argument("--generic", action="store_true")
+    ap.add_argument("--fin", default="0", help="MBX_FIN_MODE values: 0 write-through, 1 fences, 2 separate")
     args = ap.parse_args()
 
     import torch
@@ -49,14 +50,17 @@ def main():
     ext = torch.cuda.ExternalStream(ctx.stream)
     out = torch.zeros(args.launches, dtype=torch.int64, device="cuda")
 
-    configs = [(v, tp, False) for v in map(int, args.variants.split(",")) for tp in map(int, args.tpb.split(","))]
+    fins = list(map(int, args.fin.split(",")))
+    configs = [(v, tp, False, f) for v in map(int, args.variants.split(",")) for tp in map(int, args.tpb.split(","))
+               for f in fins]
     if args.generic:
-        configs += [(0, tp, True) for tp in map(int, args.tpb.split(","))]
+        configs += [(0, tp, True, fins[0]) for tp in map(int, args.tpb.split(","))]
     res = {c: [] for c in configs}
     for r in range(args.rounds):
         for c in configs:
-            v, tp, gen = c
+            v, tp, gen, fin = c
             os.environ["MBX_SCAN_VARIANT"] = str(v)
+            os.environ["MBX_FIN_MODE"] = str(fin)
             if tp:
                 os.environ["MBX_TILES_PER_BLOCK"] = str(tp)
             else:
@@ -75,9 +79,9 @@ def main():
             assert bool((got == want).all()), (c, got[:4], want)
             res[c].append(statistics.median(ts))
     for c in configs:
-        v, tp, gen = c
+        v, tp, gen, fin = c
         med = statistics.median(res[c])
-        print(json.dumps({"variant": v, "tiles_per_block": tp or "default", "generic": gen,
+        print(json.dumps({"variant": v, "tiles_per_block": tp or "default", "generic": gen, "fin_mode": fin,
                           "median_ms": med, "min_ms": min(res[c]),
                           "gbs": 8 * n / (med * 1e-3) / 1e9}), flush=True)
     ctx.close()
