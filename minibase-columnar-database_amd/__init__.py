@@ -10,5 +10,6 @@ Layout
 The directory name carries hyphens, so import it through mbx_pkg.load()
 (repository root), which registers it as the module `mbx_amd`.
 """
+from . import dist  # noqa: F401
 from . import mbx  # noqa: F401
 from .mbx import MbxError, Context, device_count, lib  # noqa: F401
