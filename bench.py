@@ -89,11 +89,18 @@ def main():
 
     import mbx_pkg
 
-    torch.cuda.set_device(local_rank)
+    # rehearsal knobs (never set by the driver): MBX_BENCH_BACKEND=gloo and
+    # MBX_BENCH_SAME_DEVICE=1 run N ranks on one GPU to exercise the N>1 flow
+    backend = os.environ.get("MBX_BENCH_BACKEND", "nccl")
+    device = 0 if os.environ.get("MBX_BENCH_SAME_DEVICE") == "1" else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
     m = mbx_pkg.load()
-    ctx = m.Context(local_rank)
+    ctx = m.Context(device)
     n = args.rows
 
     # synthetic C3 shard, generated in HBM: 4 x int32 uniform [0, 2^20)

@@ -695,23 +695,42 @@ __global__ __launch_bounds__(kBlock) void k_materialize(const uint64_t* __restri
   __syncthreads();
   int64_t off = seg_offsets[blockIdx.x];
   for (int k = 0; k < wave; ++k) off += wcount[k];
-  for (int64_t w = a0; w < a1; ++w) {
-    const uint64_t m = words[w];
-    if (m == 0) continue;
-    const bool bit = (m >> lane) & 1ull;
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (bit) {
-      const int64_t pos = off + below;
-      const int64_t row = w * 64 + lane;
-      if (ids) ids[pos] = row_offset + row;
-      for (int j = 0; j < M.nproj; ++j) {
-        const int sw = M.proj[j].stride_w;
-        const uint32_t* src = (const uint32_t*)M.proj[j].base + row * sw;
-        uint32_t* dst = (uint32_t*)M.out[j] + pos * sw;
-        for (int k = 0; k < sw; ++k) dst[k] = src[k];
+  // 64 words per step, loaded coalesced (lane = word); an exclusive scan of
+  // their popcounts gives each word's output slot; then the wave visits only
+  // the non-zero words, lane = bit, so positions and values are written
+  // densely and in ascending order.
+  for (int64_t base = a0; base < a1; base += 64) {
+    const uint64_t mw = base + lane < a1 ? words[base + lane] : 0ull;
+    const uint32_t pc = (uint32_t)__popcll(mw);
+    uint32_t incl = pc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    const uint32_t excl = incl - pc;
+    const uint32_t total = __shfl(incl, 63);
+    uint64_t nz = __ballot(mw != 0ull);
+    while (nz) {
+      const int j = __builtin_ctzll(nz);
+      nz &= nz - 1ull;
+      const uint64_t m = __shfl(mw, j);
+      const uint32_t slot = __shfl(excl, j);
+      if ((m >> lane) & 1ull) {
+        const uint32_t below =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const int64_t pos = off + slot + below;
+        const int64_t row = (base + j) * 64 + lane;
+        if (ids) ids[pos] = row_offset + row;
+        for (int p = 0; p < M.nproj; ++p) {
+          const int sw = M.proj[p].stride_w;
+          const uint32_t* src = (const uint32_t*)M.proj[p].base + row * sw;
+          uint32_t* dst = (uint32_t*)M.out[p] + pos * sw;
+          for (int k = 0; k < sw; ++k) dst[k] = src[k];
+        }
       }
     }
-    off += __popcll(m);
+    off += total;
   }
 }
 
