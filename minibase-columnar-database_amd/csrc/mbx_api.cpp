@@ -21,6 +21,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <deque>
 #include <vector>
 
 #include "mbx_internal.hpp"
@@ -63,6 +64,8 @@ struct mbx_ctx {
   int64_t* dcount = nullptr;
   int32_t* dnan = nullptr;
   uint32_t* ticket = nullptr;   // in-launch finalize ticket (always 0 between launches)
+  int64_t* ids_scratch = nullptr;  // positions for a gather whose caller wants no positions
+  int64_t ids_cap = 0;
   void* pinned = nullptr;       // 256 bytes of pinned host scratch
 };
 
@@ -88,6 +91,7 @@ struct PlanVariant {
   int32_t agg_col = -1;  // -1: filter only
   KPlan* dev = nullptr;
   int32_t fast_k = 0;
+  int32_t fast_ks = 0;
   int32_t agg_kind = kInt;
 };
 
@@ -96,8 +100,9 @@ struct mbx_plan {
   const mbx_table* t = nullptr;
   KPlan host{};
   std::vector<int32_t> slot_col;  // table column of each slot
-  bool all_4byte_literal = true;  // every term `column OP literal` on 4-byte columns
-  std::vector<PlanVariant> variants;
+  bool all_literal = true;        // every term is `column OP literal`
+  bool str_lit_fits16 = true;     // every string literal is <= 16 bytes
+  std::deque<PlanVariant> variants;
 };
 
 struct mbx_bitmap {
@@ -265,6 +270,7 @@ extern "C" int mbx_free(mbx_ctx* c) {
   hipFree(c->dcount);
   hipFree(c->dnan);
   hipFree(c->ticket);
+  hipFree(c->ids_scratch);
   if (c->pinned) hipHostFree(c->pinned);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -568,7 +574,7 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
           const int s2 = slot_for(p, o2.fld - 1);
           if (s2 < 0) return fail(MBX_E_UNSUPPORTED, "plan: more than %d distinct columns", kMaxCols);
           kt.rhs = s2;
-          p->all_4byte_literal = false;
+          p->all_literal = false;
         }
       } else {
         coln = &o2;  // literal on the left: compare column with literal, operator mirrored
@@ -586,7 +592,7 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
           if (rc) return rc;
         }
       }
-      if (ctype == MBX_ATTR_STRING) p->all_4byte_literal = false;
+      if (ctype == MBX_ATTR_STRING && kt.rhs < 0 && kt.swords > 4) p->str_lit_fits16 = false;
       if (ctype == MBX_ATTR_REAL) p->host.has_real = 1;
       p->host.terms[nterms++] = kt;
     }
@@ -631,13 +637,37 @@ static int plan_variant(mbx_plan* p, int32_t agg_col, PlanVariant** out) {
     }
     kp.agg_slot = s;
   }
-  bool four = p->all_4byte_literal && p->t->aligned16;
-  for (size_t i = 0; i < slots.size(); i++)
-    if (p->t->cols[slots[i]].attr_type == MBX_ATTR_STRING) four = false;
+  // Fast kernel eligibility: every term `column OP literal`, 16-byte aligned
+  // columns, <= 4 four-byte slots and <= 2 char(13..16) slots whose literals
+  // fit 16 bytes.  Slots are renumbered 4-byte first, strings after.
+  bool fast = p->all_literal && p->str_lit_fits16 && p->t->aligned16;
   const char* force = getenv("MBX_FORCE_GENERIC");
-  if (force && force[0] == '1') four = false;
-  v.fast_k = (four && !slots.empty() && slots.size() <= 4) ? (int32_t)slots.size() : 0;
-  if (four && slots.empty()) {
+  if (force && force[0] == '1') fast = false;
+  std::vector<int> four, wide;
+  for (size_t i = 0; i < slots.size(); i++) {
+    const TCol& tc = p->t->cols[slots[i]];
+    if (tc.attr_type != MBX_ATTR_STRING) four.push_back((int)i);
+    else if (tc.stride_w == 4) wide.push_back((int)i);
+    else fast = false;
+  }
+  if (four.size() > 4 || wide.size() > 2 || four.size() + wide.size() > 4) fast = false;
+  if (fast && !slots.empty()) {
+    std::vector<int> order(four);
+    order.insert(order.end(), wide.begin(), wide.end());
+    std::vector<int> newpos(slots.size());
+    KPlan q = kp;
+    for (size_t k = 0; k < order.size(); k++) {
+      newpos[(size_t)order[k]] = (int)k;
+      q.cols[k] = kp.cols[order[k]];
+    }
+    for (int ti = 0; ti < kp.nterms; ti++) q.terms[ti].lhs = newpos[(size_t)kp.terms[ti].lhs];
+    if (kp.agg_slot >= 0) q.agg_slot = newpos[(size_t)kp.agg_slot];
+    kp = q;
+    v.fast_k = (int32_t)four.size();
+    v.fast_ks = (int32_t)wide.size();
+  }
+  const bool all4 = fast && wide.empty();
+  if (all4 && slots.empty()) {
     // no column referenced (no filter, or only constant terms): slot 0 is
     // any 4-byte column so the fast kernel has something to stream
     for (size_t j = 0; j < p->t->cols.size(); j++)
@@ -656,7 +686,7 @@ static int plan_variant(mbx_plan* p, int32_t agg_col, PlanVariant** out) {
     hipFree(v.dev);
     return fail(MBX_E_DEVICE, "plan upload: %s", hipGetErrorString(e));
   }
-  p->variants.push_back(v);
+  p->variants.push_back(v);  // std::deque: earlier PlanVariant pointers stay valid
   *out = &p->variants.back();
   return MBX_OK;
 }
@@ -705,6 +735,7 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.partials = parts;
   L.mode = mode;
   L.fast_k = v.fast_k;
+  L.fast_ks = v.fast_ks;
   L.agg_kind = v.agg_kind;
   L.ticket = c->ticket;
   L.count_out = count_out;
@@ -1100,10 +1131,22 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
     pc[j].pad_ = 0;
   }
   if (t && sel->nbits != t->nrows) return fail(MBX_E_INVALID, "materialize: bitmap/table size mismatch");
+  if (!dev_total) dev_total = c->dcount + 1;
+  if (!dev_ids) {
+    // positions are the gather's input: keep them in context scratch
+    if (c->ids_cap < sel->nbits) {
+      if (c->ids_scratch) HIPCHK(hipFree(c->ids_scratch));
+      c->ids_scratch = nullptr;
+      c->ids_cap = 0;
+      HIPCHK(hipMalloc(&c->ids_scratch, sizeof(int64_t) * (size_t)(sel->nbits > 0 ? sel->nbits : 1)));
+      c->ids_cap = sel->nbits;
+    }
+    dev_ids = c->ids_scratch;
+  }
   HIPCHK(launch_seg_scan(sel->segs, sel->nseg, sel->seg_off, dev_total, c->stream));
   if (sel->nwords > 0)
     HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->seg_off, row_offset, dev_ids, pc, dev_out, nproj,
-                              c->stream));
+                              dev_total, c->stream));
   return MBX_OK;
 }
 

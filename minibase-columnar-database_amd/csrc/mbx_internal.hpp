@@ -102,7 +102,8 @@ struct ScanLaunch {
   uint64_t* out_words;        // device or null
   Partial* partials;          // device, one per block
   int32_t mode;
-  int32_t fast_k;             // >0: fast kernel over K 4-byte slots; 0: generic
+  int32_t fast_k;             // fast kernel: 4-byte slots 0..K-1 (fast_k + fast_ks == 0: generic)
+  int32_t fast_ks;            // fast kernel: 16-byte string slots K..K+KS-1
   int32_t agg_kind;           // kInt / kReal when mode == kModeAgg
   // in-launch finalize: the last block to arrive on `ticket` reduces all
   // partials in block order (release/acquire hand-off, zeroed by that block)
@@ -149,7 +150,8 @@ hipError_t launch_seg_scan(const Partial* seg_parts, int64_t nseg, int64_t* seg_
                            hipStream_t s);
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                               const int64_t* seg_offsets, int64_t row_offset, int64_t* ids,
-                              const ProjCol* proj, void* const* out, int32_t nproj, hipStream_t s);
+                              const ProjCol* proj, void* const* out, int32_t nproj, const int64_t* total,
+                              hipStream_t s);
 hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
                               int32_t nvalues,
                               int32_t value_words, uint64_t* const* outs, int64_t words_per_block, hipStream_t s);

@@ -289,11 +289,34 @@ __device__ __forceinline__ uint64_t pack_word16(uint32_t nib, int lane) {
 // Each wave streams whole 256-row tiles of its block's segment: one
 // global_load_dwordx4 per column per tile, terms folded into per-row
 // conjunct bitmasks (cb), the CNF holds when cb == all_conj.
-// per-tile body shared by every unroll depth: v holds the tile's K columns
-// (4 rows per lane); folds the CNF, applies deleted rows and emits the
-// requested output.
-template <int K, int MODE, bool DEL>
-__device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const int32_t (&v)[K][4],
+// One tile's column data in registers: K 4-byte slots (4 rows per lane) and
+// KS 16-byte string slots (char(13..16): 4 rows x 4 words per lane).
+template <int K, int KS>
+struct TileRegs {
+  int32_t v[K > 0 ? K : 1][4];
+  uint32_t s[KS > 0 ? KS : 1][4][4];
+};
+
+// String.compareTo sign of four zero-padded 16-byte rows against a literal of
+// <= 4 words (big-endian word order = modified-UTF-8 byte order)
+__device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const uint32_t (&lit)[4], int32_t (&c)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t x = __builtin_bswap32(rows[j][i]);
+      const int32_t d = x < lit[i] ? -1 : (x > lit[i] ? 1 : 0);
+      r = r != 0 ? r : d;
+    }
+    c[j] = r;
+  }
+}
+
+// per-tile body shared by every unroll depth: folds the CNF, applies deleted
+// rows and emits the requested output.
+template <int K, int KS, int MODE, bool DEL>
+__device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, KS>& D,
                                           int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
                                           Acc& acc, uint64_t& wave_count) {
   const int64_t nrows = L.nrows;
@@ -303,26 +326,39 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
   for (int ti = 0; ti < nterms; ++ti) {
     const KTerm& T = P->terms[ti];
     const int lhs = T.lhs;
-    int32_t a[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = v[0][j];
-#pragma unroll
-    for (int s = 1; s < K; ++s)
-      if (lhs == s) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = v[s][j];
-      }
     bool r[4];
-    if (T.kind == kInt) {
-      cmp4<int32_t>(T.op, a, T.ilit, r);
-    } else {
-      float f[4];
+    if (KS > 0 && T.kind == kStr) {
+      uint32_t lit[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        f[j] = __int_as_float(a[j]);
-        acc.nan |= (f[j] != f[j]) && (row0 + j < nrows);
+      for (int i = 0; i < 4; ++i) lit[i] = i < T.swords ? __builtin_bswap32(P->pool[T.soff + i]) : 0u;
+      int32_t c[4];
+      if (KS == 1 || lhs == K) {
+        str16_cmp4(D.s[0], lit, c);
+      } else {
+        str16_cmp4(D.s[KS > 1 ? 1 : 0], lit, c);
       }
-      cmp4<float>(T.op, f, T.flit, r);
+      cmp4<int32_t>(T.op, c, 0, r);
+    } else {
+      int32_t a[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
+#pragma unroll
+      for (int s = 1; s < K; ++s)
+        if (lhs == s) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
+        }
+      if (T.kind == kInt) {
+        cmp4<int32_t>(T.op, a, T.ilit, r);
+      } else {
+        float f[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f[j] = __int_as_float(a[j]);
+          acc.nan |= (f[j] != f[j]) && (row0 + j < nrows);
+        }
+        cmp4<float>(T.op, f, T.flit, r);
+      }
     }
     const uint32_t bit = T.conj_bit;
 #pragma unroll
@@ -346,15 +382,15 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) wave_count += __popcll(__ballot(p[j]));
-  if (MODE == kModeAgg) {
+  if (MODE == kModeAgg && K > 0) {
     int32_t g[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) g[j] = v[0][j];
+    for (int j = 0; j < 4; ++j) g[j] = D.v[0][j];
 #pragma unroll
     for (int s = 1; s < K; ++s)
       if (agg_slot == s) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) g[j] = v[s][j];
+        for (int j = 0; j < 4; ++j) g[j] = D.v[s][j];
       }
     if (agg_real) {
 #pragma unroll
@@ -383,14 +419,14 @@ __device__ __forceinline__ v4i load16(const int32_t* p) {
   return *reinterpret_cast<const v4i*>(p);
 }
 
-// U tiles per wave iteration: all U x K 16-byte loads are issued before the
-// first compare, so each wave keeps U*K*1 KiB in flight.
+// U tiles per wave iteration: all loads of the U tiles are issued before the
+// first compare (U x (K + 4 KS) x 1 KiB in flight per wave).
 // IL = false: a block owns a contiguous segment of tiles, dealt round-robin
 //   to its 4 waves (per-segment counts feed compaction).
 // IL = true:  grid-stride interleave -- at any moment the whole grid reads one
-//   contiguous window of each column (DRAM row-buffer friendly); partial
-//   counts are then per block, not per segment (COUNT / aggregate only).
-template <int K, int MODE, bool DEL, int U, bool NT, bool IL = false>
+//   contiguous window of each column; partial counts are then per block, not
+//   per segment (COUNT / aggregate only).  Measured equal on MI355X.
+template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
@@ -405,16 +441,19 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const int agg_slot = MODE == kModeAgg ? P->agg_slot : 0;
   const bool agg_real = L.agg_kind == kReal;
 
-  const int32_t* colp[K];
+  const int32_t* colp[K > 0 ? K : 1];
 #pragma unroll
   for (int s = 0; s < K; ++s) colp[s] = (const int32_t*)P->cols[s].base;
+  const int32_t* strp[KS > 0 ? KS : 1];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) strp[s] = (const int32_t*)P->cols[K + s].base;
 
   Acc acc;
   acc_init(acc);
   uint64_t wave_count = 0;
 
   for (int64_t base = t0 + wave; base < t1; base += ustep * U) {
-    int32_t v[U][K][4];
+    TileRegs<K, KS> D[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t t = base + (int64_t)u * ustep;
@@ -423,22 +462,40 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
 #pragma unroll
         for (int s = 0; s < K; ++s) {
           const v4i q = load16<NT>(colp[s] + row0);
-          v[u][s][0] = q.x;
-          v[u][s][1] = q.y;
-          v[u][s][2] = q.z;
-          v[u][s][3] = q.w;
+          D[u].v[s][0] = q.x;
+          D[u].v[s][1] = q.y;
+          D[u].v[s][2] = q.z;
+          D[u].v[s][3] = q.w;
         }
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const v4i q = load16<NT>(strp[s] + (row0 + j) * 4);
+            D[u].s[s][j][0] = (uint32_t)q.x;
+            D[u].s[s][j][1] = (uint32_t)q.y;
+            D[u].s[s][j][2] = (uint32_t)q.z;
+            D[u].s[s][j][3] = (uint32_t)q.w;
+          }
       } else {
 #pragma unroll
         for (int s = 0; s < K; ++s)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[u][s][j] = (t < t1 && row0 + j < nrows) ? colp[s][row0 + j] : 0;
+          for (int j = 0; j < 4; ++j) D[u].v[s][j] = (t < t1 && row0 + j < nrows) ? colp[s][row0 + j] : 0;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              D[u].s[s][j][i] = (t < t1 && row0 + j < nrows) ? (uint32_t)strp[s][(row0 + j) * 4 + i] : 0u;
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t t = base + (int64_t)u * ustep;
-      if (t < t1) fast_tile<K, MODE, DEL>(L, P, v[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count);
+      if (t < t1)
+        fast_tile<K, KS, MODE, DEL>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count);
     }
   }
   acc.count = lane == 0 ? (int64_t)wave_count : 0;
@@ -664,21 +721,16 @@ __global__ __launch_bounds__(1024) void k_seg_scan(const Partial* __restrict__ p
   if (threadIdx.x == 0 && total) *total = carry_sh;
 }
 
-// One block per segment; each wave owns a contiguous run of the segment's
-// words and walks it one word at a time with lane == bit: set lanes compute
-// their output slot with mbcnt (set bits below the lane), so positions and
-// projected values are written densely and in ascending order.
-struct MatArgs {
-  ProjCol proj[kMaxProj];
-  void* out[kMaxProj];
-  int32_t nproj;
-};
-
-__global__ __launch_bounds__(kBlock) void k_materialize(const uint64_t* __restrict__ words, int64_t nwords,
-                                                        int64_t words_per_block,
-                                                        const int64_t* __restrict__ seg_offsets,
-                                                        int64_t row_offset, int64_t* __restrict__ ids,
-                                                        MatArgs M) {
+// Compaction (nextSetBit order): one block per segment; each wave owns a
+// contiguous run of the segment's words.  64 words per step are loaded
+// coalesced (lane = word); an exclusive scan of their popcounts gives each
+// word's output slot; then the wave visits only the non-zero words with
+// lane = bit, writing ascending global positions densely (stores only -- no
+// load sits between two iterations).
+__global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restrict__ words, int64_t nwords,
+                                                       int64_t words_per_block,
+                                                       const int64_t* __restrict__ seg_offsets,
+                                                       int64_t row_offset, int64_t* __restrict__ ids) {
   __shared__ int64_t wcount[kWaves];
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
@@ -695,10 +747,6 @@ __global__ __launch_bounds__(kBlock) void k_materialize(const uint64_t* __restri
   __syncthreads();
   int64_t off = seg_offsets[blockIdx.x];
   for (int k = 0; k < wave; ++k) off += wcount[k];
-  // 64 words per step, loaded coalesced (lane = word); an exclusive scan of
-  // their popcounts gives each word's output slot; then the wave visits only
-  // the non-zero words, lane = bit, so positions and values are written
-  // densely and in ascending order.
   for (int64_t base = a0; base < a1; base += 64) {
     const uint64_t mw = base + lane < a1 ? words[base + lane] : 0ull;
     const uint32_t pc = (uint32_t)__popcll(mw);
@@ -719,18 +767,52 @@ __global__ __launch_bounds__(kBlock) void k_materialize(const uint64_t* __restri
       if ((m >> lane) & 1ull) {
         const uint32_t below =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        const int64_t pos = off + slot + below;
-        const int64_t row = (base + j) * 64 + lane;
-        if (ids) ids[pos] = row_offset + row;
-        for (int p = 0; p < M.nproj; ++p) {
-          const int sw = M.proj[p].stride_w;
-          const uint32_t* src = (const uint32_t*)M.proj[p].base + row * sw;
-          uint32_t* dst = (uint32_t*)M.out[p] + pos * sw;
-          for (int k = 0; k < sw; ++k) dst[k] = src[k];
-        }
+        ids[off + slot + below] = row_offset + (base + j) * 64 + lane;
       }
     }
     off += total;
+  }
+}
+
+// Late materialisation (Heapfile.findRID + getRecord per output column,
+// R/index/ColumnarIndexScan.java:292-297): out_p[i] = column_p[ids[i]] for
+// the *total selected rows; thread per output row, 4 rows in flight per
+// thread, writes coalesced, reads ascending.
+struct MatArgs {
+  ProjCol proj[kMaxProj];
+  void* out[kMaxProj];
+  int32_t nproj;
+};
+
+__global__ __launch_bounds__(kBlock) void k_gather(const int64_t* __restrict__ ids, const int64_t* __restrict__ total,
+                                                   int64_t row_offset, MatArgs M) {
+  const int64_t n = *total;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i0 = (int64_t)blockIdx.x * kBlock + threadIdx.x; i0 < n; i0 += 4 * stride) {
+    int64_t row[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = i0 + u * stride;
+      row[u] = i < n ? ids[i] - row_offset : -1;
+    }
+    for (int p = 0; p < M.nproj; ++p) {
+      const int sw = M.proj[p].stride_w;
+      const uint32_t* src = (const uint32_t*)M.proj[p].base;
+      uint32_t* dst = (uint32_t*)M.out[p];
+      if (sw == 1) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = row[u] >= 0 ? src[row[u]] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (row[u] >= 0) dst[i0 + u * stride] = v[u];
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (row[u] >= 0)
+            for (int k = 0; k < sw; ++k) dst[(i0 + u * stride) * sw + k] = src[row[u] * sw + k];
+      }
+    }
   }
 }
 
@@ -794,39 +876,43 @@ int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block) {
   return g < 1 ? 1 : g;
 }
 
-template <int K, int MODE>
+template <int K, int KS, int MODE>
 static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   if (L.deleted) {
-    hipLaunchKernelGGL((k_scan_fast<K, MODE, true, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
+    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, true, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
     return;
   }
-  if (K == 2 && MODE == kModeCount && L.variant) {  // tuning variants of the C3 kernel
+  if constexpr (K == 2 && KS == 0 && MODE == kModeCount) {  // tuning variants of the C3 kernel
     switch (L.variant) {
-      case 1: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, false>), grid, dim3(kBlock), 0, s, L); return;
-      case 2: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, false>), grid, dim3(kBlock), 0, s, L); return;
-      case 3: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, false>), grid, dim3(kBlock), 0, s, L); return;
-      case 4: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 5: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 6: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 7: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, false, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 8: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, false, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 9: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, false, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 10: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 1, true, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 11: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 2, true, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 12: hipLaunchKernelGGL((k_scan_fast<K, MODE, false, 4, true, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 1: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 1, false>), grid, dim3(kBlock), 0, s, L); return;
+      case 4: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 1, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 6: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 4, true>), grid, dim3(kBlock), 0, s, L); return;
+      case 11:
+        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, true>), grid, dim3(kBlock), 0, s, L);
+        return;
       default: break;
     }
   }
-  hipLaunchKernelGGL((k_scan_fast<K, MODE, false, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
+  hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
 }
 
+// fast_k = number of 4-byte slots, fast_ks = number of 16-byte string slots;
+// anything else goes to the one-row-per-lane generic kernel
 template <int MODE>
 static void mode_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
-  switch (L.fast_k) {
-    case 1: fast_launch<1, MODE>(L, grid, s); break;
-    case 2: fast_launch<2, MODE>(L, grid, s); break;
-    case 3: fast_launch<3, MODE>(L, grid, s); break;
-    case 4: fast_launch<4, MODE>(L, grid, s); break;
+  const int code = L.fast_ks * 8 + L.fast_k;
+  switch (code) {
+    case 1: fast_launch<1, 0, MODE>(L, grid, s); return;
+    case 2: fast_launch<2, 0, MODE>(L, grid, s); return;
+    case 3: fast_launch<3, 0, MODE>(L, grid, s); return;
+    case 4: fast_launch<4, 0, MODE>(L, grid, s); return;
+    case 8 + 0: fast_launch<0, 1, MODE>(L, grid, s); return;
+    case 8 + 1: fast_launch<1, 1, MODE>(L, grid, s); return;
+    case 8 + 2: fast_launch<2, 1, MODE>(L, grid, s); return;
+    case 8 + 3: fast_launch<3, 1, MODE>(L, grid, s); return;
+    case 16 + 0: fast_launch<0, 2, MODE>(L, grid, s); return;
+    case 16 + 1: fast_launch<1, 2, MODE>(L, grid, s); return;
+    case 16 + 2: fast_launch<2, 2, MODE>(L, grid, s); return;
     default:
       if (L.deleted)
         hipLaunchKernelGGL((k_scan_generic<MODE, true>), grid, dim3(kBlock), 0, s, L);
@@ -889,16 +975,19 @@ hipError_t launch_seg_scan(const Partial* seg_parts, int64_t nseg, int64_t* seg_
 
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                               const int64_t* seg_offsets, int64_t row_offset, int64_t* ids, const ProjCol* proj,
-                              void* const* out, int32_t nproj, hipStream_t s) {
-  MatArgs M;
-  M.nproj = nproj;
-  for (int j = 0; j < nproj && j < kMaxProj; ++j) {
-    M.proj[j] = proj[j];
-    M.out[j] = out[j];
-  }
+                              void* const* out, int32_t nproj, const int64_t* total, hipStream_t s) {
   const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
-  hipLaunchKernelGGL(k_materialize, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
-                     seg_offsets, row_offset, ids, M);
+  hipLaunchKernelGGL(k_select_ids, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
+                     seg_offsets, row_offset, ids);
+  if (nproj > 0) {
+    MatArgs M;
+    M.nproj = nproj;
+    for (int j = 0; j < nproj && j < kMaxProj; ++j) {
+      M.proj[j] = proj[j];
+      M.out[j] = out[j];
+    }
+    hipLaunchKernelGGL(k_gather, dim3(1024), dim3(kBlock), 0, s, ids, total, row_offset, M);
+  }
   return hipGetLastError();
 }
 

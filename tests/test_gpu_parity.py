@@ -240,9 +240,17 @@ C5_CNF = [[(oracle.LT, ("sym", 1), ("int", 1 << 19))], [(oracle.GE, ("sym", 2), 
           [(oracle.GE, ("sym", 3), ("str", "M"))]]
 
 
-def test_c5_mixed_filter_and_aggregates(ctx):
-    cols, _ = mixed_table(2_000_000)
-    ot, t = oracle.Table(cols), ctx.stage(cols)
+@pytest.mark.parametrize("generic", [False, True])
+@pytest.mark.parametrize("deleted", [False, True])
+def test_c5_mixed_filter_and_aggregates(ctx, generic, deleted, monkeypatch):
+    """C5 shape: int32 + float32 + char(16) (16-byte string slot of the fast
+    kernel, or the generic kernel), 3 conjuncts + SUM/MIN/MAX."""
+    if generic:
+        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+    n = 2_000_003
+    cols, _ = mixed_table(n)
+    dele = helpers.random_deleted(n, 0.07) if deleted else None
+    ot, t = oracle.Table(cols, dele), ctx.stage(cols, dele)
     n_o, w_o, _ = oracle.filescan(ot, C5_CNF)
     bm, words = gpu_select(ctx, t, C5_CNF)
     assert np.array_equal(words, w_o) and bm.count == n_o
@@ -284,7 +292,10 @@ def test_nan_raises_like_the_reference(ctx, m):
     assert e.value.code == m.mbx.E_TYPE
 
 
-def test_strings_java_order(ctx):
+@pytest.mark.parametrize("generic", [False, True])
+def test_strings_java_order(ctx, generic, monkeypatch):
+    if generic:
+        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
     vals = ["", "a", "ab", "b", "South_Dakota", "South", "é", "€", "\U0001F600", "a\u0000b", "a\u0000",
             "zzzzzzzzzzzzzzzz"]
     arr = helpers.encode_strings(vals, 16)
@@ -365,3 +376,28 @@ def test_row_range_shards_concatenate(ctx):
         ids.append(ctx.select(bm, row_offset=s))
     assert np.array_equal(np.concatenate(words), w_o)
     assert np.array_equal(np.concatenate(ids), ids_o)
+
+
+@pytest.mark.parametrize("width", [13, 16, 8, 25])
+def test_string_slot_shapes(ctx, width):
+    """Two string columns + ints: char(13..16) rows take the fast kernel's
+    16-byte slots (<= 2 of them), other widths the generic kernel; literals
+    longer than 16 bytes also fall back.  All bit-exact vs the oracle."""
+    n = 300_007
+    rng = np.random.Generator(np.random.PCG64(21))
+    words = ["", "a", "ab", "abc", "M", "Mz", "South_Dakota", "Zz", "x" * width, "é€", "a\u0000b"]
+    words = [w for w in words if len(oracle.java_mutf8(w)) <= width]
+    s1 = helpers.encode_strings([words[i] for i in rng.integers(0, len(words), n)], width)
+    s2 = helpers.encode_strings([words[i] for i in rng.integers(0, len(words), n)], width)
+    cols = [(oracle.STRING, width, s1), (oracle.INTEGER, 4, rng.integers(0, 100, n, dtype=np.int32)),
+            (oracle.STRING, width, s2)]
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    for cnf in ([[(oracle.GE, ("sym", 1), ("str", "M"))], [(oracle.LT, ("sym", 3), ("str", "ab")),
+                                                            (oracle.GT, ("sym", 2), ("int", 90))]],
+                [[(oracle.EQ, ("sym", 3), ("str", "South_Dakota"))]],
+                [[(oracle.NE, ("sym", 1), ("str", "x" * width + "y"))]],
+                [[(oracle.LE, ("str", "abc"), ("sym", 1))], [(oracle.EQ, ("sym", 2), ("int", 5))]]):
+        n_o, w_o, _ = oracle.filescan(ot, cnf)
+        bm, words_g = gpu_select(ctx, t, cnf)
+        assert np.array_equal(words_g, w_o), cnf
+        assert ctx.scan_count(ctx.compile(t, cnf)) == n_o
