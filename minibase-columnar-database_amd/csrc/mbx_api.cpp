@@ -244,8 +244,8 @@ extern "C" int mbx_init(int32_t device, mbx_ctx** out) {
     if (e == hipSuccess) e = hipMalloc(&c->dagg, sizeof(AggOut));
     if (e == hipSuccess) e = hipMalloc(&c->dcount, sizeof(int64_t) * 2);
     if (e == hipSuccess) e = hipMalloc(&c->dnan, sizeof(int32_t) * 2);
-    if (e == hipSuccess) e = hipMalloc(&c->ticket, sizeof(uint32_t) * 4);
-    if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(uint32_t) * 4);
+    if (e == hipSuccess) e = hipMalloc(&c->ticket, sizeof(uint32_t) * kTicketWords);
+    if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(uint32_t) * kTicketWords);
     if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 256, hipHostMallocDefault);
     if (e != hipSuccess) {
       rc = fail(MBX_E_DEVICE, "mbx_init: %s", hipGetErrorString(e));
@@ -746,6 +746,9 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   const char* fm = getenv("MBX_FIN_MODE");
   L.fin_mode = fm ? atoi(fm) : kFinWriteThrough;
   if (L.fin_mode == kFinSeparate) L.ticket = nullptr;
+  const char* tg = getenv("MBX_TICKET_GROUPS");
+  L.ticket_groups = tg ? atoi(tg) : kDefaultTicketGroups;
+  if (L.ticket_groups < 0 || L.ticket_groups > kMaxTicketGroups) L.ticket_groups = kDefaultTicketGroups;
   HIPCHK(launch_scan(L, c->stream));
   if (L.fin_mode == kFinSeparate)
     HIPCHK(launch_finalize(parts, grid_blocks(L.nrows, tpb), L.agg_kind, agg_out, count_out, nan_out, c->stream));

@@ -107,13 +107,26 @@ struct ScanLaunch {
   int32_t agg_kind;           // kInt / kReal when mode == kModeAgg
   // in-launch finalize: the last block to arrive on `ticket` reduces all
   // partials in block order (release/acquire hand-off, zeroed by that block)
-  uint32_t* ticket;           // device, 0 before the launch; null: no finalize
+  uint32_t* ticket;           // device, kTicketWords zeros before the launch; null: no finalize
+  int32_t ticket_groups;      // 0: one flat ticket; G: G group tickets + one top ticket
   int64_t* count_out;         // device or null
   AggOut* agg_out;            // device or null
   int32_t* nan_out;           // device or null
   int32_t variant;            // 0: default kernel; >0: tuning variant (MBX_SCAN_VARIANT)
   int32_t fin_mode;           // FinMode (MBX_FIN_MODE): how the last block sees the partials
 };
+
+// Arrival tickets of the in-launch finalize.  Blocks arrive on the ticket of
+// their group (blockIdx % G, so a group lives on one XCD -- blocks are dealt
+// to the 8 XCDs round-robin); the last arriver of a group then arrives on the
+// top ticket.  Same-address device atomics serialize (~12 ns each measured on
+// MI355X), so one flat ticket costs ~12 us per 1000 blocks when they finish
+// together; G groups cut the chain to nblocks/G + G.  Each ticket owns a
+// 128-byte line.
+constexpr int kTicketStride = 32;                 // uint32 per ticket line
+constexpr int kMaxTicketGroups = 64;
+constexpr int kTicketWords = (kMaxTicketGroups + 1) * kTicketStride;
+constexpr int kDefaultTicketGroups = 32;
 
 enum FinMode : int32_t {
   kFinWriteThrough = 0,  // sc1 partial stores + ticket, sc1 loads by the last block

@@ -197,6 +197,30 @@ __device__ __forceinline__ void finalize_block(const Partial* parts, int64_t n, 
   }
 }
 
+// One block arrives (thread 0, after its partial is drained); true for the
+// last block of the grid.  Every ticket it exhausts is reset to 0 for the next
+// launch on the stream (only the last arriver of a ticket touches it again).
+__device__ __forceinline__ bool arrive(uint32_t* ticket, int groups) {
+  const uint32_t nb = gridDim.x;
+  if (groups <= 1 || nb <= (uint32_t)groups) {
+    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t != nb - 1) return false;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  const uint32_t G = (uint32_t)groups;
+  const uint32_t g = blockIdx.x % G;
+  const uint32_t members = (nb - g + G - 1) / G;  // blocks b < nb with b % G == g
+  uint32_t* gt = ticket + (1 + g) * kTicketStride;
+  const uint32_t t = __hip_atomic_fetch_add(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t != members - 1) return false;
+  __hip_atomic_store(gt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t u = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (u != G - 1) return false;
+  __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 // Block-wide fixed-order reduction of per-thread accumulators into this
 // block's Partial; with a ticket, the last block to arrive then finalizes all
 // partials inside the same launch.  Hand-off (MI355X: per-XCD L2s are not
@@ -242,15 +266,13 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
       // write-back fence needed (MI355X_MICROARCH.md, Valid forms row 1)
       store_partial_sc1(L.partials + blockIdx.x, p);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t t = __hip_atomic_fetch_add(L.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      is_last = (t == gridDim.x - 1);
+      is_last = arrive(L.ticket, L.ticket_groups);
     } else if (L.ticket) {
       L.partials[blockIdx.x] = p;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t t = __hip_atomic_fetch_add(L.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      is_last = (t == gridDim.x - 1);
+      is_last = arrive(L.ticket, L.ticket_groups);
       if (is_last) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -266,7 +288,6 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
       finalize_block<true>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
     else
       finalize_block<false>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
-    if (threadIdx.x == 0) __hip_atomic_store(L.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -289,8 +310,11 @@ __device__ __forceinline__ uint64_t pack_word16(uint32_t nib, int lane) {
 // Each wave streams whole 256-row tiles of its block's segment: one
 // global_load_dwordx4 per column per tile, terms folded into per-row
 // conjunct bitmasks (cb), the CNF holds when cb == all_conj.
-// One tile's column data in registers: K 4-byte slots (4 rows per lane) and
-// KS 16-byte string slots (char(13..16): 4 rows x 4 words per lane).
+// One tile's column data in registers: K 4-byte slots (lane l holds rows
+// 4l..4l+3) and KS 16-byte string slots (char(13..16)).  String rows are
+// loaded so that every load instruction reads one contiguous KiB -- load j of
+// lane l holds row 64j + l -- and their compare results are moved back to the
+// 4-rows-per-lane layout through the wave ballots (= the tile's 4 BitSet words).
 template <int K, int KS>
 struct TileRegs {
   int32_t v[K > 0 ? K : 1][4];
@@ -337,7 +361,15 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
       } else {
         str16_cmp4(D.s[KS > 1 ? 1 : 0], lit, c);
       }
-      cmp4<int32_t>(T.op, c, 0, r);
+      bool rs[4];
+      cmp4<int32_t>(T.op, c, 0, rs);
+      // rs[j] is row 64j + lane; ballot j is BitSet word j of the tile
+      const uint64_t w0 = __ballot(rs[0]), w1 = __ballot(rs[1]), w2 = __ballot(rs[2]), w3 = __ballot(rs[3]);
+      const int q = lane >> 4;
+      const uint64_t w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
+      const uint32_t nib = (uint32_t)(w >> ((lane & 15) * 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = (nib >> j) & 1u;
     } else {
       int32_t a[4];
 #pragma unroll
@@ -471,7 +503,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
         for (int s = 0; s < KS; ++s)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const v4i q = load16<NT>(strp[s] + (row0 + j) * 4);
+            const v4i q = load16<NT>(strp[s] + (t * kTileRows + j * 64 + lane) * 4);
             D[u].s[s][j][0] = (uint32_t)q.x;
             D[u].s[s][j][1] = (uint32_t)q.y;
             D[u].s[s][j][2] = (uint32_t)q.z;
@@ -487,8 +519,10 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              D[u].s[s][j][i] = (t < t1 && row0 + j < nrows) ? (uint32_t)strp[s][(row0 + j) * 4 + i] : 0u;
+            for (int i = 0; i < 4; ++i) {
+              const int64_t r = t * kTileRows + j * 64 + lane;
+              D[u].s[s][j][i] = (t < t1 && r < nrows) ? (uint32_t)strp[s][r * 4 + i] : 0u;
+            }
       }
     }
 #pragma unroll
@@ -724,9 +758,10 @@ __global__ __launch_bounds__(1024) void k_seg_scan(const Partial* __restrict__ p
 // Compaction (nextSetBit order): one block per segment; each wave owns a
 // contiguous run of the segment's words.  64 words per step are loaded
 // coalesced (lane = word); an exclusive scan of their popcounts gives each
-// word's output slot; then the wave visits only the non-zero words with
-// lane = bit, writing ascending global positions densely (stores only -- no
-// load sits between two iterations).
+// word's output slot; then either each lane peels its own word's bits
+// (sparse steps: iterations = the largest popcount) or the wave visits only
+// the non-zero words with lane = bit, writing ascending global positions
+// densely (dense steps; stores only -- no load sits between two iterations).
 __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restrict__ words, int64_t nwords,
                                                        int64_t words_per_block,
                                                        const int64_t* __restrict__ seg_offsets,
@@ -759,6 +794,21 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
     const uint32_t excl = incl - pc;
     const uint32_t total = __shfl(incl, 63);
     uint64_t nz = __ballot(mw != 0ull);
+    uint32_t maxpc = pc;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) maxpc = max(maxpc, (uint32_t)__shfl_xor(maxpc, m));
+    if (2 * maxpc <= (uint32_t)__popcll(nz)) {
+      // sparse step: lane = word, each lane peels its own bits (max-popcount
+      // iterations instead of one per non-zero word)
+      uint64_t m = mw;
+      int64_t o = off + excl;
+      const int64_t rbase = row_offset + (base + lane) * 64;
+      while (m) {
+        ids[o++] = rbase + __builtin_ctzll(m);
+        m &= m - 1ull;
+      }
+      nz = 0;
+    }
     while (nz) {
       const int j = __builtin_ctzll(nz);
       nz &= nz - 1ull;

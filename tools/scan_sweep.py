@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--tpb", default="0,24,48,96,191,382")
     ap.add_argument("--generic", action="store_true")
     ap.add_argument("--fin", default="0", help="MBX_FIN_MODE values: 0 write-through, 1 fences, 2 separate")
+    ap.add_argument("--groups", default="32", help="MBX_TICKET_GROUPS values (0/1: one flat ticket)")
     args = ap.parse_args()
 
     import torch
@@ -51,15 +52,17 @@ def main():
     out = torch.zeros(args.launches, dtype=torch.int64, device="cuda")
 
     fins = list(map(int, args.fin.split(",")))
-    configs = [(v, tp, False, f) for v in map(int, args.variants.split(",")) for tp in map(int, args.tpb.split(","))
-               for f in fins]
+    grps = list(map(int, args.groups.split(",")))
+    configs = [(v, tp, False, f, g) for v in map(int, args.variants.split(",")) for tp in map(int, args.tpb.split(","))
+               for f in fins for g in grps]
     if args.generic:
-        configs += [(0, tp, True, fins[0]) for tp in map(int, args.tpb.split(","))]
+        configs += [(0, tp, True, fins[0], grps[0]) for tp in map(int, args.tpb.split(","))]
     res = {c: [] for c in configs}
     for r in range(args.rounds):
         for c in configs:
-            v, tp, gen, fin = c
+            v, tp, gen, fin, grp = c
             os.environ["MBX_SCAN_VARIANT"] = str(v)
+            os.environ["MBX_TICKET_GROUPS"] = str(grp)
             os.environ["MBX_FIN_MODE"] = str(fin)
             if tp:
                 os.environ["MBX_TILES_PER_BLOCK"] = str(tp)
@@ -79,11 +82,12 @@ def main():
             assert bool((got == want).all()), (c, got[:4], want)
             res[c].append(statistics.median(ts))
     for c in configs:
-        v, tp, gen, fin = c
+        v, tp, gen, fin, grp = c
         med = statistics.median(res[c])
         print(json.dumps({"variant": v, "tiles_per_block": tp or "default", "generic": gen, "fin_mode": fin,
+                          "ticket_groups": grp,
                           "median_ms": med, "min_ms": min(res[c]),
-                          "gbs": 8 * n / (med * 1e-3) / 1e9}), flush=True)
+                          "gbs": 8 * n / (med * 1e-3) / 1e9, "rows": n}), flush=True)
     ctx.close()
 
 
