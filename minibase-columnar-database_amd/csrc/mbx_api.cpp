@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "mbx_internal.hpp"
+#include "mbx_objects.hpp"
 
 using namespace mbx;
 
@@ -32,7 +33,7 @@ using namespace mbx;
 
 static thread_local std::string g_err;
 
-static int fail(int code, const char* fmt, ...) {
+int mbx::fail(int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -41,91 +42,6 @@ static int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
-
-#define HIPCHK(expr)                                                                  \
-  do {                                                                                \
-    hipError_t e_ = (expr);                                                           \
-    if (e_ != hipSuccess) return fail(MBX_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
-  } while (0)
-
-#define NOTNULL(p) \
-  do {             \
-    if (!(p)) return fail(MBX_E_INVALID, "%s: null argument `%s`", __func__, #p); \
-  } while (0)
-
-// ----------------------------------------------------------------- objects
-
-struct mbx_ctx {
-  int32_t device = 0;
-  hipStream_t stream = nullptr;
-  Partial* partials = nullptr;  // scratch, one per block of the largest scan so far
-  int64_t partials_cap = 0;
-  AggOut* dagg = nullptr;
-  int64_t* dcount = nullptr;
-  int32_t* dnan = nullptr;
-  uint32_t* ticket = nullptr;   // in-launch finalize ticket (always 0 between launches)
-  int64_t* ids_scratch = nullptr;  // positions for a gather whose caller wants no positions
-  int64_t ids_cap = 0;
-  void* pinned = nullptr;       // 256 bytes of pinned host scratch
-};
-
-struct TCol {
-  int32_t attr_type = 0;
-  int32_t size = 0;
-  int32_t stride_w = 1;  // device words per row
-  void* dev = nullptr;
-  bool owned = false;
-};
-
-struct mbx_table {
-  mbx_ctx* ctx = nullptr;
-  int64_t nrows = 0;
-  int64_t row_offset = 0;
-  std::vector<TCol> cols;
-  uint64_t* deleted = nullptr;
-  bool owns_deleted = false;
-  bool aligned16 = true;
-};
-
-struct PlanVariant {
-  int32_t agg_col = -1;  // -1: filter only
-  KPlan* dev = nullptr;
-  int32_t fast_k = 0;
-  int32_t fast_ks = 0;
-  int32_t agg_kind = kInt;
-};
-
-struct mbx_plan {
-  mbx_ctx* ctx = nullptr;
-  const mbx_table* t = nullptr;
-  KPlan host{};
-  std::vector<int32_t> slot_col;  // table column of each slot
-  bool all_literal = true;        // every term is `column OP literal`
-  bool str_lit_fits16 = true;     // every string literal is <= 16 bytes
-  std::deque<PlanVariant> variants;
-};
-
-struct mbx_bitmap {
-  mbx_ctx* ctx = nullptr;
-  int64_t nbits = 0;
-  int64_t nwords = 0;
-  uint64_t* words = nullptr;
-  int64_t wpb = 4;        // words per segment
-  int64_t nseg = 1;
-  Partial* segs = nullptr;  // per-segment counts (Partial.count)
-  int64_t* seg_off = nullptr;
-  int64_t count = -1;     // host copy of the cardinality, -1 = unknown
-};
-
-struct mbx_cursor {
-  mbx_ctx* ctx = nullptr;
-  int64_t count = 0;
-  int64_t next = 0;
-  const mbx_table* t = nullptr;
-  int64_t* ids = nullptr;  // device
-  std::vector<void*> outs; // device, one per projected column
-  std::vector<int32_t> proj;
-};
 
 // ----------------------------------------------------------------- helpers
 
@@ -145,7 +61,7 @@ static int ensure_partials(mbx_ctx* c, int64_t n) {
   return MBX_OK;
 }
 
-static int set_device(mbx_ctx* c) {
+int mbx::set_device(mbx_ctx* c) {
   HIPCHK(hipSetDevice(c->device));
   return MBX_OK;
 }
@@ -184,9 +100,9 @@ static void decode_device_string(const uint8_t* src, int32_t stride, uint8_t* ds
   }
 }
 
-static int64_t words_for(int64_t nbits) { return (nbits + 63) / 64; }
+int64_t mbx::words_for(int64_t nbits) { return (nbits + 63) / 64; }
 
-static int bitmap_new(mbx_ctx* c, int64_t nbits, mbx_bitmap** out) {
+int mbx::bitmap_new(mbx_ctx* c, int64_t nbits, mbx_bitmap** out) {
   mbx_bitmap* b = new (std::nothrow) mbx_bitmap();
   if (!b) return fail(MBX_E_NOMEM, "bitmap: host allocation");
   b->ctx = c;
@@ -196,11 +112,9 @@ static int bitmap_new(mbx_ctx* c, int64_t nbits, mbx_bitmap** out) {
   b->nseg = b->nwords == 0 ? 1 : (b->nwords + b->wpb - 1) / b->wpb;
   hipError_t e = hipMalloc(&b->words, sizeof(uint64_t) * (size_t)(b->nwords > 0 ? b->nwords : 1));
   if (e == hipSuccess) e = hipMalloc(&b->segs, sizeof(Partial) * (size_t)b->nseg);
-  if (e == hipSuccess) e = hipMalloc(&b->seg_off, sizeof(int64_t) * (size_t)b->nseg);
   if (e != hipSuccess) {
     hipFree(b->words);
     hipFree(b->segs);
-    hipFree(b->seg_off);
     delete b;
     return fail(MBX_E_NOMEM, "bitmap of %lld bits: %s", (long long)nbits, hipGetErrorString(e));
   }
@@ -287,7 +201,7 @@ extern "C" void* mbx_stream(mbx_ctx* c) { return c ? (void*)c->stream : nullptr;
 
 // ------------------------------------------------------------------ tables
 
-static int check_cols(const mbx_col_desc* cols, int32_t ncols) {
+int mbx::check_cols(const mbx_col_desc* cols, int32_t ncols) {
   if (ncols <= 0) return fail(MBX_E_INVALID, "table: ncols = %d", ncols);
   for (int32_t j = 0; j < ncols; j++) {
     const int32_t t = cols[j].attr_type;
@@ -301,7 +215,7 @@ static int check_cols(const mbx_col_desc* cols, int32_t ncols) {
   return MBX_OK;
 }
 
-static int32_t stride_words(const mbx_col_desc& d) {
+int32_t mbx::stride_words(const mbx_col_desc& d) {
   return d.attr_type == MBX_ATTR_STRING ? (d.size + 3) / 4 : 1;
 }
 
@@ -316,13 +230,8 @@ extern "C" int mbx_table_free(mbx_table* t) {
   return MBX_OK;
 }
 
-extern "C" int mbx_table_stage(mbx_ctx* c, const mbx_col_desc* cols, int32_t ncols, int64_t nrows,
-                               const void* const* host_cols, const uint64_t* deleted_words, int64_t row_offset,
-                               mbx_table** out) {
-  NOTNULL(c);
-  NOTNULL(cols);
-  NOTNULL(host_cols);
-  NOTNULL(out);
+int mbx::table_alloc(mbx_ctx* c, const mbx_col_desc* cols, int32_t ncols, int64_t nrows, int64_t row_offset,
+                     bool with_deleted, mbx_table** out) {
   *out = nullptr;
   int rc = check_cols(cols, ncols);
   if (rc) return rc;
@@ -349,11 +258,38 @@ extern "C" int mbx_table_stage(mbx_ctx* c, const mbx_col_desc* cols, int32_t nco
       return fail(MBX_E_NOMEM, "table: column %d (%zu bytes): %s", j, bytes, hipGetErrorString(e));
     }
     t->cols.push_back(col);
-    if (nrows == 0) continue;
+  }
+  if (with_deleted && nrows > 0) {
+    const int64_t nw = words_for(nrows);
+    hipError_t e = hipMalloc(&t->deleted, sizeof(uint64_t) * (size_t)nw);
+    if (e != hipSuccess) {
+      mbx_table_free(t);
+      return fail(MBX_E_NOMEM, "table: deleted bitmap: %s", hipGetErrorString(e));
+    }
+    t->owns_deleted = true;
+  }
+  *out = t;
+  return MBX_OK;
+}
+
+extern "C" int mbx_table_stage(mbx_ctx* c, const mbx_col_desc* cols, int32_t ncols, int64_t nrows,
+                               const void* const* host_cols, const uint64_t* deleted_words, int64_t row_offset,
+                               mbx_table** out) {
+  NOTNULL(c);
+  NOTNULL(cols);
+  NOTNULL(host_cols);
+  NOTNULL(out);
+  *out = nullptr;
+  mbx_table* t = nullptr;
+  int rc = table_alloc(c, cols, ncols, nrows, row_offset, deleted_words != nullptr, &t);
+  if (rc) return rc;
+  for (int32_t j = 0; j < ncols && nrows > 0; j++) {
+    const TCol& col = t->cols[j];
     if (!host_cols[j]) {
       mbx_table_free(t);
       return fail(MBX_E_INVALID, "table: host_cols[%d] is null", j);
     }
+    hipError_t e;
     if (col.attr_type != MBX_ATTR_STRING) {
       e = hipMemcpy(col.dev, host_cols[j], (size_t)nrows * 4, hipMemcpyHostToDevice);
     } else {
@@ -370,17 +306,15 @@ extern "C" int mbx_table_stage(mbx_ctx* c, const mbx_col_desc* cols, int32_t nco
       return fail(MBX_E_DEVICE, "table: staging column %d: %s", j, hipGetErrorString(e));
     }
   }
-  if (deleted_words && nrows > 0) {
+  if (t->deleted) {
     const int64_t nw = words_for(nrows);
     std::vector<uint64_t> d(deleted_words, deleted_words + nw);
     if (nrows & 63) d[nw - 1] &= (1ull << (nrows & 63)) - 1ull;
-    hipError_t e = hipMalloc(&t->deleted, sizeof(uint64_t) * (size_t)nw);
-    if (e == hipSuccess) e = hipMemcpy(t->deleted, d.data(), sizeof(uint64_t) * (size_t)nw, hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpy(t->deleted, d.data(), sizeof(uint64_t) * (size_t)nw, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       mbx_table_free(t);
       return fail(MBX_E_DEVICE, "table: staging deleted bitmap: %s", hipGetErrorString(e));
     }
-    t->owns_deleted = true;
   }
   *out = t;
   return MBX_OK;
@@ -834,6 +768,11 @@ static int bitmap_count_sync(mbx_ctx* c, mbx_bitmap* b, bool with_nan) {
   return with_nan ? check_nan(c) : MBX_OK;
 }
 
+int mbx::bitmap_recount(mbx_ctx* c, mbx_bitmap* b) {
+  HIPCHK(launch_seg_popcount(b->words, b->nwords, b->wpb, b->segs, c->stream));
+  return bitmap_count_sync(c, b, false);
+}
+
 extern "C" int mbx_scan_bitmap(mbx_ctx* c, const mbx_plan* pc, mbx_bitmap** out, int64_t* count) {
   NOTNULL(c);
   NOTNULL(pc);
@@ -908,7 +847,6 @@ extern "C" int mbx_bitmap_free(mbx_bitmap* b) {
   hipStreamSynchronize(b->ctx->stream);
   hipFree(b->words);
   hipFree(b->segs);
-  hipFree(b->seg_off);
   delete b;
   return MBX_OK;
 }
@@ -1100,9 +1038,16 @@ extern "C" int mbx_bitmap_index_build(mbx_ctx* c, const mbx_table* t, int32_t co
     kc.base = tc.dev;
     kc.kind = col_kind(tc.attr_type);
     kc.stride_w = tc.stride_w;
-    e = launch_index_build(kc, t->nrows, t->deleted, dvals, nvalues, vw, outs.data(), out[0]->wpb, c->stream);
-    for (int32_t v = 0; v < nvalues && e == hipSuccess; v++)
-      e = launch_seg_popcount(out[v]->words, out[v]->nwords, out[v]->wpb, out[v]->segs, c->stream);
+    if (kc.kind != kStr && tc.stride_w == 1 && !(reinterpret_cast<uintptr_t>(tc.dev) & 15)) {
+      std::vector<Partial*> segs((size_t)nvalues);
+      for (int32_t v = 0; v < nvalues; v++) segs[(size_t)v] = out[v]->segs;
+      e = launch_index_build4(kc, t->nrows, t->deleted, dvals, nvalues, outs.data(), segs.data(), out[0]->wpb,
+                              c->stream);
+    } else {
+      e = launch_index_build(kc, t->nrows, t->deleted, dvals, nvalues, vw, outs.data(), out[0]->wpb, c->stream);
+      for (int32_t v = 0; v < nvalues && e == hipSuccess; v++)
+        e = launch_seg_popcount(out[v]->words, out[v]->nwords, out[v]->wpb, out[v]->segs, c->stream);
+    }
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   hipFree(dvals);
@@ -1146,10 +1091,8 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
     }
     dev_ids = c->ids_scratch;
   }
-  HIPCHK(launch_seg_scan(sel->segs, sel->nseg, sel->seg_off, dev_total, c->stream));
-  if (sel->nwords > 0)
-    HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->seg_off, row_offset, dev_ids, pc, dev_out, nproj,
-                              dev_total, c->stream));
+  HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segs, row_offset, dev_ids, pc, dev_out, nproj,
+                            dev_total, c->stream));
   return MBX_OK;
 }
 

@@ -159,12 +159,16 @@ hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* 
                                  hipStream_t s);
 hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                                Partial* seg_parts, hipStream_t s);
-hipError_t launch_seg_scan(const Partial* seg_parts, int64_t nseg, int64_t* seg_offsets, int64_t* total,
-                           hipStream_t s);
+// positions (ascending) of the set bits + gather of the projected columns;
+// *total = the number of set bits (written on the stream)
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
-                              const int64_t* seg_offsets, int64_t row_offset, int64_t* ids,
-                              const ProjCol* proj, void* const* out, int32_t nproj, const int64_t* total,
+                              const Partial* seg_parts, int64_t row_offset, int64_t* ids,
+                              const ProjCol* proj, void* const* out, int32_t nproj, int64_t* total,
                               hipStream_t s);
+// 4-byte columns (int / float): also writes every output's segment counts
+hipError_t launch_index_build4(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
+                               int32_t nvalues, uint64_t* const* outs, Partial* const* segs, int64_t words_per_block,
+                               hipStream_t s);
 hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
                               int32_t nvalues,
                               int32_t value_words, uint64_t* const* outs, int64_t words_per_block, hipStream_t s);

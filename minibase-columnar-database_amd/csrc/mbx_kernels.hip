@@ -10,11 +10,12 @@
 //   k_bitmap_cnf     ColumnarIndexScan OR/AND over index BitSets
 //                    (R/index/ColumnarIndexScan.java:130-181) AND NOT deleted.
 //   k_bitmap_combine BitSet.and / or / andNot.
-//   k_seg_popcount / k_seg_scan / k_materialize
+//   k_seg_popcount / k_select_ids / k_gather
 //                    nextSetBit compaction + late materialisation
 //                    (R/index/ColumnarIndexScan.java:287-308): per-segment
-//                    counts -> exclusive scan -> one wave per word run writes
-//                    ascending positions and the projected values.
+//                    counts -> each block sums the counts before it and writes
+//                    its ascending positions -> thread-per-row gather of the
+//                    projected values.
 //   k_index_build    Columnarfile.createBitMapIndex (R/columnar/Columnarfile.java:698-753).
 //   k_finalize       deterministic fixed-order reduction of per-block partials.
 //
@@ -721,40 +722,6 @@ __global__ __launch_bounds__(kBlock) void k_seg_popcount(const uint64_t* __restr
   }
 }
 
-// exclusive scan of the segment counts, one block of 1024 threads
-__global__ __launch_bounds__(1024) void k_seg_scan(const Partial* __restrict__ parts, int64_t n,
-                                                   int64_t* __restrict__ offsets, int64_t* total) {
-  __shared__ int64_t wsum[16];
-  __shared__ int64_t carry_sh;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  if (threadIdx.x == 0) carry_sh = 0;
-  __syncthreads();
-  for (int64_t base = 0; base < n; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t x = i < n ? parts[i].count : 0;
-    int64_t inc = x;  // inclusive wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int64_t y = __shfl_up(inc, d);
-      if (lane >= d) inc += y;
-    }
-    if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
-    int64_t before = carry_sh;
-    for (int k = 0; k < wave; ++k) before += wsum[k];
-    if (i < n) offsets[i] = before + inc - x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int64_t s = carry_sh;
-      for (int k = 0; k < 16; ++k) s += wsum[k];
-      carry_sh = s;
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0 && total) *total = carry_sh;
-}
-
 // Compaction (nextSetBit order): one block per segment; each wave owns a
 // contiguous run of the segment's words.  64 words per step are loaded
 // coalesced (lane = word); an exclusive scan of their popcounts gives each
@@ -762,11 +729,16 @@ __global__ __launch_bounds__(1024) void k_seg_scan(const Partial* __restrict__ p
 // (sparse steps: iterations = the largest popcount) or the wave visits only
 // the non-zero words with lane = bit, writing ascending global positions
 // densely (dense steps; stores only -- no load sits between two iterations).
+// A block's output offset is the sum of the segment counts before it (read
+// straight from the producers' per-segment counts -- no separate scan
+// launch); the last block also writes the total.
 __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restrict__ words, int64_t nwords,
                                                        int64_t words_per_block,
-                                                       const int64_t* __restrict__ seg_offsets,
-                                                       int64_t row_offset, int64_t* __restrict__ ids) {
+                                                       const Partial* __restrict__ seg_parts,
+                                                       int64_t row_offset, int64_t* __restrict__ ids,
+                                                       int64_t* __restrict__ total) {
   __shared__ int64_t wcount[kWaves];
+  __shared__ int64_t wpre[kWaves];
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
   const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
@@ -776,11 +748,25 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   const int64_t a1 = min(a0 + per, s1);
   int64_t c = 0;
   for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(words[w]);
+  int64_t pre = 0;
+  for (int64_t i = threadIdx.x; i < (int64_t)blockIdx.x; i += kBlock) pre += seg_parts[i].count;
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
-  if (lane == 0) wcount[wave] = c;
+  for (int m = 32; m >= 1; m >>= 1) {
+    c += __shfl_xor(c, m);
+    pre += __shfl_xor(pre, m);
+  }
+  if (lane == 0) {
+    wcount[wave] = c;
+    wpre[wave] = pre;
+  }
   __syncthreads();
-  int64_t off = seg_offsets[blockIdx.x];
+  int64_t off = 0;
+  for (int k = 0; k < kWaves; ++k) off += wpre[k];
+  if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) {
+    int64_t all = off;
+    for (int k = 0; k < kWaves; ++k) all += wcount[k];
+    *total = all;
+  }
   for (int k = 0; k < wave; ++k) off += wcount[k];
   for (int64_t base = a0; base < a1; base += 64) {
     const uint64_t mw = base + lane < a1 ? words[base + lane] : 0ull;
@@ -903,6 +889,75 @@ __global__ __launch_bounds__(kBlock) void k_index_build(KCol col, int64_t nrows,
   }
 }
 
+// The same for a 4-byte column: lane l of a wave loads rows l, 64+l, 128+l,
+// 192+l of a 256-row tile (four coalesced 256-byte loads), so the wave ballot
+// of each compare IS one BitSet word -- per value and tile: 4 compares, 4
+// ballots, 4 scalar popcounts, one store by lanes 0..3.  U tiles in flight
+// per wave; every output's segment count is accumulated in wave-private LDS
+// slots (no separate popcount pass).
+struct IndexArgs4 {
+  uint64_t* out[64];
+  Partial* segs[64];
+};
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_index_build4(const int32_t* __restrict__ col, int32_t kind,
+                                                         int64_t nrows, const uint64_t* __restrict__ del,
+                                                         const uint32_t* __restrict__ vals, int32_t nvalues,
+                                                         IndexArgs4 A, int64_t tiles_per_block) {
+  __shared__ uint32_t cnt[kWaves][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  cnt[wave][lane] = 0u;
+  const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * tiles_per_block;
+  const int64_t t1 = min(t0 + tiles_per_block, ntiles);
+  for (int64_t base = t0 + wave; base < t1; base += (int64_t)kWaves * U) {
+    int32_t x[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t t = base + (int64_t)u * kWaves;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t r = t * kTileRows + j * 64 + lane;
+        x[u][j] = (t < t1 && r < nrows) ? __builtin_nontemporal_load(col + r) : 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t t = base + (int64_t)u * kWaves;
+      if (t >= t1) continue;
+      uint64_t live[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t w = t * kWordsPerTile + j;
+        live[j] = __ballot(w * 64 + lane < nrows) & ((del && w < nwords) ? ~del[w] : ~0ull);
+      }
+      for (int v = 0; v < nvalues; ++v) {
+        const uint32_t lit = vals[v];
+        uint64_t m[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool eq = kind == kReal ? __int_as_float(x[u][j]) == __uint_as_float(lit) : x[u][j] == (int32_t)lit;
+          m[j] = __ballot(eq) & live[j];
+        }
+        const uint64_t mine = lane == 0 ? m[0] : (lane == 1 ? m[1] : (lane == 2 ? m[2] : m[3]));
+        const int64_t w = t * kWordsPerTile + lane;
+        if (lane < 4 && w < nwords) A.out[v][w] = mine;
+        if (lane == 0) cnt[wave][v] += (uint32_t)(__popcll(m[0]) + __popcll(m[1]) + __popcll(m[2]) + __popcll(m[3]));
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nvalues) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) c += cnt[k][threadIdx.x];
+    A.segs[threadIdx.x][blockIdx.x].count = c;
+  }
+}
+
 // ---------------------------------------------------------------- launchers
 
 constexpr int kDefaultU = 2;
@@ -1017,18 +1072,14 @@ hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t wo
   return hipGetLastError();
 }
 
-hipError_t launch_seg_scan(const Partial* seg_parts, int64_t nseg, int64_t* seg_offsets, int64_t* total,
-                           hipStream_t s) {
-  hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(1024), 0, s, seg_parts, nseg, seg_offsets, total);
-  return hipGetLastError();
-}
 
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
-                              const int64_t* seg_offsets, int64_t row_offset, int64_t* ids, const ProjCol* proj,
-                              void* const* out, int32_t nproj, const int64_t* total, hipStream_t s) {
-  const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
+                              const Partial* seg_parts, int64_t row_offset, int64_t* ids, const ProjCol* proj,
+                              void* const* out, int32_t nproj, int64_t* total, hipStream_t s) {
+  if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
+  const int64_t g = (nwords + words_per_block - 1) / words_per_block;
   hipLaunchKernelGGL(k_select_ids, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
-                     seg_offsets, row_offset, ids);
+                     seg_parts, row_offset, ids, total);
   if (nproj > 0) {
     MatArgs M;
     M.nproj = nproj;
@@ -1037,6 +1088,24 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
       M.out[j] = out[j];
     }
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(kBlock), 0, s, ids, total, row_offset, M);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_index_build4(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
+                               int32_t nvalues, uint64_t* const* outs, Partial* const* segs, int64_t words_per_block,
+                               hipStream_t s) {
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
+  for (int32_t v0 = 0; v0 < nvalues; v0 += 64) {
+    IndexArgs4 A;
+    const int32_t nv = nvalues - v0 < 64 ? nvalues - v0 : 64;
+    for (int i = 0; i < nv; ++i) {
+      A.out[i] = outs[v0 + i];
+      A.segs[i] = segs[v0 + i];
+    }
+    hipLaunchKernelGGL(k_index_build4<2>, dim3((unsigned)g), dim3(kBlock), 0, s, (const int32_t*)col.base, col.kind,
+                       nrows, deleted, values + v0, nv, A, words_per_block / kWordsPerTile);
   }
   return hipGetLastError();
 }

@@ -1,0 +1,127 @@
+// mbx_objects.hpp -- host-side objects behind the opaque handles of
+// include/mbx.h and include/mbx_db.h, shared by mbx_api.cpp (scans, bitmaps,
+// cursors) and mbx_db.cpp (Minibase DB files).  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/mbx.h"
+#include "mbx_internal.hpp"
+
+namespace mbx {
+
+// ------------------------------------------------------------------ errors
+
+// sets the thread-local message mbx_last_error() returns; returns `code`
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess) return fail(MBX_E_DEVICE, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define NOTNULL(p) \
+  do {             \
+    if (!(p)) return fail(MBX_E_INVALID, "%s: null argument `%s`", __func__, #p); \
+  } while (0)
+
+}  // namespace mbx
+
+// ----------------------------------------------------------------- objects
+
+using mbx::AggOut;
+using mbx::KPlan;
+using mbx::Partial;
+
+struct mbx_ctx {
+  int32_t device = 0;
+  hipStream_t stream = nullptr;
+  Partial* partials = nullptr;  // scratch, one per block of the largest scan so far
+  int64_t partials_cap = 0;
+  AggOut* dagg = nullptr;
+  int64_t* dcount = nullptr;
+  int32_t* dnan = nullptr;
+  uint32_t* ticket = nullptr;   // in-launch finalize ticket (always 0 between launches)
+  int64_t* ids_scratch = nullptr;  // positions for a gather whose caller wants no positions
+  int64_t ids_cap = 0;
+  void* pinned = nullptr;       // 256 bytes of pinned host scratch
+};
+
+struct TCol {
+  int32_t attr_type = 0;
+  int32_t size = 0;
+  int32_t stride_w = 1;  // device words per row
+  void* dev = nullptr;
+  bool owned = false;
+};
+
+struct mbx_table {
+  mbx_ctx* ctx = nullptr;
+  int64_t nrows = 0;
+  int64_t row_offset = 0;
+  std::vector<TCol> cols;
+  uint64_t* deleted = nullptr;
+  bool owns_deleted = false;
+  bool aligned16 = true;
+};
+
+struct PlanVariant {
+  int32_t agg_col = -1;  // -1: filter only
+  KPlan* dev = nullptr;
+  int32_t fast_k = 0;
+  int32_t fast_ks = 0;
+  int32_t agg_kind = mbx::kInt;
+};
+
+struct mbx_plan {
+  mbx_ctx* ctx = nullptr;
+  const mbx_table* t = nullptr;
+  KPlan host{};
+  std::vector<int32_t> slot_col;  // table column of each slot
+  bool all_literal = true;        // every term is `column OP literal`
+  bool str_lit_fits16 = true;     // every string literal is <= 16 bytes
+  std::deque<PlanVariant> variants;
+};
+
+struct mbx_bitmap {
+  mbx_ctx* ctx = nullptr;
+  int64_t nbits = 0;
+  int64_t nwords = 0;
+  uint64_t* words = nullptr;
+  int64_t wpb = 4;        // words per segment
+  int64_t nseg = 1;
+  Partial* segs = nullptr;  // per-segment counts (Partial.count)
+  int64_t count = -1;     // host copy of the cardinality, -1 = unknown
+};
+
+struct mbx_cursor {
+  mbx_ctx* ctx = nullptr;
+  int64_t count = 0;
+  int64_t next = 0;
+  const mbx_table* t = nullptr;
+  int64_t* ids = nullptr;  // device
+  std::vector<void*> outs; // device, one per projected column
+  std::vector<int32_t> proj;
+};
+
+namespace mbx {
+
+int set_device(mbx_ctx* c);
+int32_t stride_words(const mbx_col_desc& d);
+int check_cols(const mbx_col_desc* cols, int32_t ncols);
+int64_t words_for(int64_t nbits);
+// a table whose device columns (and, with_deleted, deleted words) are
+// allocated but not filled; the caller writes them on the context stream
+int table_alloc(mbx_ctx* c, const mbx_col_desc* cols, int32_t ncols, int64_t nrows, int64_t row_offset,
+                bool with_deleted, mbx_table** out);
+int bitmap_new(mbx_ctx* c, int64_t nbits, mbx_bitmap** out);
+// recount per-segment popcounts of a bitmap written on the device, sync, and
+// set b->count
+int bitmap_recount(mbx_ctx* c, mbx_bitmap* b);
+
+}  // namespace mbx

@@ -401,3 +401,31 @@ def test_string_slot_shapes(ctx, width):
         bm, words_g = gpu_select(ctx, t, cnf)
         assert np.array_equal(words_g, w_o), cnf
         assert ctx.scan_count(ctx.compile(t, cnf)) == n_o
+
+
+@pytest.mark.parametrize("n", [1, 63, 257, 4099, 1_000_003])
+@pytest.mark.parametrize("deleted", [False, True])
+def test_index_build_int_shapes(ctx, n, deleted):
+    """k_index_build4 (4-byte columns): ragged tails, deleted rows left clear
+    (createBitMapIndex walks a ColumnScan), > 64 values (two launches), the
+    per-segment counts it writes (count + positions must agree)."""
+    cols, dele = int_table(n, hi=70, deleted_frac=0.1 if deleted else None)
+    ot, t = oracle.Table(cols, dele), ctx.stage(cols, dele)
+    vals = list(range(72))
+    bms = ctx.index_build(t, 1, [("int", v) for v in vals])
+    for v, bm in zip(vals, bms):
+        n_o, w_o = oracle.bitmap_eq(ot, 1, ("int", v))
+        assert bm.count == n_o and np.array_equal(bm.download(), w_o), v
+    ids_o = oracle.words_to_positions(oracle.bitmap_eq(ot, 1, ("int", 5))[1])
+    assert np.array_equal(ctx.select(bms[5]), ids_o)
+
+
+def test_index_build_float_column(ctx):
+    n = 100_003
+    rng = np.random.Generator(np.random.PCG64(9))
+    f = rng.integers(0, 5, n).astype(np.float32) * np.float32(0.25)
+    cols = [(oracle.INTEGER, 4, rng.integers(0, 9, n, dtype=np.int32)), (oracle.REAL, 4, f)]
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    for v, bm in zip([0.0, 0.25, 0.5, 3.0], ctx.index_build(t, 1, [("real", x) for x in [0.0, 0.25, 0.5, 3.0]])):
+        n_o, w_o = oracle.bitmap_eq(ot, 1, ("real", v))
+        assert bm.count == n_o and np.array_equal(bm.download(), w_o)
