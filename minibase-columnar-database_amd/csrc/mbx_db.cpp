@@ -1,0 +1,982 @@
+// mbx_db.cpp -- Minibase DB files (include/mbx_db.h): the page formats of
+// the reference's disk manager, heap files, Columnarfile and BitMapFile,
+// restated in C++ over an mmap of the DB file, plus the GPU staging path.
+//
+// The writer replays the reference's page-allocation order (first fit over
+// the space map, DB.allocate_page, R/diskmgr/DB.java:212-290) for the same
+// sequence of calls: Heapfile(name) (Heapfile.java:349-390), insertRecord
+// (Heapfile.java:420-520), HFPage.insertRecord (HFPage.java:337-396),
+// Columnarfile(...) (Columnarfile.java:60-192), insertTuple
+// (Columnarfile.java:400-470), BitMapFile(name, true) / BM.insertBitSet
+// (BitMapFile.java:60-120, BM.java:60-120).  Only page bytes the reference
+// defines are written; nothing about the JVM's buffer pool is modelled.
+//
+// The reader feeds mbx_db_stage: host code only walks directories (page ids
+// per column, schema records, the .md BitSet); every record is decoded on
+// the GPU (mbx_pages.hip).
+#include "../../include/mbx_db.h"
+
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "mbx_internal.hpp"
+#include "mbx_objects.hpp"
+
+using namespace mbx;
+
+namespace {
+
+constexpr int kPage = kDbPage;
+constexpr int kMaxSpace = 1024;                    // GlobalConst.MAX_SPACE
+constexpr int kBitsPerMapPage = kMaxSpace * 8;     // DB.bits_per_page
+constexpr int32_t kInvalidPage = -1;               // GlobalConst.INVALID_PAGE
+constexpr int kMaxName = MBX_DB_MAX_NAME;
+constexpr int kFileEntry = 4 + kMaxName + 2;       // DBHeaderPage.SIZE_OF_FILE_ENTRY
+constexpr int kStartEntries = 8;                   // DBHeaderPage.START_FILE_ENTRIES
+constexpr int kFirstPageUsed = 8 + 8 + 4;          // PageUsedBytes.FIRST_PAGE_USED_BYTES
+constexpr int kDirPageUsed = 8 + 8;                // PageUsedBytes.DIR_PAGE_USED_BYTES
+// HFPage header fields (HFPage.java:31-40)
+constexpr int kSlotCnt = 0, kUsedPtr = 2, kFreeSpace = 4, kType = 6, kPrev = 8, kNext = 12, kCur = 16;
+constexpr int kDpFixed = kDbSlotBase;
+constexpr int kSlotSize = 4;
+constexpr int kDpInfoSize = 8;                      // DataPageInfo.size
+constexpr int kRecsPerDirPage = (kPage - kDpFixed) / (kSlotSize + kDpInfoSize);  // 83
+constexpr int kBmRecord = kMaxSpace - kDpFixed - kSlotSize;                      // 1000
+constexpr int16_t kBmHead = 13;                     // NodeType.BMHEAD
+constexpr int kAttrNameCell = MBX_DB_MAX_ATTR_NAME + 2;
+
+inline int32_t get32(const uint8_t* p) {
+  return (int32_t)(((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3]);
+}
+inline void put32(uint8_t* p, int32_t v) {
+  p[0] = (uint8_t)((uint32_t)v >> 24);
+  p[1] = (uint8_t)((uint32_t)v >> 16);
+  p[2] = (uint8_t)((uint32_t)v >> 8);
+  p[3] = (uint8_t)v;
+}
+inline int16_t get16(const uint8_t* p) { return (int16_t)(((uint32_t)p[0] << 8) | (uint32_t)p[1]); }
+inline void put16(uint8_t* p, int32_t v) {
+  p[0] = (uint8_t)((uint32_t)v >> 8);
+  p[1] = (uint8_t)v;
+}
+
+// DataOutputStream.writeUTF of a byte string that is already modified UTF-8
+// (file and attribute names here are ASCII)
+inline void put_utf(uint8_t* p, const std::string& s) {
+  put16(p, (int32_t)s.size());
+  memcpy(p + 2, s.data(), s.size());
+}
+inline std::string get_utf(const uint8_t* p, int32_t cap) {
+  int32_t n = (uint16_t)get16(p);
+  if (n > cap - 2) n = cap - 2;
+  return std::string((const char*)p + 2, (size_t)(n > 0 ? n : 0));
+}
+
+int32_t recs_per_data_page(int32_t rec_len) { return (kPage - kDpFixed) / (kSlotSize + rec_len); }
+
+int32_t record_len(const mbx_col_desc& d) { return d.attr_type == MBX_ATTR_STRING ? d.size + 2 : 4; }
+
+struct HeapHint {
+  int32_t reclen = 0;     // valid for records at least this long
+  int32_t dir_pid = kInvalidPage;
+  int32_t dir_slot = 0;   // first directory slot worth checking
+};
+
+}  // namespace
+
+struct mbx_db {
+  std::string path;
+  int fd = -1;
+  uint8_t* base = nullptr;
+  size_t bytes = 0;
+  int32_t num_pages = 0;
+  int32_t num_map_pages = 0;
+  int64_t alloc_hint = 0;  // every page below is allocated
+  std::unordered_map<int32_t, HeapHint> hints;  // per heap file (first dir page)
+
+  uint8_t* page(int32_t pid) { return base + (size_t)pid * kPage; }
+};
+
+namespace {
+
+// -------------------------------------------------------------- space map
+
+bool page_bit(mbx_db* db, int64_t pid) {
+  const uint8_t* map = db->page(1);  // map pages are contiguous from page 1
+  return (map[pid >> 3] >> (pid & 7)) & 1;
+}
+
+void set_page_bit(mbx_db* db, int64_t pid, bool on) {
+  uint8_t* map = db->page(1);
+  if (on)
+    map[pid >> 3] |= (uint8_t)(1u << (pid & 7));
+  else
+    map[pid >> 3] &= (uint8_t)~(1u << (pid & 7));
+}
+
+// DB.allocate_page(start, 1): first zero bit of the space map
+int alloc_page(mbx_db* db, int32_t* pid) {
+  for (int64_t p = db->alloc_hint; p < db->num_pages; ++p) {
+    if (!page_bit(db, p)) {
+      set_page_bit(db, p, true);
+      db->alloc_hint = p + 1;
+      *pid = (int32_t)p;
+      return MBX_OK;
+    }
+  }
+  db->alloc_hint = db->num_pages;
+  return fail(MBX_E_NOMEM, "OutOfSpaceException: DB %s has no free page (%d pages)", db->path.c_str(),
+              db->num_pages);
+}
+
+// ----------------------------------------------------------- file entries
+
+// DBHeaderPage(page, usedBytes): next = -1, entry count, every entry pid -1
+void init_header_page(uint8_t* pg, int used) {
+  put32(pg, kInvalidPage);
+  const int n = (kMaxSpace - used) / kFileEntry;
+  put32(pg + 4, n);
+  for (int i = 0; i < n; ++i) put32(pg + kStartEntries + i * kFileEntry, kInvalidPage);
+}
+
+int32_t get_file_entry(mbx_db* db, const std::string& name) {
+  int32_t hp = 0;
+  int guard = 0;
+  while (hp != kInvalidPage && hp >= 0 && hp < db->num_pages && guard++ < db->num_pages) {
+    uint8_t* pg = db->page(hp);
+    const int32_t n = get32(pg + 4);
+    for (int32_t e = 0; e < n && kStartEntries + (e + 1) * kFileEntry <= kPage; ++e) {
+      const uint8_t* ent = pg + kStartEntries + e * kFileEntry;
+      const int32_t pid = get32(ent);
+      if (pid != kInvalidPage && get_utf(ent + 4, kMaxName + 2) == name) return pid;
+    }
+    hp = get32(pg);
+  }
+  return kInvalidPage;
+}
+
+// DB.add_file_entry (DB.java:420-500)
+int add_file_entry(mbx_db* db, const std::string& name, int32_t start) {
+  if ((int)name.size() >= kMaxName) return fail(MBX_E_INVALID, "FileNameTooLongException: %s", name.c_str());
+  if (get_file_entry(db, name) != kInvalidPage) return fail(MBX_E_INVALID, "DuplicateEntryException: %s", name.c_str());
+  int32_t hp = 0;
+  for (;;) {
+    uint8_t* pg = db->page(hp);
+    const int32_t n = get32(pg + 4);
+    for (int32_t e = 0; e < n; ++e) {
+      uint8_t* ent = pg + kStartEntries + e * kFileEntry;
+      if (get32(ent) == kInvalidPage) {
+        put32(ent, start);
+        put_utf(ent + 4, name);
+        return MBX_OK;
+      }
+    }
+    const int32_t next = get32(pg);
+    if (next != kInvalidPage) {
+      hp = next;
+      continue;
+    }
+    int32_t np;
+    int rc = alloc_page(db, &np);
+    if (rc) return rc;
+    put32(pg, np);
+    init_header_page(db->page(np), kDirPageUsed);
+    hp = np;
+  }
+}
+
+// ----------------------------------------------------------------- HFPage
+
+void hf_init(uint8_t* pg, int32_t pid) {
+  put16(pg + kSlotCnt, 0);
+  put32(pg + kCur, pid);
+  put32(pg + kPrev, kInvalidPage);
+  put32(pg + kNext, kInvalidPage);
+  put16(pg + kUsedPtr, kMaxSpace);
+  put16(pg + kFreeSpace, kMaxSpace - kDpFixed);
+}
+
+int32_t hf_available(const uint8_t* pg) { return get16(pg + kFreeSpace) - kSlotSize; }
+int32_t hf_slot_len(const uint8_t* pg, int32_t s) { return get16(pg + kDpFixed + s * kSlotSize); }
+int32_t hf_slot_off(const uint8_t* pg, int32_t s) { return (uint16_t)get16(pg + kDpFixed + s * kSlotSize + 2); }
+
+// HFPage.insertRecord: -1 when it does not fit
+int32_t hf_insert(uint8_t* pg, const uint8_t* rec, int32_t len) {
+  int32_t free_space = get16(pg + kFreeSpace);
+  if (len + kSlotSize > free_space) return -1;
+  const int32_t cnt = get16(pg + kSlotCnt);
+  int32_t i = 0;
+  while (i < cnt && hf_slot_len(pg, i) != -1) ++i;
+  if (i == cnt) {
+    free_space -= len + kSlotSize;
+    put16(pg + kSlotCnt, cnt + 1);
+  } else {
+    free_space -= len;
+  }
+  put16(pg + kFreeSpace, free_space);
+  const int32_t used = get16(pg + kUsedPtr) - len;
+  put16(pg + kUsedPtr, used);
+  put16(pg + kDpFixed + i * kSlotSize, len);
+  put16(pg + kDpFixed + i * kSlotSize + 2, used);
+  memcpy(pg + used, rec, (size_t)len);
+  return i;
+}
+
+// ---------------------------------------------------------------- Heapfile
+
+// Heapfile(name): existing first directory page, or a new one (newPage,
+// add_file_entry, init -- in that order)
+int heap_open(mbx_db* db, const std::string& name, bool create, int32_t* first_dir) {
+  *first_dir = get_file_entry(db, name);
+  if (*first_dir != kInvalidPage || !create) return MBX_OK;
+  int32_t pid;
+  int rc = alloc_page(db, &pid);
+  if (rc) return rc;
+  if ((rc = add_file_entry(db, name, pid))) return rc;
+  hf_init(db->page(pid), pid);
+  *first_dir = pid;
+  return MBX_OK;
+}
+
+// Heapfile.insertRecord: the first data page (directory order) whose
+// availspace fits the record, else a new data page registered in the first
+// directory page with room for a DataPageInfo, else a new directory page.
+int heap_insert(mbx_db* db, int32_t first_dir, const uint8_t* rec, int32_t len, int32_t* rid_pid,
+                int32_t* rid_slot) {
+  HeapHint& h = db->hints[first_dir];
+  int32_t dir = first_dir;
+  int32_t s0 = 0;
+  if (h.dir_pid != kInvalidPage && len >= h.reclen) {
+    dir = h.dir_pid;
+    s0 = h.dir_slot;
+  }
+  int32_t found_dir = kInvalidPage, found_slot = -1;
+  for (;;) {
+    uint8_t* dp = db->page(dir);
+    const int32_t cnt = get16(dp + kSlotCnt);
+    for (int32_t s = s0; s < cnt; ++s) {
+      if (hf_slot_len(dp, s) == -1) continue;
+      const uint8_t* info = dp + hf_slot_off(dp, s);
+      if (len <= get16(info)) {
+        found_dir = dir;
+        found_slot = s;
+        break;
+      }
+    }
+    if (found_slot >= 0) break;
+    if (hf_available(dp) >= kDpInfoSize) {
+      int32_t np;
+      int rc = alloc_page(db, &np);
+      if (rc) return rc;
+      uint8_t* pg = db->page(np);
+      hf_init(pg, np);
+      uint8_t info[kDpInfoSize];
+      put16(info, hf_available(pg));
+      put16(info + 2, 0);
+      put32(info + 4, np);
+      found_slot = hf_insert(dp, info, kDpInfoSize);
+      if (found_slot < 0) return fail(MBX_E_INVALID, "HFException: no space to insert rec.");
+      found_dir = dir;
+      break;
+    }
+    int32_t next = get32(dp + kNext);
+    if (next == kInvalidPage) {
+      int rc = alloc_page(db, &next);
+      if (rc) return rc;
+      uint8_t* ndp = db->page(next);
+      hf_init(ndp, next);
+      put32(ndp + kNext, kInvalidPage);
+      put32(ndp + kPrev, dir);
+      put32(dp + kNext, next);
+    }
+    dir = next;
+    s0 = 0;
+  }
+  uint8_t* dp = db->page(found_dir);
+  uint8_t* info = dp + hf_slot_off(dp, found_slot);
+  const int32_t data_pid = get32(info + 4);
+  uint8_t* pg = db->page(data_pid);
+  const int32_t slot = hf_insert(pg, rec, len);
+  if (slot < 0) return fail(MBX_E_INVALID, "SpaceNotAvailableException: no available space");
+  put16(info + 2, get16(info + 2) + 1);
+  put16(info, hf_available(pg));
+  h.reclen = len;
+  h.dir_pid = found_dir;
+  h.dir_slot = found_slot;
+  *rid_pid = data_pid;
+  *rid_slot = slot;
+  return MBX_OK;
+}
+
+// one entry per DataPageInfo in directory order: page index (the position
+// formula's dirPageIndex * 83 + dirSlot, Heapfile.loadPositionBuffer) + pid
+struct DataPage {
+  int64_t index;
+  int32_t pid;
+  int32_t recct;
+};
+
+int heap_pages(mbx_db* db, int32_t first_dir, std::vector<DataPage>* out) {
+  out->clear();
+  int32_t dir = first_dir;
+  int64_t dir_index = 0;
+  while (dir != kInvalidPage) {
+    if (dir < 0 || dir >= db->num_pages || dir_index > db->num_pages)
+      return fail(MBX_E_INVALID, "heapfile directory chain leaves the DB at page %d", dir);
+    const uint8_t* dp = db->page(dir);
+    const int32_t cnt = get16(dp + kSlotCnt);
+    for (int32_t s = 0; s < cnt && s < kRecsPerDirPage + 1; ++s) {
+      if (hf_slot_len(dp, s) == -1) continue;
+      const uint8_t* info = dp + hf_slot_off(dp, s);
+      DataPage d;
+      d.index = dir_index * kRecsPerDirPage + s;
+      d.pid = get32(info + 4);
+      d.recct = get16(info + 2);
+      if (d.pid < 0 || d.pid >= db->num_pages) return fail(MBX_E_INVALID, "DataPageInfo names page %d", d.pid);
+      out->push_back(d);
+    }
+    dir = get32(dp + kNext);
+    ++dir_index;
+  }
+  return MBX_OK;
+}
+
+// heap.Scan order: directory order, then slot order within a data page
+template <typename F>
+int heap_scan(mbx_db* db, int32_t first_dir, F&& fn) {
+  std::vector<DataPage> pages;
+  int rc = heap_pages(db, first_dir, &pages);
+  if (rc) return rc;
+  for (const DataPage& d : pages) {
+    const uint8_t* pg = db->page(d.pid);
+    const int32_t cnt = get16(pg + kSlotCnt);
+    for (int32_t s = 0; s < cnt; ++s) {
+      const int32_t len = hf_slot_len(pg, s);
+      if (len == -1) continue;
+      const int32_t off = hf_slot_off(pg, s);
+      if (len < 0 || off + len > kPage) return fail(MBX_E_INVALID, "corrupt slot %d on page %d", s, d.pid);
+      if (!fn(d, s, pg + off, len)) return MBX_OK;
+    }
+  }
+  return MBX_OK;
+}
+
+// ---------------------------------------------------------------- BitMapFile
+
+// BitMapFile header page: new BMIndexPage (newPage + HFPage.init), type
+// BMHEAD (initBitMapHeaderPage), then add_file_entry
+int bm_create_header(mbx_db* db, const std::string& name, int32_t* head) {
+  int rc = alloc_page(db, head);
+  if (rc) return rc;
+  uint8_t* pg = db->page(*head);
+  hf_init(pg, *head);
+  put16(pg + kType, kBmHead);
+  return add_file_entry(db, name, *head);
+}
+
+// BM.readBitSet: the first record of every page of the chain, concatenated
+int bm_read_bytes(mbx_db* db, int32_t head, std::vector<uint8_t>* bytes) {
+  bytes->clear();
+  int32_t p = head;
+  int guard = 0;
+  while (p != kInvalidPage) {
+    if (p < 0 || p >= db->num_pages || guard++ > db->num_pages)
+      return fail(MBX_E_INVALID, "BitMapFile chain leaves the DB at page %d", p);
+    const uint8_t* pg = db->page(p);
+    const int32_t cnt = get16(pg + kSlotCnt);
+    int32_t s = 0;
+    while (s < cnt && hf_slot_len(pg, s) == -1) ++s;
+    if (s == cnt) return fail(MBX_E_INVALID, "InvalidSlotNumberException: BitMapFile page %d holds no record", p);
+    const int32_t len = hf_slot_len(pg, s), off = hf_slot_off(pg, s);
+    if (len < 0 || off + len > kPage) return fail(MBX_E_INVALID, "corrupt BitMapFile page %d", p);
+    bytes->insert(bytes->end(), pg + off, pg + off + len);
+    p = get32(pg + kNext);
+  }
+  return MBX_OK;
+}
+
+// BitSet.toByteArray(): little-endian bytes up to the last non-zero one
+std::vector<uint8_t> bitset_bytes(const uint64_t* words, int64_t nwords) {
+  int64_t nb = nwords * 8;
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(words);
+  while (nb > 0 && b[nb - 1] == 0) --nb;
+  return std::vector<uint8_t>(b, b + nb);
+}
+
+// BM.insertBitSet into a header page with no record yet: 1000-byte chunks,
+// header page first, then new pages chained by next / prev
+int bm_insert_bitset(mbx_db* db, int32_t head, const std::vector<uint8_t>& bytes) {
+  const int64_t nchunks = ((int64_t)bytes.size() + kBmRecord - 1) / kBmRecord;
+  if (nchunks == 0) return fail(MBX_E_INVALID, "BM.insertBitSet: empty BitSet (no chunk to store)");
+  int32_t prev = kInvalidPage;
+  int32_t cur = head;
+  std::vector<uint8_t> rec(kBmRecord);
+  for (int64_t i = 0; i < nchunks; ++i) {
+    if (i > 0) {
+      int rc = alloc_page(db, &cur);
+      if (rc) return rc;
+      hf_init(db->page(cur), cur);
+    }
+    std::fill(rec.begin(), rec.end(), 0);
+    const int64_t start = i * kBmRecord;
+    const int64_t n = std::min<int64_t>(kBmRecord, (int64_t)bytes.size() - start);
+    memcpy(rec.data(), bytes.data() + start, (size_t)n);
+    uint8_t* pg = db->page(cur);
+    if (hf_insert(pg, rec.data(), kBmRecord) < 0) return fail(MBX_E_INVALID, "BitMapFile page %d is full", cur);
+    put32(pg + kNext, kInvalidPage);
+    put32(pg + kPrev, prev);
+    if (prev != kInvalidPage) put32(db->page(prev) + kNext, cur);
+    prev = cur;
+  }
+  return MBX_OK;
+}
+
+// BitMapFile.insert(position) on an existing file (the .md BitSet): set the
+// bit inside its 1000-byte chunk, creating chunk pages up to it
+int bm_set_bit(mbx_db* db, int32_t head, int64_t position) {
+  const int64_t chunk = position / (kBmRecord * 8);
+  int32_t p = head;
+  for (int64_t i = 0;; ++i) {
+    uint8_t* pg = db->page(p);
+    if (i == chunk) {
+      const int32_t cnt = get16(pg + kSlotCnt);
+      int32_t s = 0;
+      while (s < cnt && hf_slot_len(pg, s) == -1) ++s;
+      if (s == cnt) return fail(MBX_E_INVALID, "BitMapFile page %d holds no record", p);
+      uint8_t* rec = pg + hf_slot_off(pg, s);
+      const int64_t bit = position - chunk * kBmRecord * 8;
+      rec[bit >> 3] |= (uint8_t)(1u << (bit & 7));
+      return MBX_OK;
+    }
+    int32_t next = get32(pg + kNext);
+    if (next == kInvalidPage) {
+      int rc = alloc_page(db, &next);
+      if (rc) return rc;
+      uint8_t* npg = db->page(next);
+      hf_init(npg, next);
+      std::vector<uint8_t> zero(kBmRecord, 0);
+      hf_insert(npg, zero.data(), kBmRecord);
+      put32(npg + kNext, kInvalidPage);
+      put32(npg + kPrev, p);
+      put32(pg + kNext, next);
+    }
+    p = next;
+  }
+}
+
+// ----------------------------------------------------------- Columnarfile
+
+struct Schema {
+  int32_t ncols = 0;
+  std::vector<mbx_col_desc> cols;
+  std::vector<std::string> names;
+  std::vector<uint8_t> btree_exist, bitmap_exist;
+  std::vector<std::string> bm_values;  // "col.value" records
+};
+
+int read_schema(mbx_db* db, const std::string& name, Schema* sc) {
+  const int32_t hdr = get_file_entry(db, name + ".hdr");
+  if (hdr == kInvalidPage) return fail(MBX_E_INVALID, "Columnar File does not exist: %s", name.c_str());
+  std::vector<std::vector<uint8_t>> recs;
+  int rc = heap_scan(db, hdr, [&](const DataPage&, int32_t, const uint8_t* r, int32_t len) {
+    recs.emplace_back(r, r + len);
+    return true;
+  });
+  if (rc) return rc;
+  if (recs.size() < 6 || recs[0].size() < 4) return fail(MBX_E_INVALID, "Columnar File does not exist: %s", name.c_str());
+  sc->ncols = get32(recs[0].data());
+  const int32_t n = sc->ncols;
+  if (n <= 0 || (int64_t)recs[1].size() < 4LL * n || (int64_t)recs[2].size() < 4LL * n ||
+      (int64_t)recs[3].size() < (int64_t)kAttrNameCell * n)
+    return fail(MBX_E_INVALID, "%s.hdr: malformed header records", name.c_str());
+  sc->cols.resize((size_t)n);
+  sc->names.resize((size_t)n);
+  for (int32_t i = 0; i < n; ++i) {
+    sc->cols[(size_t)i].attr_type = get32(recs[1].data() + 4 * i);
+    sc->cols[(size_t)i].size = get32(recs[2].data() + 4 * i);
+    sc->names[(size_t)i] = get_utf(recs[3].data() + kAttrNameCell * i, kAttrNameCell);
+  }
+  sc->btree_exist = recs[4];
+  sc->bitmap_exist = recs[5];
+  for (size_t k = 6; k < recs.size(); ++k) sc->bm_values.push_back(get_utf(recs[k].data(), (int32_t)recs[k].size()));
+  return MBX_OK;
+}
+
+int open_db_file(const char* path, bool create, int32_t num_pages, mbx_db** out) {
+  *out = nullptr;
+  if (!path) return fail(MBX_E_INVALID, "DB: null path");
+  const int fd = create ? ::open(path, O_RDWR | O_CREAT | O_TRUNC, 0644) : ::open(path, O_RDWR);
+  if (fd < 0) return fail(MBX_E_INVALID, "FileIOException: cannot open %s", path);
+  if (create) {
+    if (num_pages < 2) num_pages = 2;
+    if (ftruncate(fd, (off_t)num_pages * kPage) != 0) {
+      ::close(fd);
+      return fail(MBX_E_NOMEM, "FileIOException: cannot size %s to %d pages", path, num_pages);
+    }
+  } else {
+    struct stat st;
+    uint8_t first[kPage];
+    if (fstat(fd, &st) != 0 || st.st_size < kPage || pread(fd, first, kPage, 0) != kPage) {
+      ::close(fd);
+      return fail(MBX_E_INVALID, "InvalidPageNumberException: %s is not a Minibase DB", path);
+    }
+    num_pages = get32(first + kPage - 4);
+    if (num_pages < 2 || (int64_t)num_pages * kPage > (int64_t)st.st_size) {
+      ::close(fd);
+      return fail(MBX_E_INVALID, "%s: numDBPages %d does not match the file size", path, num_pages);
+    }
+  }
+  mbx_db* db = new (std::nothrow) mbx_db();
+  if (!db) {
+    ::close(fd);
+    return fail(MBX_E_NOMEM, "DB: host allocation");
+  }
+  db->path = path;
+  db->fd = fd;
+  db->num_pages = num_pages;
+  db->num_map_pages = (num_pages + kBitsPerMapPage - 1) / kBitsPerMapPage;
+  db->bytes = (size_t)num_pages * kPage;
+  void* m = mmap(nullptr, db->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (m == MAP_FAILED) {
+    ::close(fd);
+    delete db;
+    return fail(MBX_E_NOMEM, "DB: mmap of %s failed", path);
+  }
+  db->base = (uint8_t*)m;
+  if (create) {
+    // DBFirstPage(page): header entries, numDBPages; space map: pages
+    // 0 .. num_map_pages are in use (DB.openDB(name, num_pgs))
+    init_header_page(db->page(0), kFirstPageUsed);
+    put32(db->page(0) + kPage - 4, num_pages);
+    for (int64_t p = 0; p <= db->num_map_pages; ++p) set_page_bit(db, p, true);
+  }
+  db->alloc_hint = 0;
+  while (db->alloc_hint < db->num_pages && page_bit(db, db->alloc_hint)) ++db->alloc_hint;
+  *out = db;
+  return MBX_OK;
+}
+
+}  // namespace
+
+// ================================================================== C-ABI
+
+extern "C" int mbx_db_create(const char* path, int32_t num_pages, mbx_db** out) {
+  NOTNULL(out);
+  return open_db_file(path, true, num_pages, out);
+}
+
+extern "C" int mbx_db_open(const char* path, mbx_db** out) {
+  NOTNULL(out);
+  return open_db_file(path, false, 0, out);
+}
+
+extern "C" int mbx_db_close(mbx_db* db) {
+  if (!db) return MBX_OK;
+  int rc = MBX_OK;
+  if (db->base) {
+    if (msync(db->base, db->bytes, MS_SYNC) != 0) rc = fail(MBX_E_INVALID, "FileIOException: msync %s", db->path.c_str());
+    munmap(db->base, db->bytes);
+  }
+  if (db->fd >= 0) ::close(db->fd);
+  delete db;
+  return rc;
+}
+
+extern "C" int mbx_db_info(const mbx_db* cdb, int32_t* num_pages, int32_t* allocated_pages) {
+  NOTNULL(cdb);
+  mbx_db* db = const_cast<mbx_db*>(cdb);
+  if (num_pages) *num_pages = db->num_pages;
+  if (allocated_pages) {
+    int32_t n = 0;
+    for (int64_t p = 0; p < db->num_pages; ++p) n += page_bit(db, p) ? 1 : 0;
+    *allocated_pages = n;
+  }
+  return MBX_OK;
+}
+
+extern "C" int mbx_db_file_entry(mbx_db* db, const char* name, int32_t* first_page) {
+  NOTNULL(db);
+  NOTNULL(name);
+  NOTNULL(first_page);
+  *first_page = get_file_entry(db, name);
+  return MBX_OK;
+}
+
+extern "C" int mbx_db_columnar_create(mbx_db* db, const char* name, int32_t ncols, const mbx_col_desc* cols,
+                                      const char* const* attr_names) {
+  NOTNULL(db);
+  NOTNULL(name);
+  NOTNULL(cols);
+  NOTNULL(attr_names);
+  const std::string cf = name;
+  if ((int)cf.size() > MBX_DB_MAX_CF_NAME) return fail(MBX_E_INVALID, "File name too long: %s", name);
+  if (ncols <= 0 || ncols > 4096) return fail(MBX_E_INVALID, "Columnarfile: %d columns", ncols);
+  for (int32_t i = 0; i < ncols; ++i) {
+    if (!attr_names[i]) return fail(MBX_E_INVALID, "Columnarfile: attr_names[%d] is null", i);
+    if ((int)strlen(attr_names[i]) > MBX_DB_MAX_ATTR_NAME) return fail(MBX_E_INVALID, "Attribute name too long.");
+    const int32_t t = cols[i].attr_type;
+    if (t != MBX_ATTR_INTEGER && t != MBX_ATTR_REAL && t != MBX_ATTR_STRING)
+      return fail(MBX_E_TYPE, "Columnarfile: column %d has AttrType %d", i, t);
+    if (t == MBX_ATTR_STRING && (cols[i].size <= 0 || cols[i].size + 2 > kMaxSpace - kDpFixed - kSlotSize))
+      return fail(MBX_E_INVALID, "Columnarfile: char(%d) does not fit a page", cols[i].size);
+  }
+  if (get_file_entry(db, cf + ".hdr") != kInvalidPage)
+    return fail(MBX_E_INVALID, "Columnarfile %s already exists", name);
+  int32_t hdr;
+  int rc = heap_open(db, cf + ".hdr", true, &hdr);
+  if (rc) return rc;
+  // header records (Columnarfile.java:72-118)
+  std::vector<uint8_t> r_n(4), r_t(4 * (size_t)ncols), r_s(4 * (size_t)ncols), r_names((size_t)kAttrNameCell * ncols, 0),
+      r_bt((size_t)ncols, 0), r_bm((size_t)ncols, 0);
+  put32(r_n.data(), ncols);
+  for (int32_t i = 0; i < ncols; ++i) {
+    put32(r_t.data() + 4 * i, cols[i].attr_type);
+    put32(r_s.data() + 4 * i, cols[i].attr_type == MBX_ATTR_STRING ? cols[i].size : 4);
+    put_utf(r_names.data() + kAttrNameCell * i, attr_names[i]);
+  }
+  int32_t pid, slot;
+  for (const std::vector<uint8_t>* r : {&r_n, &r_t, &r_s, &r_names, &r_bt, &r_bm})
+    if ((rc = heap_insert(db, hdr, r->data(), (int32_t)r->size(), &pid, &slot))) return rc;
+  for (int32_t i = 0; i < ncols; ++i) {
+    int32_t first;
+    if ((rc = heap_open(db, cf + "." + std::to_string(i), true, &first))) return rc;
+  }
+  // markedDeleted = new BitMapFile(name + ".md", true): header page + one
+  // 1000-byte zero record
+  int32_t md;
+  if ((rc = bm_create_header(db, cf + ".md", &md))) return rc;
+  std::vector<uint8_t> zero(kBmRecord, 0);
+  if (hf_insert(db->page(md), zero.data(), kBmRecord) < 0) return fail(MBX_E_INVALID, ".md header page is full");
+  int32_t dtid;
+  return heap_open(db, cf + ".dtid", true, &dtid);
+}
+
+extern "C" int mbx_db_columnar_insert(mbx_db* db, const char* name, int64_t nrows, const void* const* host_cols) {
+  NOTNULL(db);
+  NOTNULL(name);
+  if (nrows < 0) return fail(MBX_E_INVALID, "insert: nrows %lld", (long long)nrows);
+  if (nrows == 0) return MBX_OK;
+  NOTNULL(host_cols);
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  for (uint8_t b : sc.bitmap_exist)
+    if (b == 1) return fail(MBX_E_UNSUPPORTED, "insert into %s: bitmap indexes are maintained on the GPU path, "
+                            "rebuild them after the insert", name);
+  for (uint8_t b : sc.btree_exist)
+    if (b == 1) return fail(MBX_E_UNSUPPORTED, "insert into %s: B-tree indexes are out of scope", name);
+  const int32_t n = sc.ncols;
+  std::vector<int32_t> heap((size_t)n), rl((size_t)n);
+  for (int32_t i = 0; i < n; ++i) {
+    if (!host_cols[i]) return fail(MBX_E_INVALID, "insert: host_cols[%d] is null", i);
+    heap[(size_t)i] = get_file_entry(db, std::string(name) + "." + std::to_string(i));
+    if (heap[(size_t)i] == kInvalidPage) return fail(MBX_E_INVALID, "%s.%d is missing", name, i);
+    rl[(size_t)i] = record_len(sc.cols[(size_t)i]);
+  }
+  std::vector<uint8_t> rec(kPage);
+  for (int64_t r = 0; r < nrows; ++r) {
+    for (int32_t i = 0; i < n; ++i) {
+      const mbx_col_desc& d = sc.cols[(size_t)i];
+      if (d.attr_type == MBX_ATTR_STRING) {
+        const uint8_t* src = (const uint8_t*)host_cols[i] + (size_t)r * (size_t)d.size;
+        const int32_t len = (int32_t)strnlen((const char*)src, (size_t)d.size);
+        std::fill(rec.begin(), rec.begin() + rl[(size_t)i], 0);
+        put16(rec.data(), len);
+        memcpy(rec.data() + 2, src, (size_t)len);
+      } else {
+        uint32_t v;
+        memcpy(&v, (const uint8_t*)host_cols[i] + (size_t)r * 4, 4);
+        put32(rec.data(), (int32_t)v);
+      }
+      int32_t pid, slot;
+      if ((rc = heap_insert(db, heap[(size_t)i], rec.data(), rl[(size_t)i], &pid, &slot))) return rc;
+    }
+  }
+  return MBX_OK;
+}
+
+namespace {
+
+// positions of a column heapfile: page table + nrows (max position + 1)
+struct ColumnPages {
+  std::vector<DataPage> pages;
+  std::vector<int32_t> page_of;  // page index -> pid
+  int64_t nrows = 0;
+  int64_t records = 0;
+  int32_t rec_len = 0;
+  int32_t recs_per_page = 0;
+  int32_t max_pid = -1;
+};
+
+int column_pages(mbx_db* db, const std::string& file, int32_t rec_len, ColumnPages* cp) {
+  const int32_t first = get_file_entry(db, file);
+  if (first == kInvalidPage) return fail(MBX_E_INVALID, "heapfile %s is missing", file.c_str());
+  int rc = heap_pages(db, first, &cp->pages);
+  if (rc) return rc;
+  cp->rec_len = rec_len;
+  cp->recs_per_page = recs_per_data_page(rec_len);
+  int64_t npi = 0;
+  for (const DataPage& d : cp->pages) npi = std::max(npi, d.index + 1);
+  cp->page_of.assign((size_t)npi, kInvalidPage);
+  for (const DataPage& d : cp->pages) {
+    cp->page_of[(size_t)d.index] = d.pid;
+    cp->max_pid = std::max(cp->max_pid, d.pid);
+    const int32_t cnt = get16(db->page(d.pid) + kSlotCnt);
+    if (cnt < 0 || cnt > cp->recs_per_page)
+      return fail(MBX_E_INVALID, "%s: data page %d holds %d slots (max %d)", file.c_str(), d.pid, cnt,
+                  cp->recs_per_page);
+    if (cnt > 0) cp->nrows = std::max(cp->nrows, d.index * cp->recs_per_page + cnt);
+    cp->records += d.recct;
+  }
+  return MBX_OK;
+}
+
+}  // namespace
+
+extern "C" int mbx_db_columnar_info(mbx_db* db, const char* name, int32_t max_cols, int32_t* ncols,
+                                    mbx_col_desc* cols, char* attr_names, int64_t* nrows, int64_t* live) {
+  NOTNULL(db);
+  NOTNULL(name);
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  if (ncols) *ncols = sc.ncols;
+  for (int32_t i = 0; i < sc.ncols && i < max_cols; ++i) {
+    if (cols) cols[i] = sc.cols[(size_t)i];
+    if (attr_names) {
+      char* cell = attr_names + (size_t)i * (MBX_DB_MAX_ATTR_NAME + 1);
+      memset(cell, 0, MBX_DB_MAX_ATTR_NAME + 1);
+      memcpy(cell, sc.names[(size_t)i].data(), std::min<size_t>(sc.names[(size_t)i].size(), MBX_DB_MAX_ATTR_NAME));
+    }
+  }
+  if (nrows || live) {
+    ColumnPages cp;
+    if ((rc = column_pages(db, std::string(name) + ".0", record_len(sc.cols[0]), &cp))) return rc;
+    if (nrows) *nrows = cp.nrows;
+    if (live) {
+      int64_t del = 0;
+      const int32_t md = get_file_entry(db, std::string(name) + ".md");
+      if (md != kInvalidPage) {
+        std::vector<uint8_t> bytes;
+        if ((rc = bm_read_bytes(db, md, &bytes))) return rc;
+        for (uint8_t b : bytes) del += __builtin_popcount(b);
+      }
+      *live = cp.records - del;
+    }
+  }
+  return MBX_OK;
+}
+
+extern "C" int mbx_db_mark_deleted(mbx_db* db, const char* name, int64_t position) {
+  NOTNULL(db);
+  NOTNULL(name);
+  if (position < 0) return fail(MBX_E_INVALID, "Invalid position");
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  // RIDs of the position in every column (Heapfile.findRID)
+  std::vector<uint8_t> tid((size_t)sc.ncols * 8);
+  for (int32_t i = 0; i < sc.ncols; ++i) {
+    ColumnPages cp;
+    if ((rc = column_pages(db, std::string(name) + "." + std::to_string(i), record_len(sc.cols[(size_t)i]), &cp)))
+      return rc;
+    const int64_t pi = position / cp.recs_per_page;
+    if (pi >= (int64_t)cp.page_of.size() || cp.page_of[(size_t)pi] == kInvalidPage)
+      return fail(MBX_E_INVALID, "Invalid Position %lld", (long long)position);
+    put32(tid.data() + 8 * i, (int32_t)(position - pi * cp.recs_per_page));  // RID.writeToByteArray: slotNo
+    put32(tid.data() + 8 * i + 4, cp.page_of[(size_t)pi]);                  // then pageNo
+  }
+  const int32_t md = get_file_entry(db, std::string(name) + ".md");
+  if (md == kInvalidPage) return fail(MBX_E_INVALID, "%s.md is missing", name);
+  if ((rc = bm_set_bit(db, md, position))) return rc;
+  int32_t dtid;
+  if ((rc = heap_open(db, std::string(name) + ".dtid", true, &dtid))) return rc;
+  int32_t pid, slot;
+  return heap_insert(db, dtid, tid.data(), (int32_t)tid.size(), &pid, &slot);
+}
+
+extern "C" int mbx_db_bitmap_write(mbx_db* db, const char* filename, const uint64_t* words, int64_t nwords) {
+  NOTNULL(db);
+  NOTNULL(filename);
+  if (nwords < 0 || (nwords > 0 && !words)) return fail(MBX_E_INVALID, "bitmap_write: %lld words", (long long)nwords);
+  if (get_file_entry(db, filename) != kInvalidPage)
+    return fail(MBX_E_INVALID, "The BitMapFile %s is already created.", filename);
+  const std::vector<uint8_t> bytes = bitset_bytes(words, nwords);
+  if (bytes.empty()) return fail(MBX_E_INVALID, "BM.insertBitSet: %s would be an empty BitSet", filename);
+  int32_t head;
+  int rc = bm_create_header(db, filename, &head);
+  if (rc) return rc;
+  return bm_insert_bitset(db, head, bytes);
+}
+
+extern "C" int mbx_db_bitmap_read(mbx_db* db, const char* filename, uint64_t* words, int64_t nwords_cap,
+                                  int64_t* nwords_out) {
+  NOTNULL(db);
+  NOTNULL(filename);
+  const int32_t head = get_file_entry(db, filename);
+  if (head == kInvalidPage) return fail(MBX_E_INVALID, "The file %s does not exist.", filename);
+  std::vector<uint8_t> bytes;
+  int rc = bm_read_bytes(db, head, &bytes);
+  if (rc) return rc;
+  const int64_t nw = ((int64_t)bytes.size() + 7) / 8;
+  if (nwords_out) *nwords_out = nw;
+  if (words && nwords_cap > 0) {
+    const int64_t n = std::min(nw, nwords_cap);
+    memset(words, 0, (size_t)nwords_cap * 8);
+    memcpy(words, bytes.data(), (size_t)std::min<int64_t>((int64_t)bytes.size(), n * 8));
+  }
+  return MBX_OK;
+}
+
+// ------------------------------------------------------------ GPU staging
+
+extern "C" int mbx_db_stage(mbx_ctx* c, mbx_db* db, const char* name, mbx_table** out) {
+  NOTNULL(c);
+  NOTNULL(db);
+  NOTNULL(name);
+  NOTNULL(out);
+  *out = nullptr;
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  const int32_t n = sc.ncols;
+  std::vector<ColumnPages> cps((size_t)n);
+  int64_t nrows = 0;
+  int32_t max_pid = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if ((rc = column_pages(db, std::string(name) + "." + std::to_string(i), record_len(sc.cols[(size_t)i]),
+                           &cps[(size_t)i])))
+      return rc;
+    nrows = std::max(nrows, cps[(size_t)i].nrows);
+    max_pid = std::max(max_pid, cps[(size_t)i].max_pid);
+  }
+  std::vector<uint8_t> md_bytes;
+  const int32_t md = get_file_entry(db, std::string(name) + ".md");
+  if (md != kInvalidPage && (rc = bm_read_bytes(db, md, &md_bytes))) return rc;
+  const int64_t nwords = words_for(nrows);
+  const int64_t md_words = std::min<int64_t>(((int64_t)md_bytes.size() + 7) / 8, nwords);
+
+  mbx_table* t = nullptr;
+  if ((rc = table_alloc(c, sc.cols.data(), n, nrows, 0, true, &t))) return rc;
+  // device scratch: page image, page tables, present sets, .md words, flags
+  const int64_t image_pages = (int64_t)max_pid + 1;
+  uint8_t* dimg = nullptr;
+  int32_t* dpage_of = nullptr;
+  uint64_t* dpresent = nullptr;
+  uint64_t* dmd = nullptr;
+  int32_t* dflags = nullptr;
+  int64_t npi_total = 0;
+  for (const ColumnPages& cp : cps) npi_total += (int64_t)cp.page_of.size();
+  const int64_t pw = nwords > 0 ? nwords : 1;
+  void* pinned = nullptr;
+  const size_t chunk = (size_t)32 << 20;
+  hipStream_t s = c->stream;
+  hipError_t e = hipMalloc(&dimg, (size_t)image_pages * kPage);
+  if (e == hipSuccess) e = hipMalloc(&dpage_of, sizeof(int32_t) * (size_t)(npi_total > 0 ? npi_total : 1));
+  if (e == hipSuccess) e = hipMalloc(&dpresent, sizeof(uint64_t) * (size_t)pw * (size_t)n);
+  if (e == hipSuccess) e = hipMalloc(&dmd, sizeof(uint64_t) * (size_t)(md_words > 0 ? md_words : 1));
+  if (e == hipSuccess) e = hipMalloc(&dflags, sizeof(int32_t) * 2);
+  if (e == hipSuccess) e = hipHostMalloc(&pinned, 2 * chunk, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMemsetAsync(dpresent, 0, sizeof(uint64_t) * (size_t)pw * (size_t)n, s);
+  if (e == hipSuccess) e = hipMemsetAsync(dflags, 0, sizeof(int32_t) * 2, s);
+  for (int32_t i = 0; i < n && e == hipSuccess; ++i) {
+    const TCol& tc = t->cols[(size_t)i];
+    e = hipMemsetAsync(tc.dev, 0, (size_t)(nrows > 0 ? nrows : 1) * (size_t)tc.stride_w * 4, s);
+  }
+  // the used part of the DB file, as it lies on disk, through two pinned
+  // chunks (the copy of one overlaps the memcpy into the other)
+  {
+    const size_t total = (size_t)image_pages * kPage;
+    hipEvent_t done[2] = {nullptr, nullptr};
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&done[0], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&done[1], hipEventDisableTiming);
+    int k = 0;
+    for (size_t off = 0; off < total && e == hipSuccess; off += chunk, k ^= 1) {
+      const size_t len = std::min(chunk, total - off);
+      e = hipEventSynchronize(done[k]);
+      uint8_t* buf = (uint8_t*)pinned + (size_t)k * chunk;
+      if (e == hipSuccess) {
+        memcpy(buf, db->base + off, len);
+        e = hipMemcpyAsync(dimg + off, buf, len, hipMemcpyHostToDevice, s);
+      }
+      if (e == hipSuccess) e = hipEventRecord(done[k], s);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (done[0]) hipEventDestroy(done[0]);
+    if (done[1]) hipEventDestroy(done[1]);
+  }
+  std::vector<int32_t> page_of;
+  page_of.reserve((size_t)npi_total);
+  for (const ColumnPages& cp : cps) page_of.insert(page_of.end(), cp.page_of.begin(), cp.page_of.end());
+  if (e == hipSuccess && npi_total > 0)
+    e = hipMemcpy(dpage_of, page_of.data(), sizeof(int32_t) * page_of.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && md_words > 0) {
+    std::vector<uint64_t> mdw((size_t)md_words, 0);
+    memcpy(mdw.data(), md_bytes.data(), std::min<size_t>(md_bytes.size(), (size_t)md_words * 8));
+    e = hipMemcpy(dmd, mdw.data(), sizeof(uint64_t) * (size_t)md_words, hipMemcpyHostToDevice);
+  }
+  int64_t pofs = 0;
+  for (int32_t i = 0; i < n && e == hipSuccess; ++i) {
+    const ColumnPages& cp = cps[(size_t)i];
+    const TCol& tc = t->cols[(size_t)i];
+    PageDecodeArgs A;
+    A.image = dimg;
+    A.image_pages = image_pages;
+    A.page_of = dpage_of + pofs;
+    A.npages = (int64_t)cp.page_of.size();
+    A.rec_len = cp.rec_len;
+    A.recs_per_page = cp.recs_per_page;
+    A.kind = tc.attr_type == MBX_ATTR_STRING ? kStr : (tc.attr_type == MBX_ATTR_REAL ? kReal : kInt);
+    A.size = tc.size;
+    A.stride = tc.stride_w * 4;
+    A.pad_ = 0;
+    A.out = (uint8_t*)tc.dev;
+    A.present = dpresent + (size_t)pw * (size_t)i;
+    A.nrows = nrows;
+    A.err = dflags;
+    e = launch_page_decode(A, s);
+    pofs += A.npages;
+  }
+  if (e == hipSuccess)
+    e = launch_present_merge(dpresent, dpresent + pw, n - 1, pw, dmd, md_words, nrows, t->deleted, dflags + 1, s);
+  int32_t flags[2] = {0, 0};
+  if (e == hipSuccess) e = hipMemcpyAsync(flags, dflags, sizeof(flags), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  hipFree(dimg);
+  hipFree(dpage_of);
+  hipFree(dpresent);
+  hipFree(dmd);
+  hipFree(dflags);
+  if (pinned) hipHostFree(pinned);
+  if (e != hipSuccess) {
+    mbx_table_free(t);
+    return fail(MBX_E_DEVICE, "db_stage %s: %s", name, hipGetErrorString(e));
+  }
+  if (flags[0]) {
+    mbx_table_free(t);
+    return fail(MBX_E_INVALID, "db_stage %s: malformed data pages (flags 0x%x)", name, flags[0]);
+  }
+  if (flags[1] & 1) {
+    mbx_table_free(t);
+    return fail(MBX_E_INVALID, "Invalid position calculations: the column heapfiles of %s disagree", name);
+  }
+  if (!(flags[1] & 2) && t->deleted) {
+    // every position holds a live record: scan without a deleted mask
+    hipFree(t->deleted);
+    t->deleted = nullptr;
+    t->owns_deleted = false;
+  }
+  *out = t;
+  return MBX_OK;
+}

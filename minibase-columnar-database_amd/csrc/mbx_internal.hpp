@@ -146,6 +146,32 @@ struct BitmapCnf {
   int32_t nconj;
 };
 
+// ---- Minibase DB pages (mbx_pages.hip, include/mbx_db.h)
+constexpr int kDbPage = 1024;      // GlobalConst.MINIBASE_PAGESIZE
+constexpr int kDbSlotBase = 20;    // HFPage.DPFIXED: slot directory start
+
+struct PageDecodeArgs {
+  const uint8_t* image;      // device copy of DB pages 0..image_pages-1
+  int64_t image_pages;
+  const int32_t* page_of;    // page index -> pid (-1: none), npages entries
+  int64_t npages;
+  int32_t rec_len;           // record bytes (4, or n + 2 for char(n))
+  int32_t recs_per_page;     // (1024 - 20) / (4 + rec_len)
+  int32_t kind;              // ColKind
+  int32_t size;              // char(n): n
+  int32_t stride;            // output bytes per row
+  int32_t pad_;
+  uint8_t* out;              // column image, nrows rows
+  uint64_t* present;         // BitSet of positions that hold a record
+  int64_t nrows;
+  int32_t* err;              // bit flags of malformed pages
+};
+
+hipError_t launch_page_decode(const PageDecodeArgs& A, hipStream_t s);
+hipError_t launch_present_merge(const uint64_t* present0, const uint64_t* other, int32_t nother, int64_t nwords_each,
+                                const uint64_t* md, int64_t md_words, int64_t nrows, uint64_t* del, int32_t* flags,
+                                hipStream_t s);
+
 int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block);
 int64_t choose_tiles_per_block(int64_t nrows);
 

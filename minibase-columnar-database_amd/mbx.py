@@ -86,6 +86,10 @@ EXPORTS = [
     "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_bitmap_index_build",
     "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
     "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close",
+    # include/mbx_db.h
+    "mbx_db_create", "mbx_db_open", "mbx_db_close", "mbx_db_info", "mbx_db_file_entry", "mbx_db_columnar_create",
+    "mbx_db_columnar_insert", "mbx_db_columnar_info", "mbx_db_mark_deleted", "mbx_db_bitmap_write",
+    "mbx_db_bitmap_read", "mbx_db_stage",
 ]
 
 _lib = None
@@ -138,6 +142,18 @@ def lib():
         "mbx_cursor_next": ([V, I64, V, P(V), P(I64)], ctypes.c_int),
         "mbx_cursor_restart": ([V], ctypes.c_int),
         "mbx_cursor_close": ([V], ctypes.c_int),
+        "mbx_db_create": ([ctypes.c_char_p, I32, P(V)], ctypes.c_int),
+        "mbx_db_open": ([ctypes.c_char_p, P(V)], ctypes.c_int),
+        "mbx_db_close": ([V], ctypes.c_int),
+        "mbx_db_info": ([V, P(I32), P(I32)], ctypes.c_int),
+        "mbx_db_file_entry": ([V, ctypes.c_char_p, P(I32)], ctypes.c_int),
+        "mbx_db_columnar_create": ([V, ctypes.c_char_p, I32, P(ColDesc), P(ctypes.c_char_p)], ctypes.c_int),
+        "mbx_db_columnar_insert": ([V, ctypes.c_char_p, I64, P(V)], ctypes.c_int),
+        "mbx_db_columnar_info": ([V, ctypes.c_char_p, I32, P(I32), P(ColDesc), V, P(I64), P(I64)], ctypes.c_int),
+        "mbx_db_mark_deleted": ([V, ctypes.c_char_p, I64], ctypes.c_int),
+        "mbx_db_bitmap_write": ([V, ctypes.c_char_p, V, I64], ctypes.c_int),
+        "mbx_db_bitmap_read": ([V, ctypes.c_char_p, V, I64, P(I64)], ctypes.c_int),
+        "mbx_db_stage": ([V, V, ctypes.c_char_p, P(V)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -285,6 +301,14 @@ class Context:
         _chk(lib().mbx_table_wrap(self.h, descs, len(col_descs), nrows, ptrs, dev_deleted, row_offset,
                                   ctypes.byref(h)))
         return Table(self, h, nrows, list(col_descs), row_offset, keep=[descs, ptrs])
+
+    def stage_db(self, db, name):
+        """mbx_db_stage: a Columnarfile of a Minibase DB file -> HBM table
+        (records decoded on the GPU, reference positions kept)."""
+        info = db.columnar_info(name)
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_db_stage(self.h, db.h, name.encode(), ctypes.byref(h)))
+        return Table(self, h, info["nrows"], [(t, s) for t, s in info["cols"]], 0)
 
     # -- plans / scans ---------------------------------------------------
     def compile(self, table, cnf):
@@ -486,3 +510,92 @@ class Cursor(_Handle):
 
     def restart(self):
         _chk(lib().mbx_cursor_restart(self.h))
+
+
+class Db:
+    """A Minibase DB file (include/mbx_db.h); host-side page I/O only."""
+
+    def __init__(self, path, num_pages=None):
+        h = ctypes.c_void_p()
+        if num_pages is None:
+            _chk(lib().mbx_db_open(os.fsencode(path), ctypes.byref(h)))
+        else:
+            _chk(lib().mbx_db_create(os.fsencode(path), num_pages, ctypes.byref(h)))
+        self.h, self.path = h, path
+
+    def close(self):
+        if getattr(self, "h", None):
+            _chk(lib().mbx_db_close(self.h))
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self):
+        n, a = ctypes.c_int32(), ctypes.c_int32()
+        _chk(lib().mbx_db_info(self.h, ctypes.byref(n), ctypes.byref(a)))
+        return n.value, a.value
+
+    def file_entry(self, name):
+        p = ctypes.c_int32()
+        _chk(lib().mbx_db_file_entry(self.h, name.encode(), ctypes.byref(p)))
+        return p.value
+
+    def columnar_create(self, name, cols, attr_names):
+        """cols: [(attr_type, size)], size = n for char(n), 4 otherwise."""
+        descs = (ColDesc * len(cols))()
+        for j, (t, sz) in enumerate(cols):
+            descs[j].attr_type, descs[j].size = t, sz
+        names = (ctypes.c_char_p * len(cols))(*[n.encode() for n in attr_names])
+        _chk(lib().mbx_db_columnar_create(self.h, name.encode(), len(cols), descs, names))
+
+    def columnar_insert(self, name, columns):
+        """columns: [(attr_type, size, ndarray)] as for Context.stage."""
+        arrs = []
+        nrows = None
+        for t, size, a in columns:
+            if t == INTEGER:
+                a = np.ascontiguousarray(a, dtype=np.int32)
+            elif t == REAL:
+                a = np.ascontiguousarray(a, dtype=np.float32)
+            else:
+                a = np.ascontiguousarray(a, dtype=np.uint8).reshape(-1, size)
+            arrs.append(a)
+            nrows = a.shape[0] if nrows is None else nrows
+        ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        _chk(lib().mbx_db_columnar_insert(self.h, name.encode(), nrows, ptrs))
+
+    def columnar_info(self, name, max_cols=256):
+        n = ctypes.c_int32()
+        descs = (ColDesc * max_cols)()
+        names = ctypes.create_string_buffer(16 * max_cols)
+        nrows, live = ctypes.c_int64(), ctypes.c_int64()
+        _chk(lib().mbx_db_columnar_info(self.h, name.encode(), max_cols, ctypes.byref(n), descs, names,
+                                        ctypes.byref(nrows), ctypes.byref(live)))
+        k = min(n.value, max_cols)
+        return {"ncols": n.value, "cols": [(descs[j].attr_type, descs[j].size) for j in range(k)],
+                "names": [names.raw[16 * j:16 * j + 16].split(b"\0")[0].decode() for j in range(k)],
+                "nrows": nrows.value, "live": live.value}
+
+    def mark_deleted(self, name, position):
+        _chk(lib().mbx_db_mark_deleted(self.h, name.encode(), position))
+
+    def bitmap_write(self, filename, words):
+        w = np.ascontiguousarray(words, dtype=np.uint64)
+        _chk(lib().mbx_db_bitmap_write(self.h, filename.encode(), w.ctypes.data if len(w) else None, len(w)))
+
+    def bitmap_read(self, filename):
+        n = ctypes.c_int64()
+        _chk(lib().mbx_db_bitmap_read(self.h, filename.encode(), None, 0, ctypes.byref(n)))
+        w = np.zeros(max(1, n.value), dtype=np.uint64)
+        _chk(lib().mbx_db_bitmap_read(self.h, filename.encode(), w.ctypes.data, len(w), ctypes.byref(n)))
+        return w[:n.value]

@@ -13,7 +13,11 @@ engine run over minidata.txt) as TEXT and writes tests/golden/phase3_golden.json
     the whole CNF);
   * "indexes_query": the rows (A, B, C, D) and the count printed by
     `indexes_query` (MultiIndexQuery -> ColumnarIndexScan.get_next), in the
-    engine's position order.
+    engine's position order;
+  * "db_pages": the DB pages `batchinsert minidata.txt db cf 4` wrote and the
+    pages the first `index db cf <col> ...` of each column read (PCounter sets
+    the engine prints) -- they pin the page numbering of the Minibase DB
+    writer (include/mbx_db.h) and which data pages hold each column.
 
 All queries run over minidata.txt (500 rows, A:char(25) B:char(25) C:int
 D:int), committed as tests/golden/minidata.tsv (a byte copy).  Nothing under
@@ -52,6 +56,7 @@ def split_cnf(s):
 def main():
     lines = open(REF, encoding="utf-8", errors="replace").read().split("\n")
     bitsets, counts, iq = {}, {}, []
+    db_pages = {"column_scan_reads": {}}
     i = 0
     while i < len(lines):
         ln = lines[i]
@@ -64,7 +69,20 @@ def main():
         while j < len(lines) and not lines[j].startswith("> "):
             j += 1
         body = lines[i + 1:j]
-        if cmd == "bmj" and len(toks) >= 6 and toks[1] == "db":
+        if cmd in ("batchinsert", "index"):
+            # PCounter page sets (R/diskmgr/PCounter.java) printed after the command
+            sets = {}
+            for k, b in enumerate(body):
+                m = re.match(r"(Read|Wrote) Pages: \{(.*)\}", b)
+                if m:
+                    sets[m.group(1)] = ([int(x.split("=")[0]) for x in m.group(2).split(",") if "=" in x], i + k + 2)
+            if cmd == "batchinsert" and "Wrote" in sets and "batchinsert_wrote" not in db_pages:
+                db_pages["batchinsert_wrote"], db_pages["batchinsert_line"] = sets["Wrote"]
+                db_pages["batchinsert_cmd"] = ln[2:].strip()
+            elif cmd == "index" and len(toks) >= 5 and "Read" in sets:
+                db_pages["column_scan_reads"].setdefault(toks[3], {"pages": sets["Read"][0], "line": sets["Read"][1],
+                                                                   "cmd": ln[2:].strip()})
+        elif cmd == "bmj" and len(toks) >= 6 and toks[1] == "db":
             outer, inner = split_cnf(toks[4]), split_cnf(toks[5])
             for k, b in enumerate(body):
                 for tag, cnf, raw in (("OuterConstraint", outer, toks[4]), ("InnerConstraint", inner, toks[5])):
@@ -107,6 +125,7 @@ def main():
         "bitsets": list(bitsets.values()),
         "full_constraint_counts": list(counts.values()),
         "indexes_query": iq,
+        "db_pages": db_pages,
     }
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)

@@ -8,19 +8,24 @@ import pytest
 import helpers
 import mbx_pkg
 
-HEADER = os.path.join(helpers.ROOT, "include", "mbx.h")
+HEADERS = [os.path.join(helpers.ROOT, "include", h) for h in sorted(os.listdir(os.path.join(helpers.ROOT, "include")))
+           if h.endswith(".h")]
 
 
 def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(mbx_[a-z_0-9]+)\s*\(", src, flags=re.M)))
+    out = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        out |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s*(mbx_[a-z_0-9]+)\s*\(", src, flags=re.M))
+    return sorted(out)
 
 
 def test_header_declares_the_boundary():
     fns = declared_functions()
     for must in ["mbx_init", "mbx_table_stage", "mbx_plan_compile", "mbx_scan_count", "mbx_scan_bitmap",
-                 "mbx_bitmap_cnf", "mbx_materialize", "mbx_cursor_next", "mbx_scan_aggregate"]:
+                 "mbx_bitmap_cnf", "mbx_materialize", "mbx_cursor_next", "mbx_scan_aggregate", "mbx_db_open",
+                 "mbx_db_stage", "mbx_db_columnar_insert"]:
         assert must in fns
 
 

@@ -1,0 +1,270 @@
+"""Minibase DB files (include/mbx_db.h).
+
+CPU tests: the C++ writer against the page numbers the reference engine
+printed for `batchinsert minidata.txt db cf 4` (tests/golden/phase3_golden.json
+"db_pages", R/phase3_output:19-22,3172,3228,3246,3264), and against the CPU
+restatement of the reader (oracle/minibase_pages.py) for every format detail.
+GPU tests: mbx_db_stage (pages -> HBM -> k_page_decode) against the same
+restatement, and queries over the staged table against the scan oracle.
+"""
+import numpy as np
+import pytest
+
+import helpers
+import mbx_pkg
+import minibase_pages as mp
+import oracle
+
+GOLD = helpers.load_golden()
+
+
+@pytest.fixture(scope="module")
+def m():
+    return mbx_pkg.load()
+
+
+def minidata_db(m, path, num_pages=1024 * 1024):
+    """BatchInsert minidata.txt into a fresh DB (SystemDefs(db, 1024*1024, ...),
+    R/input/BatchInsert.java:52-57)."""
+    rows = helpers.load_minidata()
+    cols = helpers.minidata_columns(rows)
+    db = m.mbx.Db(path, num_pages)
+    db.columnar_create("cf", [(t, s) for t, s, _ in cols], ["A", "B", "C", "D"])
+    db.columnar_insert("cf", cols)
+    return db, cols
+
+
+def test_batchinsert_page_numbers_match_reference(m, tmp_path):
+    db, _ = minidata_db(m, str(tmp_path / "db"))
+    db.close()
+    img = mp.DbImage(str(tmp_path / "db"))
+    gp = GOLD["db_pages"]
+    # space map: pages 0..128 (first page + 128 map pages of a 1M-page DB)
+    # are reserved at creation; the engine wrote 0, 1 and then 129..176
+    written = sorted(set(gp["batchinsert_wrote"]))
+    assert mp.allocated_pages(img) == list(range(0, 129)) + [p for p in written if p >= 129]
+    fe = mp.file_entries(img)
+    assert fe == {"cf.hdr": 129, "cf.0": 131, "cf.1": 132, "cf.2": 133, "cf.3": 134, "cf.md": 135, "cf.dtid": 136}
+    # the data pages of each column = the pages the engine read when it
+    # scanned that column (minus the hdr, .md and directory pages)
+    for i, colname in enumerate("ABCD"):
+        reads = gp["column_scan_reads"][colname]["pages"]
+        assert 131 + i in reads
+        want = sorted(p for p in reads if 137 <= p <= 176)
+        got = sorted(pid for _, pid, _ in mp.heap_data_pages(img, fe[f"cf.{i}"]))
+        assert got == want, colname
+
+
+def test_minidata_round_trip_through_reader_restatement(m, tmp_path):
+    db, cols = minidata_db(m, str(tmp_path / "db"), num_pages=4096)
+    info = db.columnar_info("cf")
+    assert info["ncols"] == 4 and info["names"] == ["A", "B", "C", "D"]
+    assert info["cols"] == [(oracle.STRING, 25), (oracle.STRING, 25), (oracle.INTEGER, 4), (oracle.INTEGER, 4)]
+    assert info["nrows"] == 500 and info["live"] == 500
+    db.close()
+    img = mp.DbImage(str(tmp_path / "db"))
+    sc = mp.columnar_schema(img, "cf")
+    assert sc["names"] == ["A", "B", "C", "D"] and sc["btree"] == [0] * 4 and sc["bitmap"] == [0] * 4
+    n, got, dele = mp.columnar_table(img, "cf")
+    assert n == 500 and not dele.any()
+    for (t, s, a), (t2, s2, b) in zip(cols, got):
+        assert (t, s) == (t2, s2) and np.array_equal(a, b)
+
+
+def test_page_layouts(m, tmp_path):
+    """HFPage fill: 125 int32 / 32 char(25) / 45 char(16) records per data
+    page, 83 DataPageInfo per directory page, records packed from the end."""
+    n = 125 * 83 + 7   # spills into a second directory page for the int column
+    rng = np.random.Generator(np.random.PCG64(3))
+    words = ["alpha", "b", "", "é€", "x" * 16]
+    cols = [(oracle.INTEGER, 4, rng.integers(-2**31, 2**31 - 1, n, dtype=np.int32)),
+            (oracle.STRING, 16, helpers.encode_strings([words[i] for i in rng.integers(0, 5, n)], 16)),
+            (oracle.REAL, 4, rng.random(n, dtype=np.float32))]
+    path = str(tmp_path / "db")
+    with m.mbx.Db(path, 8192) as db:
+        db.columnar_create("t", [(t, s) for t, s, _ in cols], ["i", "s", "f"])
+        db.columnar_insert("t", cols)
+    img = mp.DbImage(path)
+    fe = mp.file_entries(img)
+    for i, rpp in enumerate([125, 45, 125]):
+        pages = mp.heap_data_pages(img, fe[f"t.{i}"])
+        assert [pi for pi, _, _ in pages] == list(range(len(pages)))
+        assert all(rc == rpp for _, _, rc in pages[:-1])
+        pg = img.page(pages[0][1])
+        assert mp.be16(pg, 0) == rpp and mp.be16(pg, 2) == 1024 - rpp * (4 if i != 1 else 18)
+    nd = sum(1 for _ in iter_dir_pages(img, fe["t.0"]))
+    assert nd == 2
+    nrows, got, dele = mp.columnar_table(img, "t")
+    assert nrows == n and not dele.any()
+    for (t, s, a), (_, _, b) in zip(cols, got):
+        assert np.array_equal(a, b)
+
+
+def iter_dir_pages(img, first):
+    d = first
+    while d != mp.INVALID:
+        yield d
+        d = mp.be32(img.page(d), 12)
+
+
+def test_append_and_mark_deleted(m, tmp_path):
+    path = str(tmp_path / "db")
+    rng = np.random.Generator(np.random.PCG64(5))
+    a = [(oracle.INTEGER, 4, rng.integers(0, 50, 1000, dtype=np.int32))]
+    b = [(oracle.INTEGER, 4, rng.integers(0, 50, 333, dtype=np.int32))]
+    with m.mbx.Db(path, 4096) as db:
+        db.columnar_create("cf", [(oracle.INTEGER, 4)], ["x"])
+        db.columnar_insert("cf", a)
+        db.columnar_insert("cf", b)      # a second batchinsert appends
+        for p in (0, 7, 999, 1000, 1332, 64):
+            db.mark_deleted("cf", p)
+        info = db.columnar_info("cf")
+        assert info["nrows"] == 1333 and info["live"] == 1333 - 6
+        with pytest.raises(m.MbxError):
+            db.mark_deleted("cf", 5000)    # findRID: Invalid Position
+    img = mp.DbImage(path)
+    n, (col,), dele = mp.columnar_table(img, "cf")
+    assert n == 1333 and np.array_equal(col[2], np.concatenate([a[0][2], b[0][2]]))
+    assert sorted(oracle.words_to_positions(dele)) == [0, 7, 64, 999, 1000, 1332]
+    # cf.dtid holds one TID record (numColumns RIDs: slotNo, pageNo) per delete
+    recs = [r for _, _, r in mp.heap_records(img, mp.file_entries(img)["cf.dtid"])]
+    assert len(recs) == 6 and all(len(r) == 8 for r in recs)
+    data = {pi: pid for pi, pid, _ in mp.heap_data_pages(img, mp.file_entries(img)["cf.0"])}
+    assert mp.be32(recs[2], 0) == 999 % 125 and mp.be32(recs[2], 4) == data[999 // 125]
+
+
+def test_bitmap_files(m, tmp_path):
+    path = str(tmp_path / "db")
+    rng = np.random.Generator(np.random.PCG64(8))
+    big = rng.integers(0, 2**63, 300, dtype=np.uint64)           # 19200 bits -> 3 chunk pages
+    small = np.zeros(2, dtype=np.uint64)
+    small[1] = np.uint64(1) << np.uint64(40)
+    with m.mbx.Db(path, 4096) as db:
+        db.bitmap_write("cf.bm.0.7", big)
+        db.bitmap_write("cf.bm.0.8", small)
+        with pytest.raises(m.MbxError):
+            db.bitmap_write("cf.bm.0.9", np.zeros(4, dtype=np.uint64))   # empty BitSet
+        with pytest.raises(m.MbxError):
+            db.bitmap_write("cf.bm.0.7", big)                           # exists
+        assert np.array_equal(db.bitmap_read("cf.bm.0.7")[:300], big)
+        assert np.array_equal(db.bitmap_read("cf.bm.0.8")[:2], small)
+    img = mp.DbImage(path)
+    w = mp.bitmap_words(img, "cf.bm.0.7")
+    assert np.array_equal(w[:300], big) and not w[300:].any()
+    head = img.page(mp.file_entries(img)["cf.bm.0.7"])
+    assert mp.be16(head, 6) == 13                     # NodeType.BMHEAD
+    assert mp.hf_slots(head) == [(0, 1000, 24)]       # one 1000-byte record
+    assert np.array_equal(mp.bitmap_words(img, "cf.bm.0.8")[:2], small)
+
+
+def test_many_files_spill_into_directory_pages(m, tmp_path):
+    """More than 17 file entries: DB.add_file_entry allocates DBDirectoryPages
+    (18 entries each) -- as page 205 in the reference run of `index db cf A bitmap`."""
+    path = str(tmp_path / "db")
+    with m.mbx.Db(path, 4096) as db:
+        for k in range(40):
+            w = np.zeros(1, dtype=np.uint64)
+            w[0] = np.uint64(1 + k)
+            db.bitmap_write(f"f{k}", w)
+        for k in range(40):
+            assert db.file_entry(f"f{k}") >= 0
+        assert db.file_entry("nope") == -1
+    img = mp.DbImage(path)
+    fe = mp.file_entries(img)
+    assert len(fe) == 40 and mp.be32(img.page(0), 4) == 17
+    dir1 = mp.be32(img.page(0), 0)
+    assert dir1 > 0 and mp.be32(img.page(dir1), 4) == 18
+    for k in range(40):
+        assert int(mp.bitmap_words(img, f"f{k}")[0]) == 1 + k
+
+
+def test_errors(m, tmp_path):
+    path = str(tmp_path / "db")
+    with m.mbx.Db(path, 200) as db:
+        db.columnar_create("cf", [(oracle.INTEGER, 4)], ["x"])
+        with pytest.raises(m.MbxError):
+            db.columnar_create("cf", [(oracle.INTEGER, 4)], ["x"])         # exists
+        with pytest.raises(m.MbxError):
+            db.columnar_create("a_name_too_long_for_minibase", [(oracle.INTEGER, 4)], ["x"])
+        with pytest.raises(m.MbxError):
+            db.columnar_info("missing")
+        with pytest.raises(m.MbxError) as e:                                # OutOfSpaceException
+            db.columnar_insert("cf", [(oracle.INTEGER, 4, np.zeros(200 * 125, dtype=np.int32))])
+        assert e.value.code == m.mbx.E_NOMEM
+    with pytest.raises(m.MbxError):
+        m.mbx.Db(str(tmp_path / "absent"))
+
+
+# ------------------------------------------------------------------- GPU
+
+@pytest.fixture(scope="module")
+def ctx(m):
+    c = m.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.gpu
+def test_stage_minidata_goldens(m, ctx, tmp_path):
+    """Golden BitSets of the reference transcript over a table staged from a
+    Minibase DB file by the GPU page decoder."""
+    db, cols = minidata_db(m, str(tmp_path / "db"), num_pages=4096)
+    t = ctx.stage_db(db, "cf")
+    for g in GOLD["bitsets"]:
+        bm = ctx.scan_bitmap(ctx.compile(t, helpers.golden_cnf(g["cnf"])))
+        assert list(oracle.words_to_positions(bm.download())) == g["positions"]
+    ids, outs = ctx.materialize(t, ctx.scan_bitmap(ctx.compile(t, None)), [0, 1, 2, 3])
+    assert np.array_equal(ids, np.arange(500))
+    for (tt, s, a), o in zip(cols, outs):
+        assert np.array_equal(a, o)
+    db.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 124, 125, 126, 125 * 83, 125 * 83 + 1, 200_003])
+def test_stage_matches_reader_restatement(m, ctx, tmp_path, n):
+    path = str(tmp_path / "db")
+    rng = np.random.Generator(np.random.PCG64(n))
+    words = ["", "a", "M", "Mz", "South_Dakota", "é€", "a\u0000b", "zzzzzzzzzzzzzzzz"]
+    cols = [(oracle.INTEGER, 4, rng.integers(-1000, 1000, n, dtype=np.int32)),
+            (oracle.STRING, 16, helpers.encode_strings([words[i] for i in rng.integers(0, len(words), n)], 16)),
+            (oracle.REAL, 4, rng.random(n, dtype=np.float32)),
+            (oracle.STRING, 25, helpers.encode_strings([words[i] for i in rng.integers(0, len(words), n)], 25))]
+    with m.mbx.Db(path, 1 << 16) as db:
+        db.columnar_create("cf", [(t, s) for t, s, _ in cols], ["i", "s", "f", "w"])
+        db.columnar_insert("cf", cols)
+        for p in range(0, n, 97):
+            db.mark_deleted("cf", p)
+        t = ctx.stage_db(db, "cf")
+    nrows, ocols, dele = mp.columnar_table(mp.DbImage(path), "cf")
+    assert nrows == n
+    ot = oracle.Table(ocols, dele)
+    all_rows = ctx.scan_bitmap(ctx.compile(t, None))
+    assert np.array_equal(all_rows.download(), oracle.filescan(ot, None)[1])
+    ids, outs = ctx.materialize(t, all_rows, [0, 1, 2, 3])
+    live = np.array(oracle.words_to_positions(oracle.filescan(ot, None)[1]), dtype=np.int64)
+    assert np.array_equal(ids, live)
+    for (tt, s, a), o in zip(cols, outs):
+        assert np.array_equal(a[live], o)
+    for cnf in ([[(oracle.LT, ("sym", 1), ("int", 0))], [(oracle.GE, ("sym", 2), ("str", "M"))]],
+                [[(oracle.EQ, ("sym", 4), ("str", "a\u0000b")), (oracle.GT, ("sym", 3), ("real", 0.5))]]):
+        n_o, w_o, _ = oracle.filescan(ot, cnf)
+        bm = ctx.scan_bitmap(ctx.compile(t, cnf))
+        assert bm.count == n_o and np.array_equal(bm.download(), w_o)
+
+
+@pytest.mark.gpu
+def test_stage_rejects_malformed_pages(m, ctx, tmp_path):
+    path = str(tmp_path / "db")
+    with m.mbx.Db(path, 1024) as db:
+        db.columnar_create("cf", [(oracle.INTEGER, 4)], ["x"])
+        db.columnar_insert("cf", [(oracle.INTEGER, 4, np.arange(300, dtype=np.int32))])
+    img = mp.DbImage(path)
+    pid = mp.heap_data_pages(img, mp.file_entries(img)["cf.0"])[0][1]
+    with open(path, "r+b") as f:        # slot 3 claims a 5-byte record
+        f.seek(pid * 1024 + 20 + 4 * 3)
+        f.write(b"\x00\x05")
+    with m.mbx.Db(path) as db:
+        with pytest.raises(m.MbxError) as e:
+            ctx.stage_db(db, "cf")
+        assert "malformed" in str(e.value)
