@@ -64,6 +64,13 @@ int mbx_db_close(mbx_db* db);
 /* DB.db_num_pages and the number of pages set in the space map. */
 int mbx_db_info(const mbx_db* db, int32_t* num_pages, int32_t* allocated_pages);
 
+/* DB.allocate_page(start, run_size) (R/diskmgr/DB.java:212-290): the first
+ * run of free pages (first fit over the space map), marked in use; and
+ * DB.add_file_entry (DB.java:420-500).  For files this library does not model
+ * (B+-tree index files) so page numbering stays the reference's. */
+int mbx_db_allocate_pages(mbx_db* db, int32_t run_size, int32_t* start);
+int mbx_db_add_file_entry(mbx_db* db, const char* name, int32_t start);
+
 /* DB.get_file_entry (R/diskmgr/DB.java:520-590): *first_page = the file's
  * first page, or -1 when no entry has that name (not an error). */
 int mbx_db_file_entry(mbx_db* db, const char* name, int32_t* first_page);
@@ -100,6 +107,30 @@ int mbx_db_mark_deleted(mbx_db* db, const char* name, int64_t position);
  * words of the stored image (ceil(bytes/8)); words[] gets min(cap, that). */
 int mbx_db_bitmap_write(mbx_db* db, const char* filename, const uint64_t* words, int64_t nwords);
 int mbx_db_bitmap_read(mbx_db* db, const char* filename, uint64_t* words, int64_t nwords_cap, int64_t* nwords_out);
+
+/* Columnarfile.createBitMapIndex(col) (R/columnar/Columnarfile.java:698-753)
+ * on the GPU: distinct live values in first-occurrence order (k_distinct),
+ * one BitSet per value (k_index_build4 / k_index_build) over `t` -- the
+ * table mbx_db_stage produced for `name` -- then, in the reference's order,
+ * one BitMapFile cf.bm.<col>.<value> header + hdr registry record "col.value"
+ * per value, the BitSet chunks (BM.insertBitSet, values in java.util.HashMap
+ * iteration order) and bitmapExist[col] = 1.  Int and char(n) columns, as in
+ * the reference; at most 65536 distinct values.  *nvalues = values indexed
+ * (0 when the column already had a bitmap index: the reference is a no-op). */
+int mbx_db_create_bitmap_index(mbx_ctx* ctx, mbx_db* db, const char* name, const mbx_table* t, int32_t col,
+                               int32_t* nvalues);
+
+/* The bitmap-index registry of column col ("col.value" records of cf.hdr,
+ * Columnarfile.java:150-162): *count values, written NUL-separated (modified
+ * UTF-8 text of the value) into buf when it is large enough; *bytes = the
+ * size needed. */
+int mbx_db_bitmap_values(mbx_db* db, const char* name, int32_t col, char* buf, int64_t cap, int32_t* count,
+                         int64_t* bytes);
+
+/* BitMapFile `filename` -> a device bitmap of nbits bits (BM.readBitSet; bits
+ * past nbits are dropped, missing words are zero), ready for
+ * mbx_bitmap_cnf / mbx_materialize. */
+int mbx_db_bitmap_stage(mbx_ctx* ctx, mbx_db* db, const char* filename, int64_t nbits, mbx_bitmap** out);
 
 /* Stage a Columnarfile from the DB file into HBM: the used pages of the file
  * are copied to the device as they lie on disk and one k_page_decode launch

@@ -67,7 +67,7 @@ int mbx::set_device(mbx_ctx* c) {
 }
 
 // device string image: modified UTF-8, C0 80 -> 00 01, zero padded to stride
-static void encode_device_string(const uint8_t* src, int32_t len, uint8_t* dst, int32_t stride) {
+void mbx::encode_device_string(const uint8_t* src, int32_t len, uint8_t* dst, int32_t stride) {
   int32_t n = len < stride ? len : stride;
   // the payload ends at the first 0x00 (zero padding never occurs inside modified UTF-8)
   int32_t m = 0;
@@ -84,7 +84,7 @@ static void encode_device_string(const uint8_t* src, int32_t len, uint8_t* dst, 
   }
 }
 
-static void decode_device_string(const uint8_t* src, int32_t stride, uint8_t* dst, int32_t size) {
+void mbx::decode_device_string(const uint8_t* src, int32_t stride, uint8_t* dst, int32_t size) {
   memset(dst, 0, (size_t)size);
   for (int32_t i = 0; i < stride && i < size; i++) {
     if (src[i] == 0x00) {
@@ -1024,6 +1024,15 @@ extern "C" int mbx_bitmap_index_build(mbx_ctx* c, const mbx_table* t, int32_t co
       encode_device_string((const uint8_t*)o.string, o.string_len, (uint8_t*)&vals[(size_t)v * vw], vw * 4);
     }
   }
+  return index_build_encoded(c, t, col, vals.data(), nvalues, out);
+}
+
+int mbx::index_build_encoded(mbx_ctx* c, const mbx_table* t, int32_t col, const uint32_t* host_vals,
+                             int32_t nvalues, mbx_bitmap** out) {
+  const TCol& tc = t->cols[(size_t)col];
+  const int32_t vw = tc.attr_type == MBX_ATTR_STRING ? tc.stride_w : 1;
+  int rc = MBX_OK;
+  std::vector<uint32_t> vals(host_vals, host_vals + (size_t)nvalues * (size_t)vw);
   for (int32_t v = 0; v < nvalues; v++) out[v] = nullptr;
   uint32_t* dvals = nullptr;
   HIPCHK(hipMalloc(&dvals, vals.size() * 4));

@@ -125,6 +125,22 @@ void set_page_bit(mbx_db* db, int64_t pid, bool on) {
     map[pid >> 3] &= (uint8_t)~(1u << (pid & 7));
 }
 
+// DB.allocate_page(start, run): first run of `run` zero bits
+int alloc_run(mbx_db* db, int32_t run, int32_t* start) {
+  int64_t len = 0;
+  for (int64_t p = db->alloc_hint; p < db->num_pages; ++p) {
+    len = page_bit(db, p) ? 0 : len + 1;
+    if (len == run) {
+      const int64_t s = p - run + 1;
+      for (int64_t q = s; q <= p; ++q) set_page_bit(db, q, true);
+      while (db->alloc_hint < db->num_pages && page_bit(db, db->alloc_hint)) ++db->alloc_hint;
+      *start = (int32_t)s;
+      return MBX_OK;
+    }
+  }
+  return fail(MBX_E_NOMEM, "OutOfSpaceException: DB %s has no run of %d free pages", db->path.c_str(), run);
+}
+
 // DB.allocate_page(start, 1): first zero bit of the space map
 int alloc_page(mbx_db* db, int32_t* pid) {
   for (int64_t p = db->alloc_hint; p < db->num_pages; ++p) {
@@ -605,6 +621,20 @@ extern "C" int mbx_db_info(const mbx_db* cdb, int32_t* num_pages, int32_t* alloc
   return MBX_OK;
 }
 
+extern "C" int mbx_db_allocate_pages(mbx_db* db, int32_t run_size, int32_t* start) {
+  NOTNULL(db);
+  NOTNULL(start);
+  if (run_size < 1) return fail(MBX_E_INVALID, "InvalidRunSizeException: %d", run_size);
+  return alloc_run(db, run_size, start);
+}
+
+extern "C" int mbx_db_add_file_entry(mbx_db* db, const char* name, int32_t start) {
+  NOTNULL(db);
+  NOTNULL(name);
+  if (start < 0 || start >= db->num_pages) return fail(MBX_E_INVALID, "InvalidPageNumberException: %d", start);
+  return add_file_entry(db, name, start);
+}
+
 extern "C" int mbx_db_file_entry(mbx_db* db, const char* name, int32_t* first_page) {
   NOTNULL(db);
   NOTNULL(name);
@@ -979,4 +1009,275 @@ extern "C" int mbx_db_stage(mbx_ctx* c, mbx_db* db, const char* name, mbx_table*
   }
   *out = t;
   return MBX_OK;
+}
+
+// ------------------------------------------------- bitmap-index persistence
+
+namespace {
+
+// modified UTF-8 -> UTF-16 code units (DataInputStream.readUTF)
+std::vector<uint16_t> mutf8_units(const std::string& s) {
+  std::vector<uint16_t> u;
+  for (size_t i = 0; i < s.size();) {
+    const uint8_t b = (uint8_t)s[i];
+    if (b < 0x80) {
+      u.push_back(b);
+      i += 1;
+    } else if ((b & 0xE0) == 0xC0 && i + 1 < s.size()) {
+      u.push_back((uint16_t)(((b & 0x1F) << 6) | ((uint8_t)s[i + 1] & 0x3F)));
+      i += 2;
+    } else if (i + 2 < s.size()) {
+      u.push_back((uint16_t)(((b & 0x0F) << 12) | (((uint8_t)s[i + 1] & 0x3F) << 6) | ((uint8_t)s[i + 2] & 0x3F)));
+      i += 3;
+    } else {
+      u.push_back(b);
+      i += 1;
+    }
+  }
+  return u;
+}
+
+int32_t java_string_hash(const std::string& mutf8) {
+  uint32_t h = 0;
+  for (uint16_t c : mutf8_units(mutf8)) h = 31u * h + c;
+  return (int32_t)h;
+}
+
+// java.util.HashMap iteration order of keys put in the given order (JDK 8+:
+// table of 16 at the first put, doubled when size exceeds 0.75 * capacity or
+// when a bin reaches 8 nodes while the table is smaller than 64; buckets
+// visited in index order, each bin in insertion order -- bins that would
+// become trees keep list order here, a documented approximation)
+std::vector<size_t> hashmap_order(const std::vector<int32_t>& hashes) {
+  auto spread = [](int32_t h) { return (uint32_t)h ^ ((uint32_t)h >> 16); };
+  uint32_t cap = 16;
+  std::unordered_map<uint32_t, int> bins;
+  auto rebuild = [&](size_t upto) {
+    bins.clear();
+    for (size_t j = 0; j < upto; ++j) bins[spread(hashes[j]) & (cap - 1)]++;
+  };
+  for (size_t i = 0; i < hashes.size(); ++i) {
+    const uint32_t b = spread(hashes[i]) & (cap - 1);
+    const int before = bins[b]++;
+    if (before >= 8 && cap < 64) {  // treeifyBin -> resize()
+      cap *= 2;
+      rebuild(i + 1);
+    }
+    if (i + 1 > (size_t)(cap * 3 / 4)) {
+      cap *= 2;
+      rebuild(i + 1);
+    }
+  }
+  std::vector<size_t> order(hashes.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+    return (spread(hashes[a]) & (cap - 1)) < (spread(hashes[b]) & (cap - 1));
+  });
+  return order;
+}
+
+constexpr int64_t kMaxDistinct = 65536;
+
+int find_hdr_record(mbx_db* db, int32_t hdr, int32_t index, uint8_t** rec, int32_t* len) {
+  int32_t k = 0;
+  *rec = nullptr;
+  int rc = heap_scan(db, hdr, [&](const DataPage& d, int32_t s, const uint8_t*, int32_t l) {
+    if (k++ == index) {
+      uint8_t* pg = db->page(d.pid);
+      *rec = pg + hf_slot_off(pg, s);
+      *len = l;
+      return false;
+    }
+    return true;
+  });
+  if (rc) return rc;
+  if (!*rec) return fail(MBX_E_INVALID, "hdr record %d is missing", index);
+  return MBX_OK;
+}
+
+}  // namespace
+
+extern "C" int mbx_db_create_bitmap_index(mbx_ctx* c, mbx_db* db, const char* name, const mbx_table* t, int32_t col,
+                                          int32_t* nvalues) {
+  NOTNULL(c);
+  NOTNULL(db);
+  NOTNULL(name);
+  NOTNULL(t);
+  if (nvalues) *nvalues = 0;
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  if (col < 0 || col >= sc.ncols) return fail(MBX_E_RANGE, "createBitMapIndex: column %d of %d", col, sc.ncols);
+  if ((int32_t)t->cols.size() != sc.ncols) return fail(MBX_E_INVALID, "createBitMapIndex: table is not %s", name);
+  const int32_t type = sc.cols[(size_t)col].attr_type;
+  if (type != MBX_ATTR_INTEGER && type != MBX_ATTR_STRING)
+    return fail(MBX_E_UNSUPPORTED, "createBitMapIndex: AttrType %d columns have no bitmap index in the reference",
+                type);
+  if ((size_t)col < sc.bitmap_exist.size() && sc.bitmap_exist[(size_t)col] == 1) return MBX_OK;
+  if ((rc = set_device(c))) return rc;
+  const TCol& tc = t->cols[(size_t)col];
+  const int64_t nrows = t->nrows;
+  hipStream_t s = c->stream;
+
+  // 1. distinct live values and their first positions (k_distinct)
+  int64_t cap = 64;
+  while (cap < 2 * std::min<int64_t>(nrows, kMaxDistinct)) cap *= 2;
+  unsigned long long *keys = nullptr, *minpos = nullptr;
+  int32_t* dflag = nullptr;
+  HIPCHK(hipMalloc(&keys, sizeof(unsigned long long) * (size_t)cap));
+  hipError_t e = hipMalloc(&minpos, sizeof(unsigned long long) * (size_t)cap);
+  if (e == hipSuccess) e = hipMalloc(&dflag, sizeof(int32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(keys, 0xFF, sizeof(unsigned long long) * (size_t)cap, s);
+  if (e == hipSuccess) e = hipMemsetAsync(minpos, 0xFF, sizeof(unsigned long long) * (size_t)cap, s);
+  if (e == hipSuccess) e = hipMemsetAsync(dflag, 0, sizeof(int32_t), s);
+  KCol kc;
+  kc.base = tc.dev;
+  kc.kind = type == MBX_ATTR_STRING ? kStr : kInt;
+  kc.stride_w = tc.stride_w;
+  if (e == hipSuccess) {
+    DistinctArgs A;
+    A.col = kc;
+    A.nrows = nrows;
+    A.del = t->deleted;
+    A.keys = keys;
+    A.minpos = minpos;
+    A.cap = cap;
+    A.overflow = dflag;
+    e = launch_distinct(A, s);
+  }
+  std::vector<unsigned long long> hmin((size_t)cap);
+  int32_t overflow = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(hmin.data(), minpos, sizeof(unsigned long long) * (size_t)cap,
+                                          hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(&overflow, dflag, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  hipFree(keys);
+  hipFree(minpos);
+  hipFree(dflag);
+  if (e != hipSuccess) return fail(MBX_E_DEVICE, "createBitMapIndex: %s", hipGetErrorString(e));
+  std::vector<int64_t> first;
+  for (unsigned long long p : hmin)
+    if (p != kEmptySlot) first.push_back((int64_t)p);
+  if (overflow || (int64_t)first.size() > kMaxDistinct)
+    return fail(MBX_E_UNSUPPORTED, "createBitMapIndex: more than %lld distinct values", (long long)kMaxDistinct);
+  std::sort(first.begin(), first.end());
+  const int32_t nv = (int32_t)first.size();
+  if (nv == 0) {
+    // no live row: the reference registers nothing and only sets the flag
+    uint8_t* rec;
+    int32_t len;
+    if ((rc = find_hdr_record(db, get_file_entry(db, std::string(name) + ".hdr"), 5, &rec, &len))) return rc;
+    if (col < len) rec[col] = 1;
+    return MBX_OK;
+  }
+
+  // 2. the values themselves (device image of the first-occurrence rows)
+  const int32_t vw = kc.kind == kStr ? tc.stride_w : 1;
+  std::vector<uint32_t> vals((size_t)nv * (size_t)vw);
+  {
+    int64_t* drows = nullptr;
+    uint32_t* dvals = nullptr;
+    HIPCHK(hipMalloc(&drows, sizeof(int64_t) * (size_t)nv));
+    e = hipMalloc(&dvals, sizeof(uint32_t) * vals.size());
+    if (e == hipSuccess) e = hipMemcpyAsync(drows, first.data(), sizeof(int64_t) * (size_t)nv, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = launch_rows_fetch(kc, drows, nv, dvals, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(vals.data(), dvals, sizeof(uint32_t) * vals.size(), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(drows);
+    hipFree(dvals);
+    if (e != hipSuccess) return fail(MBX_E_DEVICE, "createBitMapIndex: %s", hipGetErrorString(e));
+  }
+  std::vector<std::string> text((size_t)nv);
+  std::vector<int32_t> hashes((size_t)nv);
+  for (int32_t v = 0; v < nv; ++v) {
+    if (kc.kind == kStr) {
+      std::vector<uint8_t> buf((size_t)tc.size + 1, 0);
+      decode_device_string((const uint8_t*)&vals[(size_t)v * vw], vw * 4, buf.data(), tc.size);
+      text[(size_t)v] = std::string((const char*)buf.data(), strnlen((const char*)buf.data(), (size_t)tc.size));
+      hashes[(size_t)v] = java_string_hash(text[(size_t)v]);
+    } else {
+      const int32_t x = (int32_t)vals[(size_t)v];
+      text[(size_t)v] = std::to_string(x);
+      hashes[(size_t)v] = x;  // Integer.hashCode
+    }
+  }
+
+  // 3. one BitSet per value on the GPU
+  std::vector<mbx_bitmap*> bms((size_t)nv, nullptr);
+  if ((rc = index_build_encoded(c, t, col, vals.data(), nv, bms.data()))) return rc;
+  auto free_all = [&]() {
+    for (mbx_bitmap* b : bms) mbx_bitmap_free(b);
+  };
+
+  // 4. files, in the reference's order: per value (scan order) the header
+  // page + file entry, then the hdr registry record; then the BitSet chunks
+  // in HashMap order; then bitmapExist
+  const std::string cf = name;
+  const int32_t hdr = get_file_entry(db, cf + ".hdr");
+  std::vector<int32_t> heads((size_t)nv);
+  for (int32_t v = 0; v < nv && !rc; ++v) {
+    const std::string key = std::to_string(col) + "." + text[(size_t)v];
+    rc = bm_create_header(db, cf + ".bm." + key, &heads[(size_t)v]);
+    std::vector<uint8_t> rec(key.size() + 2, 0);
+    put_utf(rec.data(), key);
+    int32_t pid, slot;
+    if (!rc) rc = heap_insert(db, hdr, rec.data(), (int32_t)rec.size(), &pid, &slot);
+  }
+  std::vector<uint64_t> words;
+  for (size_t k : hashmap_order(hashes)) {
+    if (rc) break;
+    mbx_bitmap* b = bms[k];
+    words.assign((size_t)(b->nwords > 0 ? b->nwords : 1), 0ull);
+    if (b->nwords > 0 && (rc = mbx_bitmap_download(c, b, words.data(), b->nwords))) break;
+    rc = bm_insert_bitset(db, heads[k], bitset_bytes(words.data(), b->nwords));
+  }
+  free_all();
+  if (rc) return rc;
+  uint8_t* rec;
+  int32_t len;
+  if ((rc = find_hdr_record(db, hdr, 5, &rec, &len))) return rc;
+  if (col < len) rec[col] = 1;
+  if (nvalues) *nvalues = nv;
+  return MBX_OK;
+}
+
+extern "C" int mbx_db_bitmap_values(mbx_db* db, const char* name, int32_t col, char* buf, int64_t cap,
+                                    int32_t* count, int64_t* bytes) {
+  NOTNULL(db);
+  NOTNULL(name);
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  const std::string prefix = std::to_string(col) + ".";
+  std::string out;
+  int32_t n = 0;
+  for (const std::string& r : sc.bm_values) {
+    if (r.compare(0, prefix.size(), prefix) != 0) continue;
+    out += r.substr(prefix.size());
+    out.push_back('\0');
+    ++n;
+  }
+  if (count) *count = n;
+  if (bytes) *bytes = (int64_t)out.size();
+  if (buf && cap >= (int64_t)out.size()) memcpy(buf, out.data(), out.size());
+  return MBX_OK;
+}
+
+extern "C" int mbx_db_bitmap_stage(mbx_ctx* c, mbx_db* db, const char* filename, int64_t nbits, mbx_bitmap** out) {
+  NOTNULL(c);
+  NOTNULL(db);
+  NOTNULL(filename);
+  NOTNULL(out);
+  *out = nullptr;
+  if (nbits < 0) return fail(MBX_E_INVALID, "bitmap_stage: nbits %lld", (long long)nbits);
+  const int32_t head = get_file_entry(db, filename);
+  if (head == kInvalidPage) return fail(MBX_E_INVALID, "The file %s does not exist.", filename);
+  std::vector<uint8_t> bytes;
+  int rc = bm_read_bytes(db, head, &bytes);
+  if (rc) return rc;
+  const int64_t nw = words_for(nbits);
+  std::vector<uint64_t> words((size_t)(nw > 0 ? nw : 1), 0ull);
+  memcpy(words.data(), bytes.data(), std::min<size_t>(bytes.size(), (size_t)nw * 8));
+  if (nbits & 63) words[(size_t)nw - 1] &= (1ull << (nbits & 63)) - 1ull;
+  return mbx_bitmap_upload(c, nbits, words.data(), out);
 }

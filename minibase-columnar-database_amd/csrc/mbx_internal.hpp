@@ -172,6 +172,21 @@ hipError_t launch_present_merge(const uint64_t* present0, const uint64_t* other,
                                 const uint64_t* md, int64_t md_words, int64_t nrows, uint64_t* del, int32_t* flags,
                                 hipStream_t s);
 
+constexpr unsigned long long kEmptySlot = ~0ull;
+
+struct DistinctArgs {
+  KCol col;
+  int64_t nrows;
+  const uint64_t* del;          // deleted positions are skipped (ColumnScan)
+  unsigned long long* keys;     // cap slots, kEmptySlot = free; else a representative row
+  unsigned long long* minpos;   // cap slots, kEmptySlot initially; smallest row with the value
+  int64_t cap;                  // power of two
+  int32_t* overflow;
+};
+
+hipError_t launch_distinct(const DistinctArgs& A, hipStream_t s);
+hipError_t launch_rows_fetch(const KCol& c, const int64_t* rows, int64_t n, uint32_t* out, hipStream_t s);
+
 int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block);
 int64_t choose_tiles_per_block(int64_t nrows);
 

@@ -120,6 +120,13 @@ int64_t words_for(int64_t nbits);
 int table_alloc(mbx_ctx* c, const mbx_col_desc* cols, int32_t ncols, int64_t nrows, int64_t row_offset,
                 bool with_deleted, mbx_table** out);
 int bitmap_new(mbx_ctx* c, int64_t nbits, mbx_bitmap** out);
+// one BitSet per value of column `col` (values in the device image: 1 word
+// for int/float, stride_w words for char(n)); out[nvalues]
+int index_build_encoded(mbx_ctx* c, const mbx_table* t, int32_t col, const uint32_t* host_vals, int32_t nvalues,
+                        mbx_bitmap** out);
+// host modified UTF-8 (zero padded to len) <-> device string image (stride bytes)
+void encode_device_string(const uint8_t* src, int32_t len, uint8_t* dst, int32_t stride);
+void decode_device_string(const uint8_t* src, int32_t stride, uint8_t* dst, int32_t size);
 // recount per-segment popcounts of a bitmap written on the device, sync, and
 // set b->count
 int bitmap_recount(mbx_ctx* c, mbx_bitmap* b);

@@ -12,6 +12,8 @@
 //   k_present_merge  deleted = NOT present(column 0) OR cf.md, and a mismatch
 //                    flag when another column's present set differs
 //                    (Columnarfile.java:480-482 "Invalid position calculations").
+//   k_distinct       distinct live values + first position (createBitMapIndex).
+//   k_rows_fetch     a few rows of a column (the distinct values themselves).
 //
 // Byte/integer work, HBM bound: per page 1 KiB read + the decoded records
 // written; no MFMA, no LDS.
@@ -108,6 +110,93 @@ __global__ __launch_bounds__(kBlock) void k_present_merge(const uint64_t* __rest
     del[w] = d;
     if (d) atomicOr(flags, 2);
   }
+}
+
+// ------------------------------------------------ distinct column values
+//
+// Columnarfile.createBitMapIndex registers one BitMapFile per distinct value
+// of the live rows, in first-occurrence (ColumnScan) order
+// (R/columnar/Columnarfile.java:698-753).  One pass over the column inserts
+// every live row into an open-addressing table in HBM whose slots hold a
+// representative row (the key: rows compare by column value) and the
+// smallest position holding that value.  A row first READS the slot's
+// minimum and only issues atomicMin when it is smaller, so a low-cardinality
+// column (the bitmap-index case) costs reads of a few hot L2 lines, not
+// same-address atomics per row.
+
+__device__ __forceinline__ uint64_t mix64(uint64_t h) {
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdull;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ull;
+  h ^= h >> 33;
+  return h;
+}
+
+__device__ __forceinline__ uint64_t row_hash(const KCol& c, int64_t row) {
+  const uint32_t* p = (const uint32_t*)c.base + row * c.stride_w;
+  uint64_t h = 1469598103934665603ull;
+  for (int i = 0; i < c.stride_w; ++i) h = (h ^ p[i]) * 1099511628211ull;
+  return mix64(h);
+}
+
+__device__ __forceinline__ bool rows_equal(const KCol& c, int64_t a, int64_t b) {
+  const uint32_t* pa = (const uint32_t*)c.base + a * c.stride_w;
+  const uint32_t* pb = (const uint32_t*)c.base + b * c.stride_w;
+  for (int i = 0; i < c.stride_w; ++i)
+    if (pa[i] != pb[i]) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(kBlock) void k_distinct(DistinctArgs A) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const uint64_t mask = (uint64_t)A.cap - 1;
+  for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < A.nrows; row += stride) {
+    if (A.del && ((A.del[row >> 6] >> (row & 63)) & 1ull)) continue;
+    uint64_t h = row_hash(A.col, row) & mask;
+    bool placed = false;
+    for (int64_t probe = 0; probe < A.cap; ++probe, h = (h + 1) & mask) {
+      unsigned long long k = __hip_atomic_load(A.keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == kEmptySlot) {
+        k = atomicCAS(A.keys + h, kEmptySlot, (unsigned long long)row);
+        if (k == kEmptySlot) k = (unsigned long long)row;
+      }
+      if (rows_equal(A.col, (int64_t)k, row)) {
+        const unsigned long long m =
+            __hip_atomic_load(A.minpos + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned long long)row < m) atomicMin(A.minpos + h, (unsigned long long)row);
+        placed = true;
+        break;
+      }
+    }
+    if (!placed) atomicOr(A.overflow, 1);
+  }
+}
+
+// rows[i] of a column -> out (stride_w words per row)
+__global__ __launch_bounds__(kBlock) void k_rows_fetch(KCol c, const int64_t* __restrict__ rows, int64_t n,
+                                                       uint32_t* __restrict__ out) {
+  const int64_t total = n * c.stride_w;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = i / c.stride_w, w = i - r * c.stride_w;
+    out[i] = ((const uint32_t*)c.base)[rows[r] * c.stride_w + w];
+  }
+}
+
+hipError_t launch_distinct(const DistinctArgs& A, hipStream_t s) {
+  if (A.nrows <= 0) return hipSuccess;
+  int64_t g = (A.nrows + kBlock - 1) / kBlock;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(k_distinct, dim3((unsigned)g), dim3(kBlock), 0, s, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_rows_fetch(const KCol& c, const int64_t* rows, int64_t n, uint32_t* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  int64_t g = (n * c.stride_w + kBlock - 1) / kBlock;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(k_rows_fetch, dim3((unsigned)g), dim3(kBlock), 0, s, c, rows, n, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_page_decode(const PageDecodeArgs& A, hipStream_t s) {

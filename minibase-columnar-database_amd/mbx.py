@@ -89,7 +89,8 @@ EXPORTS = [
     # include/mbx_db.h
     "mbx_db_create", "mbx_db_open", "mbx_db_close", "mbx_db_info", "mbx_db_file_entry", "mbx_db_columnar_create",
     "mbx_db_columnar_insert", "mbx_db_columnar_info", "mbx_db_mark_deleted", "mbx_db_bitmap_write",
-    "mbx_db_bitmap_read", "mbx_db_stage",
+    "mbx_db_bitmap_read", "mbx_db_stage", "mbx_db_allocate_pages", "mbx_db_add_file_entry",
+    "mbx_db_create_bitmap_index", "mbx_db_bitmap_values", "mbx_db_bitmap_stage",
 ]
 
 _lib = None
@@ -154,6 +155,11 @@ def lib():
         "mbx_db_bitmap_write": ([V, ctypes.c_char_p, V, I64], ctypes.c_int),
         "mbx_db_bitmap_read": ([V, ctypes.c_char_p, V, I64, P(I64)], ctypes.c_int),
         "mbx_db_stage": ([V, V, ctypes.c_char_p, P(V)], ctypes.c_int),
+        "mbx_db_allocate_pages": ([V, I32, P(I32)], ctypes.c_int),
+        "mbx_db_add_file_entry": ([V, ctypes.c_char_p, I32], ctypes.c_int),
+        "mbx_db_create_bitmap_index": ([V, V, ctypes.c_char_p, V, I32, P(I32)], ctypes.c_int),
+        "mbx_db_bitmap_values": ([V, ctypes.c_char_p, I32, V, I64, P(I32), P(I64)], ctypes.c_int),
+        "mbx_db_bitmap_stage": ([V, V, ctypes.c_char_p, I64, P(V)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -301,6 +307,17 @@ class Context:
         _chk(lib().mbx_table_wrap(self.h, descs, len(col_descs), nrows, ptrs, dev_deleted, row_offset,
                                   ctypes.byref(h)))
         return Table(self, h, nrows, list(col_descs), row_offset, keep=[descs, ptrs])
+
+    def create_bitmap_index(self, db, name, table, col):
+        """mbx_db_create_bitmap_index: `index db cf <col> bitmap` on the GPU."""
+        n = ctypes.c_int32()
+        _chk(lib().mbx_db_create_bitmap_index(self.h, db.h, name.encode(), table.h, col, ctypes.byref(n)))
+        return n.value
+
+    def stage_db_bitmap(self, db, filename, nbits):
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_db_bitmap_stage(self.h, db.h, filename.encode(), nbits, ctypes.byref(h)))
+        return Bitmap(self, h, nbits)
 
     def stage_db(self, db, name):
         """mbx_db_stage: a Columnarfile of a Minibase DB file -> HBM table
@@ -585,6 +602,22 @@ class Db:
         return {"ncols": n.value, "cols": [(descs[j].attr_type, descs[j].size) for j in range(k)],
                 "names": [names.raw[16 * j:16 * j + 16].split(b"\0")[0].decode() for j in range(k)],
                 "nrows": nrows.value, "live": live.value}
+
+    def allocate_pages(self, run):
+        p = ctypes.c_int32()
+        _chk(lib().mbx_db_allocate_pages(self.h, run, ctypes.byref(p)))
+        return p.value
+
+    def add_file_entry(self, name, start):
+        _chk(lib().mbx_db_add_file_entry(self.h, name.encode(), start))
+
+    def bitmap_values(self, name, col):
+        """Registered bitmap-index values of a column (modified UTF-8 bytes)."""
+        cnt, nb = ctypes.c_int32(), ctypes.c_int64()
+        _chk(lib().mbx_db_bitmap_values(self.h, name.encode(), col, None, 0, ctypes.byref(cnt), ctypes.byref(nb)))
+        buf = ctypes.create_string_buffer(max(1, nb.value))
+        _chk(lib().mbx_db_bitmap_values(self.h, name.encode(), col, buf, nb.value, ctypes.byref(cnt), ctypes.byref(nb)))
+        return buf.raw[:nb.value].split(b"\0")[:cnt.value]
 
     def mark_deleted(self, name, position):
         _chk(lib().mbx_db_mark_deleted(self.h, name.encode(), position))

@@ -82,6 +82,10 @@ def main():
             elif cmd == "index" and len(toks) >= 5 and "Read" in sets:
                 db_pages["column_scan_reads"].setdefault(toks[3], {"pages": sets["Read"][0], "line": sets["Read"][1],
                                                                    "cmd": ln[2:].strip()})
+                if "Wrote" in sets:
+                    db_pages.setdefault("index_runs", []).append(
+                        {"cmd": ln[2:].strip(), "col": toks[3], "kind": toks[4], "wrote": sets["Wrote"][0],
+                         "line": sets["Wrote"][1]})
         elif cmd == "bmj" and len(toks) >= 6 and toks[1] == "db":
             outer, inner = split_cnf(toks[4]), split_cnf(toks[5])
             for k, b in enumerate(body):

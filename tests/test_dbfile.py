@@ -268,3 +268,100 @@ def test_stage_rejects_malformed_pages(m, ctx, tmp_path):
         with pytest.raises(m.MbxError) as e:
             ctx.stage_db(db, "cf")
         assert "malformed" in str(e.value)
+
+
+def first_occurrence(values):
+    seen, out = set(), []
+    for v in values:
+        if v not in seen:
+            seen.add(v)
+            out.append(v)
+    return out
+
+
+@pytest.mark.gpu
+def test_bitmap_index_persistence_matches_reference_pages(m, ctx, tmp_path):
+    """`index db cf A btree` then `index db cf {A,B,C,D} bitmap` as in the
+    reference session (R/phase3_output:3167-3265): the B+-tree file is only
+    reserved (18 pages + its file entry -- out of scope), the bitmap indexes
+    are built on the GPU and written as BitMapFiles; the pages each command
+    allocates equal the ones the reference wrote, the registry holds the
+    values in first-occurrence order and every BitMapFile holds the oracle's
+    BitSet."""
+    path = str(tmp_path / "db")
+    db, cols = minidata_db(m, path)
+    runs = [r for r in GOLD["db_pages"]["index_runs"] if r["line"] <= 3265]
+    assert [r["cmd"] for r in runs] == ["index db cf A btree", "index db cf A bitmap", "index db cf B bitmap",
+                                        "index db cf C bitmap", "index db cf D bitmap"]
+    head = db.allocate_pages(1)
+    db.add_file_entry("cf.btree.0", head)
+    assert db.allocate_pages(17) == head + 1
+    assert head == 177
+    t = ctx.stage_db(db, "cf")
+    rows = helpers.load_minidata()
+    ot = oracle.Table(cols)
+    before = db.info()[1]
+    top = 194
+    for r in runs[1:]:
+        col = "ABCD".index(r["col"])
+        n = ctx.create_bitmap_index(db, "cf", t, col)
+        want_vals = first_occurrence([row[col] for row in rows])
+        assert n == len(want_vals)
+        new = [p for p in sorted(set(r["wrote"])) if p > top]
+        after = db.info()[1]
+        assert after - before == len(new), r["cmd"]
+        assert new == list(range(top + 1, top + 1 + len(new)))
+        before, top = after, new[-1]
+        got_vals = db.bitmap_values("cf", col)
+        assert got_vals == [oracle.java_mutf8(str(v)) for v in want_vals]
+        for v in want_vals:
+            w = db.bitmap_read(f"cf.bm.{col}.{v}")
+            spec = ("str", v) if col < 2 else ("int", v)
+            n_o, w_o = oracle.bitmap_eq(ot, col, spec)
+            assert np.array_equal(w[:len(w_o)], w_o[:len(w)]) and not w[len(w_o):].any()
+            bm = ctx.stage_db_bitmap(db, f"cf.bm.{col}.{v}", 500)
+            assert bm.count == n_o
+        assert ctx.create_bitmap_index(db, "cf", t, col) == 0     # already indexed: no-op
+    db.close()
+    img = mp.DbImage(path)
+    assert mp.columnar_schema(img, "cf")["bitmap"] == [1, 1, 1, 1]
+
+
+@pytest.mark.gpu
+def test_bitmap_index_large_and_deleted(m, ctx, tmp_path):
+    """Multi-chunk BitMapFiles (positions past 8000 bits), deleted rows left
+    out of every BitSet, value order = first live occurrence."""
+    path = str(tmp_path / "db")
+    n = 50_000
+    rng = np.random.Generator(np.random.PCG64(12))
+    vals = rng.integers(-5, 40, n, dtype=np.int32)
+    words = ["Ohio", "Iowa", "Utah", "é", "Wyoming_12"]
+    svals = [words[i] for i in rng.integers(0, len(words), n)]
+    cols = [(oracle.INTEGER, 4, vals), (oracle.STRING, 12, helpers.encode_strings(svals, 12))]
+    with m.mbx.Db(path, 1 << 15) as db:
+        db.columnar_create("cf", [(oracle.INTEGER, 4), (oracle.STRING, 12)], ["v", "s"])
+        db.columnar_insert("cf", cols)
+        dead = sorted(set(int(x) for x in rng.integers(0, n, 500)))
+        for p in dead:
+            db.mark_deleted("cf", p)
+        t = ctx.stage_db(db, "cf")
+        assert ctx.create_bitmap_index(db, "cf", t, 0) > 0
+        assert ctx.create_bitmap_index(db, "cf", t, 1) > 0
+        live = np.ones(n, dtype=bool)
+        live[dead] = False
+        assert db.bitmap_values("cf", 0) == [str(v).encode() for v in first_occurrence(vals[live].tolist())]
+        assert db.bitmap_values("cf", 1) == [oracle.java_mutf8(v) for v in
+                                             first_occurrence([s for s, l in zip(svals, live) if l])]
+    img = mp.DbImage(path)
+    _, ocols, dele = mp.columnar_table(img, "cf")
+    ot = oracle.Table(ocols, dele)
+    for v in set(vals[live].tolist()):
+        n_o, w_o = oracle.bitmap_eq(ot, 0, ("int", v))
+        w = mp.bitmap_words(img, f"cf.bm.0.{v}")
+        k = min(len(w), len(w_o))
+        assert np.array_equal(w[:k], w_o[:k]) and not w[k:].any() and not w_o[k:].any()
+    for s in set(s for s, l in zip(svals, live) if l):
+        n_o, w_o = oracle.bitmap_eq(ot, 1, ("str", s))
+        w = mp.bitmap_words(img, "cf.bm.1." + oracle.java_mutf8(s).decode("utf-8", "surrogatepass"))
+        k = min(len(w), len(w_o))
+        assert np.array_equal(w[:k], w_o[:k]) and not w[k:].any()
