@@ -3,6 +3,9 @@
 // operator mirror (minibase.hpp):
 //
 //   batchinsert DATAFILE DBNAME COLUMNARFILENAME NUMCOLUMNS   (R/input/BatchInsert.java:17-137)
+//     (DBNAME is a Minibase DB file in the working directory, created with
+//      1024*1024 pages when absent -- include/mbx_db.h; the other commands
+//      open it and stage the Columnarfile to HBM with the GPU page decoder)
 //   index DBNAME COLUMNARFILENAME COLUMNNAME bitmap            (R/input/Index.java:16-67)
 //   query DBNAME COLUMNARFILENAME [TARGETCOLS] {C,OP,V} NUMBUF FILESCAN|COLUMNSCAN|BITMAP
 //                                                              (R/input/Query.java:35-361)
@@ -34,8 +37,6 @@ using iterator::RelSpec;
 
 namespace {
 
-std::set<std::string> g_dbs;
-
 std::vector<std::string> split(const std::string& s, char sep) {
   std::vector<std::string> out;
   std::string cur;
@@ -57,8 +58,6 @@ std::string trim(const std::string& s) {
   while (b > a && isspace((unsigned char)s[b - 1])) b--;
   return s.substr(a, b - a);
 }
-
-std::string cf_key(const std::string& db, const std::string& cf) { return db + "/" + cf; }
 
 void print_results_footer(int64_t n) {
   std::cout << "\n************************************************************************\n"
@@ -94,8 +93,9 @@ void batchinsert(const std::vector<std::string>& a) {
       throw std::runtime_error("column attr type is not supported.");
     }
   }
-  g_dbs.insert(db);
-  columnar::Columnarfile cf(cf_key(db, cfname), numcolumns, names, types, sizes);
+  // SystemDefs(db, exists ? 0 : 1024*1024, ...) (R/input/BatchInsert.java:52-57)
+  mbx_db* dbh = global::SystemDefs::open(db, 1024 * 1024);
+  columnar::Columnarfile cf(dbh, cfname, numcolumns, names, types, sizes);
   std::vector<std::vector<int32_t>> ints;
   std::vector<std::vector<float>> reals;
   std::vector<std::vector<std::string>> strs;
@@ -125,14 +125,13 @@ void batchinsert(const std::vector<std::string>& a) {
     }
     n++;
   }
-  cf.insertColumns(ints, reals, strs, n);
-  cf.table();  // stage to HBM now, like BatchInsert writing the pages
+  cf.insertColumns(ints, reals, strs, n);  // pages written to the DB file
   std::cout << "Record count: " << cf.getTupleCnt() << "\n";
 }
 
 columnar::Columnarfile open_cf(const std::string& db, const std::string& cf) {
-  if (!g_dbs.count(db)) throw std::runtime_error("Database does not exist.");
-  return columnar::Columnarfile(cf_key(db, cf));
+  if (!global::SystemDefs::exists(db)) throw std::runtime_error("Database does not exist.");
+  return columnar::Columnarfile(global::SystemDefs::open(db, 0), cf);
 }
 
 void index_cmd(const std::vector<std::string>& a) {

@@ -72,9 +72,39 @@ void close_all_files();
 }
 namespace global {
 
+static std::map<std::string, mbx_db*>& open_dbs() {
+  static std::map<std::string, mbx_db*> m;
+  return m;
+}
+static mbx_db* g_db = nullptr;
+
+bool SystemDefs::exists(const std::string& dbname) {
+  FILE* f = fopen(dbname.c_str(), "rb");
+  if (f) fclose(f);
+  return f != nullptr;
+}
+
+mbx_db* SystemDefs::open(const std::string& dbname, int num_pgs) {
+  auto& m = open_dbs();
+  auto it = m.find(dbname);
+  if (it != m.end()) return g_db = it->second;
+  mbx_db* db = nullptr;
+  if (exists(dbname))
+    chk<chainexception::ChainException>(mbx_db_open(dbname.c_str(), &db), "DB.openDB " + dbname);
+  else
+    chk<chainexception::ChainException>(mbx_db_create(dbname.c_str(), num_pgs, &db), "DB.openDB " + dbname);
+  m[dbname] = db;
+  return g_db = db;
+}
+
+mbx_db* SystemDefs::db() { return g_db; }
+
 // flushAllPages + close: every device object goes before the context
 void SystemDefs::shutdown() {
   columnar::close_all_files();
+  for (auto& kv : open_dbs()) mbx_db_close(kv.second);
+  open_dbs().clear();
+  g_db = nullptr;
   if (g_ctx) mbx_free(g_ctx);
   g_ctx = nullptr;
 }
@@ -171,17 +201,22 @@ namespace columnar {
 std::string int_key(int v) { return std::to_string(v); }
 
 struct Columnarfile::Impl {
+  mbx_db* db = nullptr;
+  std::string name;
   std::vector<std::string> names;
   std::vector<AttrType> types;
   std::vector<short> sizes;  // attrSizes: 4 or char(n)
-  int64_t nrows = 0;
-  std::vector<std::vector<uint8_t>> host;  // staging image per column
-  std::vector<uint64_t> deleted;
-  bool any_deleted = false;
   mbx_table* table = nullptr;
-  bool dirty = true;
-  std::map<int, std::map<std::string, BitSetPtr>> bitmaps;  // col -> value key -> BitMapFile
+  bool dirty = true;  // the DB file changed since the table was staged
+  std::map<int, std::map<std::string, BitSetPtr>> bitmaps;  // staged BitMapFiles: col -> value key
   BitSetPtr deleted_bm;
+  bool deleted_loaded = false;
+  void invalidate() {
+    bitmaps.clear();
+    deleted_bm.reset();
+    deleted_loaded = false;
+    dirty = true;
+  }
   ~Impl() {
     bitmaps.clear();
     deleted_bm.reset();
@@ -189,8 +224,10 @@ struct Columnarfile::Impl {
   }
 };
 
-static std::map<std::string, std::shared_ptr<Columnarfile::Impl>>& registry() {
-  static std::map<std::string, std::shared_ptr<Columnarfile::Impl>> r;
+// one Impl per (DB, Columnarfile) so every iterator of a session shares the
+// staged table and the staged index BitSets
+static std::map<std::pair<mbx_db*, std::string>, std::shared_ptr<Columnarfile::Impl>>& registry() {
+  static std::map<std::pair<mbx_db*, std::string>, std::shared_ptr<Columnarfile::Impl>> r;
   return r;
 }
 
@@ -199,7 +236,6 @@ void close_all_files() { registry().clear(); }
 DeviceBitSet::~DeviceBitSet() {
   if (b_) mbx_bitmap_free(b_);
 }
-
 int64_t DeviceBitSet::cardinality() const {
   int64_t c = 0;
   mbx_bitmap_info(b_, nullptr, nullptr, &c);
@@ -231,57 +267,117 @@ std::vector<int64_t> DeviceBitSet::positions(int64_t row_offset) const {
   return ids;
 }
 
-Columnarfile::Columnarfile(const std::string& name) : name_(name) {
-  auto it = registry().find(name);
-  if (it == registry().end()) throw chainexception::ChainException("Columnarfile " + name + " does not exist");
-  impl_ = it->second;
+static void load_schema(Columnarfile::Impl& I) {
+  int32_t n = 0;
+  chk<chainexception::ChainException>(mbx_db_columnar_info(I.db, I.name.c_str(), 0, &n, nullptr, nullptr, nullptr,
+                                                           nullptr),
+                                      "Columnar File does not exist.");
+  std::vector<mbx_col_desc> d((size_t)n);
+  std::vector<char> names((size_t)n * (MBX_DB_MAX_ATTR_NAME + 1));
+  chk<chainexception::ChainException>(mbx_db_columnar_info(I.db, I.name.c_str(), n, &n, d.data(), names.data(),
+                                                           nullptr, nullptr),
+                                      "Columnarfile " + I.name);
+  I.names.clear();
+  I.types.clear();
+  I.sizes.clear();
+  for (int32_t j = 0; j < n; j++) {
+    I.names.emplace_back(names.data() + (size_t)j * (MBX_DB_MAX_ATTR_NAME + 1));
+    I.types.emplace_back(d[(size_t)j].attr_type);
+    I.sizes.push_back((short)d[(size_t)j].size);
+  }
 }
 
-Columnarfile::Columnarfile(const std::string& name, int numColumns, const std::vector<std::string>& colNames,
-                           const std::vector<AttrType>& types, const std::vector<short>& sizes)
+static std::shared_ptr<Columnarfile::Impl> find_or_open(mbx_db* db, const std::string& name) {
+  if (!db) throw chainexception::ChainException("Database does not exist.");
+  auto& reg = registry();
+  auto it = reg.find({db, name});
+  if (it != reg.end()) return it->second;
+  auto I = std::make_shared<Columnarfile::Impl>();
+  I->db = db;
+  I->name = name;
+  load_schema(*I);
+  reg[{db, name}] = I;
+  return I;
+}
+
+Columnarfile::Columnarfile(mbx_db* db, const std::string& name) : name_(name) { impl_ = find_or_open(db, name); }
+
+Columnarfile::Columnarfile(mbx_db* db, const std::string& name, int numColumns,
+                           const std::vector<std::string>& colNames, const std::vector<AttrType>& types,
+                           const std::vector<short>& sizes)
     : name_(name) {
   if ((int)colNames.size() != numColumns || (int)types.size() != numColumns || (int)sizes.size() != numColumns)
-    throw chainexception::ChainException("Columnarfile: schema arity mismatch");
-  impl_ = std::make_shared<Impl>();
-  impl_->names = colNames;
-  impl_->types = types;
-  impl_->sizes = sizes;
-  impl_->host.resize((size_t)numColumns);
-  registry()[name] = impl_;
+    throw chainexception::ChainException("Columns Meta Info lengths are not equal to num columns.");
+  int32_t first = -1;
+  chk<chainexception::ChainException>(mbx_db_file_entry(db, (name + ".hdr").c_str(), &first), "get_file_entry");
+  if (first < 0) {
+    std::vector<mbx_col_desc> d((size_t)numColumns);
+    std::vector<const char*> nm((size_t)numColumns);
+    for (int j = 0; j < numColumns; j++) {
+      d[(size_t)j].attr_type = types[(size_t)j].attrType;
+      d[(size_t)j].size = sizes[(size_t)j];
+      nm[(size_t)j] = colNames[(size_t)j].c_str();
+    }
+    chk<chainexception::ChainException>(mbx_db_columnar_create(db, name.c_str(), numColumns, d.data(), nm.data()),
+                                        "Columnarfile " + name);
+  }
+  impl_ = find_or_open(db, name);
+  if ((int)impl_->types.size() != numColumns) throw chainexception::ChainException("Existing file has diff num of cols");
+  for (int j = 0; j < numColumns; j++) {
+    if (impl_->types[(size_t)j].attrType != types[(size_t)j].attrType)
+      throw chainexception::ChainException("Unmatched Type");
+    if (impl_->sizes[(size_t)j] != sizes[(size_t)j]) throw chainexception::ChainException("Unmatched Size");
+    if (impl_->names[(size_t)j] != colNames[(size_t)j]) throw chainexception::ChainException("Unmatched Name");
+  }
 }
 
 void Columnarfile::insertColumns(const std::vector<std::vector<int32_t>>& ints,
                                  const std::vector<std::vector<float>>& reals,
                                  const std::vector<std::vector<std::string>>& strs, int64_t nrows) {
   Impl& I = *impl_;
+  std::vector<std::vector<uint8_t>> host(I.types.size());
+  std::vector<const void*> p(I.types.size());
   size_t ki = 0, kr = 0, ks = 0;
   for (size_t j = 0; j < I.types.size(); j++) {
-    std::vector<uint8_t>& h = I.host[j];
-    const size_t old = h.size();
+    std::vector<uint8_t>& h = host[j];
     if (I.types[j].attrType == AttrType::attrInteger) {
       const auto& v = ints.at(ki++);
-      h.resize(old + (size_t)nrows * 4);
-      memcpy(h.data() + old, v.data(), (size_t)nrows * 4);
+      h.resize((size_t)nrows * 4);
+      memcpy(h.data(), v.data(), (size_t)nrows * 4);
     } else if (I.types[j].attrType == AttrType::attrReal) {
       const auto& v = reals.at(kr++);
-      h.resize(old + (size_t)nrows * 4);
-      memcpy(h.data() + old, v.data(), (size_t)nrows * 4);
+      h.resize((size_t)nrows * 4);
+      memcpy(h.data(), v.data(), (size_t)nrows * 4);
     } else {
       const auto& v = strs.at(ks++);
       const size_t sz = (size_t)I.sizes[j];
-      h.resize(old + (size_t)nrows * sz, 0);
+      h.assign((size_t)nrows * sz, 0);
       for (int64_t r = 0; r < nrows; r++) {
         if (v[(size_t)r].size() > sz) throw chainexception::ChainException("column value exceeds size limit");
-        memcpy(h.data() + old + (size_t)r * sz, v[(size_t)r].data(), v[(size_t)r].size());
+        memcpy(h.data() + (size_t)r * sz, v[(size_t)r].data(), v[(size_t)r].size());
       }
     }
+    p[j] = h.data();
   }
-  I.nrows += nrows;
-  I.deleted.resize((size_t)((I.nrows + 63) / 64), 0);
-  I.dirty = true;
+  chk<chainexception::ChainException>(mbx_db_columnar_insert(I.db, I.name.c_str(), nrows, p.data()),
+                                      "Columnarfile.insertTuple");
+  I.invalidate();
 }
 
-int64_t Columnarfile::getTupleCnt() const { return impl_->nrows; }
+int64_t Columnarfile::getTupleCnt() const {
+  int64_t live = 0;
+  chk<chainexception::ChainException>(mbx_db_columnar_info(impl_->db, impl_->name.c_str(), 0, nullptr, nullptr,
+                                                           nullptr, nullptr, &live),
+                                      "getTupleCnt");
+  return live;
+}
+
+int64_t Columnarfile::positions() const {
+  int64_t n = 0;
+  mbx_table_info(table(), &n, nullptr, nullptr);
+  return n;
+}
+
 int Columnarfile::getFieldCount() const { return (int)impl_->types.size(); }
 std::vector<AttrType> Columnarfile::getAttributeTypes() const { return impl_->types; }
 std::vector<short> Columnarfile::getAttrSizes() const { return impl_->sizes; }
@@ -301,125 +397,96 @@ int Columnarfile::colNameToIndex(const std::string& name) const {
 
 std::string Columnarfile::indexToColName(int idx) const { return impl_->names.at((size_t)idx); }
 
+// the DB file's pages -> HBM, records decoded by the GPU (mbx_db_stage)
 mbx_table* Columnarfile::table() const {
   Impl& I = *impl_;
   if (I.table && !I.dirty) return I.table;
-  mbx_ctx* c = global::SystemDefs::ctx();
   if (I.table) {
-    // cached index bitmaps and the deleted BitSet refer to the old image
-    I.bitmaps.clear();
-    I.deleted_bm.reset();
     mbx_table_free(I.table);
     I.table = nullptr;
   }
-  std::vector<mbx_col_desc> d(I.types.size());
-  std::vector<const void*> p(I.types.size());
-  for (size_t j = 0; j < I.types.size(); j++) {
-    d[j].attr_type = I.types[j].attrType;
-    d[j].size = I.sizes[j];
-    p[j] = I.host[j].data();
-  }
-  chk<chainexception::ChainException>(
-      mbx_table_stage(c, d.data(), (int32_t)d.size(), I.nrows, p.data(), I.any_deleted ? I.deleted.data() : nullptr,
-                      0, &I.table),
-      "Columnarfile " + name_ + ": staging to HBM");
+  chk<chainexception::ChainException>(mbx_db_stage(global::SystemDefs::ctx(), I.db, I.name.c_str(), &I.table),
+                                      "Columnarfile " + name_ + ": staging to HBM");
   I.dirty = false;
   return I.table;
-}
-
-static std::string value_key(const Columnarfile::Impl& I, int col, int64_t row) {
-  const auto& h = I.host[(size_t)col];
-  if (I.types[(size_t)col].attrType == AttrType::attrString) {
-    const size_t sz = (size_t)I.sizes[(size_t)col];
-    const char* s = (const char*)h.data() + (size_t)row * sz;
-    return std::string(s, strnlen(s, sz));
-  }
-  int32_t v;
-  memcpy(&v, h.data() + (size_t)row * 4, 4);
-  return int_key(v);
 }
 
 void Columnarfile::createBitMapIndex(int colNo) {
   Impl& I = *impl_;
   if (colNo < 0 || colNo >= (int)I.types.size()) throw chainexception::ChainException("createBitMapIndex: column");
-  if (I.types[(size_t)colNo].attrType == AttrType::attrReal)
-    throw chainexception::ChainException("createBitMapIndex: attrReal columns are not indexed by the reference");
-  mbx_table* t = table();
-  // the value dictionary (the `.hdr` "col.value" registry): distinct values
-  // of the live rows, in first-seen position order
-  std::vector<std::string> keys;
-  std::set<std::string> seen;
-  for (int64_t r = 0; r < I.nrows; r++) {
-    if (I.any_deleted && ((I.deleted[(size_t)(r >> 6)] >> (r & 63)) & 1ull)) continue;
-    std::string k = value_key(I, colNo, r);
-    if (seen.insert(k).second) keys.push_back(k);
-  }
-  std::vector<mbx_operand> vals(keys.size());
-  for (size_t v = 0; v < keys.size(); v++) {
-    memset(&vals[v], 0, sizeof(mbx_operand));
-    vals[v].type = I.types[(size_t)colNo].attrType;
-    if (vals[v].type == AttrType::attrInteger) vals[v].integer = atoi(keys[v].c_str());
-    else {
-      vals[v].string = keys[v].data();
-      vals[v].string_len = (int32_t)keys[v].size();
-    }
-  }
-  auto& reg = I.bitmaps[colNo];
-  reg.clear();
-  for (size_t v0 = 0; v0 < vals.size(); v0 += 256) {
-    const size_t nv = std::min<size_t>(256, vals.size() - v0);
-    std::vector<mbx_bitmap*> out(nv, nullptr);
-    chk<chainexception::ChainException>(
-        mbx_bitmap_index_build(global::SystemDefs::ctx(), t, colNo, vals.data() + v0, (int32_t)nv, out.data()),
-        "createBitMapIndex");
-    for (size_t v = 0; v < nv; v++) reg[keys[v0 + v]] = std::make_shared<DeviceBitSet>(out[v]);
-  }
+  int32_t n = 0;
+  chk<chainexception::ChainException>(
+      mbx_db_create_bitmap_index(global::SystemDefs::ctx(), I.db, I.name.c_str(), table(), colNo, &n),
+      "createBitMapIndex");
+  I.bitmaps.erase(colNo);
 }
 
-bool Columnarfile::bitmapIndexExists(int colNo) const { return impl_->bitmaps.count(colNo) > 0; }
-
 std::vector<std::string> Columnarfile::getBitmapValues(int colNo) const {
+  int32_t cnt = 0;
+  int64_t bytes = 0;
+  chk<chainexception::ChainException>(
+      mbx_db_bitmap_values(impl_->db, impl_->name.c_str(), colNo, nullptr, 0, &cnt, &bytes), "getBitmapValues");
+  std::vector<char> buf((size_t)bytes + 1, 0);
+  chk<chainexception::ChainException>(
+      mbx_db_bitmap_values(impl_->db, impl_->name.c_str(), colNo, buf.data(), bytes, &cnt, &bytes),
+      "getBitmapValues");
   std::vector<std::string> v;
-  auto it = impl_->bitmaps.find(colNo);
-  if (it != impl_->bitmaps.end())
-    for (const auto& kv : it->second) v.push_back(kv.first);
+  for (size_t k = 0; k < (size_t)bytes;) {
+    v.emplace_back(buf.data() + k);
+    k += v.back().size() + 1;
+  }
   return v;
 }
 
+bool Columnarfile::bitmapIndexExists(int colNo) const { return !getBitmapValues(colNo).empty(); }
+
+// getBitmapIndex (Columnarfile.java:1103-1127): the BitMapFile of the value,
+// staged to HBM once; a value without one reads as an empty BitSet (:1124)
 BitSetPtr Columnarfile::getBitmapIndex(int colNo, const std::string& key) const {
-  auto it = impl_->bitmaps.find(colNo);
-  if (it != impl_->bitmaps.end()) {
-    auto jt = it->second.find(key);
-    if (jt != it->second.end()) return jt->second;
-  }
-  // a value without a BitMapFile reads as an empty BitSet (Columnarfile.java:1124),
-  // made on the device as a CNF with one empty OR-conjunct
+  Impl& I = *impl_;
+  table();  // staging first: a changed DB file drops every staged BitSet
+  auto& staged = I.bitmaps[colNo];
+  auto jt = staged.find(key);
+  if (jt != staged.end()) return jt->second;
+  const int64_t nbits = positions();
+  const std::string file = I.name + ".bm." + std::to_string(colNo) + "." + key;
+  int32_t head = -1;
+  chk<chainexception::ChainException>(mbx_db_file_entry(I.db, file.c_str(), &head), "get_file_entry");
   mbx_bitmap* z = nullptr;
-  int64_t cnt = 0;
-  int32_t offs[2] = {0, 0};
-  chk<chainexception::ChainException>(
-      mbx_bitmap_cnf(global::SystemDefs::ctx(), impl_->nrows, nullptr, offs, 1, nullptr, &z, &cnt), "empty BitSet");
-  return std::make_shared<DeviceBitSet>(z);
+  if (head >= 0) {
+    chk<chainexception::ChainException>(
+        mbx_db_bitmap_stage(global::SystemDefs::ctx(), I.db, file.c_str(), nbits, &z), "BitMapFile " + file);
+  } else {
+    // a CNF with one empty OR-conjunct: the empty BitSet, made on the device
+    int64_t cnt = 0;
+    int32_t offs[2] = {0, 0};
+    chk<chainexception::ChainException>(
+        mbx_bitmap_cnf(global::SystemDefs::ctx(), nbits, nullptr, offs, 1, nullptr, &z, &cnt), "empty BitSet");
+  }
+  auto b = std::make_shared<DeviceBitSet>(z);
+  staged[key] = b;
+  return b;
 }
 
 BitSetPtr Columnarfile::getMarkedDeleted() const {
   Impl& I = *impl_;
-  if (!I.any_deleted) return nullptr;
-  if (!I.deleted_bm) {
+  table();
+  if (!I.deleted_loaded) {
     mbx_bitmap* b = nullptr;
     chk<chainexception::ChainException>(
-        mbx_bitmap_upload(global::SystemDefs::ctx(), I.nrows, I.deleted.data(), &b), "markedDeleted");
-    I.deleted_bm = std::make_shared<DeviceBitSet>(b);
+        mbx_db_bitmap_stage(global::SystemDefs::ctx(), I.db, (I.name + ".md").c_str(), positions(), &b),
+        "markedDeleted");
+    auto bs = std::make_shared<DeviceBitSet>(b);
+    I.deleted_bm = bs->cardinality() > 0 ? bs : nullptr;
+    I.deleted_loaded = true;
   }
   return I.deleted_bm;
 }
 
 void Columnarfile::markTupleDeleted(int64_t position) {
   Impl& I = *impl_;
-  if (position < 0 || position >= I.nrows) throw chainexception::ChainException("markTupleDeleted: position");
-  I.deleted[(size_t)(position >> 6)] |= 1ull << (position & 63);
-  I.any_deleted = true;
-  I.dirty = true;
+  chk<chainexception::ChainException>(mbx_db_mark_deleted(I.db, I.name.c_str(), position), "markTupleDeleted");
+  I.invalidate();
 }
 
 }  // namespace columnar
@@ -535,7 +602,7 @@ static void fill_row(heap::Tuple& J, const std::vector<AttrType>& types, const s
 ColumnarFileScan::ColumnarFileScan(const std::string& file_name, const std::vector<AttrType>& in1,
                                    const std::vector<short>& s1_sizes, short len_in1, int n_out_flds,
                                    const std::vector<FldSpec>& proj_list, CondExpr* const* outFilter)
-    : f_(file_name), in1_(in1), perm_mat_(proj_list) {
+    : f_(global::SystemDefs::db(), file_name), in1_(in1), perm_mat_(proj_list) {
   if ((int)in1.size() != len_in1 || len_in1 != f_.getFieldCount())
     throw FileScanException("ColumnarFileScan: in1/len_in1 do not match " + file_name);
   if ((int)proj_list.size() != n_out_flds) throw FileScanException("ColumnarFileScan: n_out_flds");
@@ -705,7 +772,7 @@ static BitSetPtr or_bitmaps(const columnar::Columnarfile& cf, const std::vector<
   mbx_bitmap* out = nullptr;
   int64_t n = 0;
   BitSetPtr del = cf.getMarkedDeleted();
-  chk<IndexException>(mbx_bitmap_cnf(global::SystemDefs::ctx(), cf.getTupleCnt(), bms.data(), offs.data(),
+  chk<IndexException>(mbx_bitmap_cnf(global::SystemDefs::ctx(), cf.positions(), bms.data(), offs.data(),
                                      (int32_t)conjuncts.size(), del ? del->get() : nullptr, &out, &n),
                       "index BitSet CNF");
   return std::make_shared<columnar::DeviceBitSet>(out);

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/mbx.h"
+#include "../../include/mbx_db.h"
 
 // Everything lives in `minibase::` (the Java packages become nested
 // namespaces; `index` would otherwise collide with POSIX index(3)).
@@ -65,9 +66,16 @@ struct TID {  // R/global/TID.java: numRIDs + position
 };
 // SystemDefs (R/global/SystemDefs.java:6-9): the process-wide engine state;
 // here the GPU context every operator launches on.
+// SystemDefs(dbname, num_pgs, ...) (R/global/SystemDefs.java:19-80): the
+// open Minibase DB file (JavabaseDB) and the GPU context.  open() creates the
+// file with num_pgs pages when it does not exist (BatchInsert passes
+// 1024*1024), else opens it; files stay open until shutdown().
 class SystemDefs {
  public:
   static mbx_ctx* ctx();
+  static mbx_db* open(const std::string& dbname, int num_pgs);
+  static mbx_db* db();  // the DB opened last (JavabaseDB)
+  static bool exists(const std::string& dbname);
   static void shutdown();
 };
 }  // namespace global
@@ -186,17 +194,20 @@ class DeviceBitSet {
 using BitSetPtr = std::shared_ptr<DeviceBitSet>;
 
 // R/columnar/Columnarfile.java: the file's schema + its HBM image.
+// A Columnarfile of a Minibase DB file (include/mbx_db.h); its rows are
+// staged to HBM by the GPU page decoder on first use after a change.
 class Columnarfile {
  public:
-  // open an existing file (:239-359)
-  explicit Columnarfile(const std::string& name);
-  // create (:49-231) from decoded column values; strings as modified UTF-8
-  Columnarfile(const std::string& name, int numColumns, const std::vector<std::string>& colNames,
+  // open an existing file (:194-300)
+  Columnarfile(mbx_db* db, const std::string& name);
+  // create (:60-192), or open it when it exists with the same arity
+  Columnarfile(mbx_db* db, const std::string& name, int numColumns, const std::vector<std::string>& colNames,
                const std::vector<AttrType>& types, const std::vector<short>& sizes);
 
   void insertColumns(const std::vector<std::vector<int32_t>>& ints, const std::vector<std::vector<float>>& reals,
                      const std::vector<std::vector<std::string>>& strs, int64_t nrows);
-  int64_t getTupleCnt() const;
+  int64_t getTupleCnt() const;  // live tuples
+  int64_t positions() const;     // highest position + 1 (bits of every BitSet)
   int getFieldCount() const;
   std::vector<AttrType> getAttributeTypes() const;
   std::vector<short> getStringSizes() const;  // sizes of the string columns, in order
