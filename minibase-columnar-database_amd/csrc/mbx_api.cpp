@@ -1110,13 +1110,13 @@ static int64_t col_bytes(const mbx_table* t, int32_t j) {
   return (int64_t)tc.stride_w * 4;
 }
 
-static int ensure_count(mbx_ctx* c, mbx_bitmap* b) {
+int mbx::ensure_count(mbx_ctx* c, mbx_bitmap* b) {
   if (b->count >= 0) return MBX_OK;
   return bitmap_count_sync(c, b, false);
 }
 
 // device rows (stride) -> caller layout (size bytes, modified UTF-8)
-static void unpack_rows(const TCol& tc, const uint8_t* dev_img, int64_t n, void* host_out) {
+void mbx::unpack_rows(const TCol& tc, const uint8_t* dev_img, int64_t n, void* host_out) {
   if (tc.attr_type != MBX_ATTR_STRING) {
     memcpy(host_out, dev_img, (size_t)n * 4);
     return;

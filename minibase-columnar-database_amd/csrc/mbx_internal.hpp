@@ -187,6 +187,55 @@ struct DistinctArgs {
 hipError_t launch_distinct(const DistinctArgs& A, hipStream_t s);
 hipError_t launch_rows_fetch(const KCol& c, const int64_t* rows, int64_t n, uint32_t* out, hipStream_t s);
 
+// ---- joins (mbx_join.hip, include/mbx_join.h)
+constexpr int kMaxJoinTerms = 16;
+
+struct JoinTerm {
+  int32_t kind;        // ColKind of both columns
+  int32_t op;          // CmpOp; -1: never true (aopNOP / opRANGE)
+  const void* ocol;    // outer column (table-local rows)
+  const void* icol;    // inner column
+  int32_t ostride_w, istride_w;
+  uint32_t conj_bit;
+  int32_t pad_;
+};
+
+struct JoinArgs {
+  JoinTerm terms[kMaxJoinTerms];
+  int32_t nterms;
+  uint32_t all_conj;
+  int32_t mode;                 // 0 BMJ, 1 NLJ
+  int32_t pad_;
+  const int64_t* opos;          // outer selection: table-local rows, ascending
+  int64_t no;
+  const int64_t* ipos;          // inner selection
+  int64_t ni;
+  int64_t block;                // NLJ outer block (tuples per pass)
+  int64_t row0, nrows;          // matrix rows of this launch
+  int64_t words_per_row;
+  uint64_t* out;                // nrows * words_per_row words
+  int32_t* nan;
+};
+
+struct JoinDecode {
+  int32_t mode;
+  int32_t pad_;
+  const int64_t* opos;
+  const int64_t* ipos;
+  int64_t ni, block, row0, words_per_row;
+  int64_t outer_offset, inner_offset;  // tables' row_offset (global positions)
+  int64_t base;                         // output index of the first pair of this chunk
+  int64_t* out_outer;
+  int64_t* out_inner;
+  int32_t* out_pass;
+};
+
+hipError_t launch_join_matrix(const JoinArgs& A, hipStream_t s);
+hipError_t launch_join_decode(const int64_t* ids, const int64_t* n, int64_t max_n, const JoinDecode& D,
+                              hipStream_t s);
+hipError_t launch_gather_pos(const int64_t* pos, int64_t n, int64_t row_offset, const void* col, int32_t stride_w,
+                             void* out, hipStream_t s);
+
 int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block);
 int64_t choose_tiles_per_block(int64_t nrows);
 

@@ -127,6 +127,10 @@ int index_build_encoded(mbx_ctx* c, const mbx_table* t, int32_t col, const uint3
 // host modified UTF-8 (zero padded to len) <-> device string image (stride bytes)
 void encode_device_string(const uint8_t* src, int32_t len, uint8_t* dst, int32_t stride);
 void decode_device_string(const uint8_t* src, int32_t stride, uint8_t* dst, int32_t size);
+// device column image rows -> caller layout (char(n): n bytes modified UTF-8)
+void unpack_rows(const TCol& tc, const uint8_t* dev_img, int64_t n, void* host_out);
+// b->count on the host (one finalize + sync when unknown)
+int ensure_count(mbx_ctx* c, mbx_bitmap* b);
 // recount per-segment popcounts of a bitmap written on the device, sync, and
 // set b->count
 int bitmap_recount(mbx_ctx* c, mbx_bitmap* b);

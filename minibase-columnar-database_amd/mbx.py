@@ -91,7 +91,20 @@ EXPORTS = [
     "mbx_db_columnar_insert", "mbx_db_columnar_info", "mbx_db_mark_deleted", "mbx_db_bitmap_write",
     "mbx_db_bitmap_read", "mbx_db_stage", "mbx_db_allocate_pages", "mbx_db_add_file_entry",
     "mbx_db_create_bitmap_index", "mbx_db_bitmap_values", "mbx_db_bitmap_stage",
+    # include/mbx_join.h
+    "mbx_join", "mbx_join_info", "mbx_join_fetch", "mbx_join_free", "mbx_gather",
 ]
+JOIN_BMJ, JOIN_NLJ = 0, 1
+
+
+class JoinTerm(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("outer_col", ctypes.c_int32), ("inner_col", ctypes.c_int32),
+                ("pad_", ctypes.c_int32)]
+
+
+class JoinCnf(ctypes.Structure):
+    _fields_ = [("terms", ctypes.POINTER(JoinTerm)), ("conj_offsets", ctypes.POINTER(ctypes.c_int32)),
+                ("nconj", ctypes.c_int32)]
 
 _lib = None
 
@@ -160,6 +173,11 @@ def lib():
         "mbx_db_create_bitmap_index": ([V, V, ctypes.c_char_p, V, I32, P(I32)], ctypes.c_int),
         "mbx_db_bitmap_values": ([V, ctypes.c_char_p, I32, V, I64, P(I32), P(I64)], ctypes.c_int),
         "mbx_db_bitmap_stage": ([V, V, ctypes.c_char_p, I64, P(V)], ctypes.c_int),
+        "mbx_join": ([V, V, V, V, V, P(JoinCnf), I32, I64, P(V)], ctypes.c_int),
+        "mbx_join_info": ([V, P(I64), P(I64)], ctypes.c_int),
+        "mbx_join_fetch": ([V, V, I64, I64, V, V, V], ctypes.c_int),
+        "mbx_join_free": ([V], ctypes.c_int),
+        "mbx_gather": ([V, V, V, I64, P(I32), I32, P(V)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -307,6 +325,42 @@ class Context:
         _chk(lib().mbx_table_wrap(self.h, descs, len(col_descs), nrows, ptrs, dev_deleted, row_offset,
                                   ctypes.byref(h)))
         return Table(self, h, nrows, list(col_descs), row_offset, keep=[descs, ptrs])
+
+    def join(self, outer, outer_sel, inner, inner_sel, cnf, order, outer_block=0):
+        """mbx_join: cnf = [[(op, outer_col, inner_col), ...], ...] (0-based
+        columns); returns (outer positions, inner positions, passes) in the
+        reference's order."""
+        terms = [t for conj in cnf for t in conj]
+        tarr = (JoinTerm * max(1, len(terms)))()
+        for k, (op, a, b) in enumerate(terms):
+            tarr[k].op, tarr[k].outer_col, tarr[k].inner_col = op, a, b
+        offs, o = [0], 0
+        for conj in cnf:
+            o += len(conj)
+            offs.append(o)
+        oarr = (ctypes.c_int32 * len(offs))(*offs)
+        c = JoinCnf(tarr, oarr, len(cnf))
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_join(self.h, outer.h, outer_sel.h, inner.h, inner_sel.h, ctypes.byref(c), order, outer_block,
+                            ctypes.byref(h)))
+        try:
+            n, p = ctypes.c_int64(), ctypes.c_int64()
+            _chk(lib().mbx_join_info(h, ctypes.byref(n), ctypes.byref(p)))
+            op_ = np.zeros(max(1, n.value), dtype=np.int64)
+            ip_ = np.zeros(max(1, n.value), dtype=np.int64)
+            ps = np.zeros(max(1, n.value), dtype=np.int32)
+            _chk(lib().mbx_join_fetch(self.h, h, 0, n.value, op_.ctypes.data, ip_.ctypes.data, ps.ctypes.data))
+            return op_[:n.value], ip_[:n.value], ps[:n.value], p.value
+        finally:
+            lib().mbx_join_free(h)
+
+    def gather(self, table, positions, proj):
+        pos = np.ascontiguousarray(positions, dtype=np.int64)
+        outs = [table.empty_column(j, len(pos)) for j in proj]
+        ptrs = (ctypes.c_void_p * max(1, len(outs)))(*[o.ctypes.data for o in outs])
+        pj = (ctypes.c_int32 * max(1, len(proj)))(*proj)
+        _chk(lib().mbx_gather(self.h, table.h, pos.ctypes.data, len(pos), pj, len(proj), ptrs))
+        return outs
 
     def create_bitmap_index(self, db, name, table, col):
         """mbx_db_create_bitmap_index: `index db cf <col> bitmap` on the GPU."""

@@ -53,10 +53,58 @@ def split_cnf(s):
     return conjs
 
 
+STATS = ("Tuple Size: ", "Number of Tuples Buffer Can Hold: ", "Total Outer Tuples By Full Constraint: ",
+         "Total Outer Tuples By Iterator: ")
+
+
+def parse_join(cmd, raw, toks, body, line):
+    """One `nlj` / `bmj` run: header, rows (with the inner-table pass each
+    nlj row was printed in), count, the nlj statistics, or the error."""
+    out = {"cmd": cmd, "raw": raw, "line": line, "rows": [], "passes": [], "stats": {}, "count": None,
+           "error": None, "bitsets": {}}
+    header, cur_pass, k = None, None, 0
+    while k < len(body):
+        b = body[k].rstrip()
+        k += 1
+        if b.startswith("java.lang") or b.startswith("Exception") or "Exception:" in b.split(" ")[0]:
+            out["error"] = b
+            break
+        if not b or b.startswith("****") or b.startswith("Replacer:") or b.startswith("\tat ") or \
+                b.startswith("Size while writing") or b.startswith("Read Page") or b.startswith("Write Page") or \
+                b.startswith("Read Pages") or b.startswith("Wrote Pages") or b.startswith("Pinned Pages"):
+            continue
+        m = re.match(r"Next Pass Over Inner Table: (\d+)", b)
+        if m:
+            cur_pass = int(m.group(1))
+            continue
+        if any(b.startswith(st) for st in STATS):
+            key, val = b.split(": ", 1)
+            out["stats"][key] = int(val)
+            continue
+        m = re.match(r"Total Results Count By Query: (\d+)", b)
+        if m:
+            out["count"] = int(m.group(1))
+            continue
+        if b.startswith("OuterConstraint Bitset") or b.startswith("InnerConstraint Bitset"):
+            nxt = body[k].strip() if k < len(body) else ""
+            out["bitsets"][b.split(" ")[0]] = [int(x) for x in nxt.strip("{}").split(",") if x.strip()]
+            k += 1
+            continue
+        if header is None:
+            header = b
+            continue
+        if out["count"] is None:
+            out["rows"].append(b)
+            out["passes"].append(cur_pass)
+    out["header"] = header
+    return out
+
+
 def main():
     lines = open(REF, encoding="utf-8", errors="replace").read().split("\n")
     bitsets, counts, iq = {}, {}, []
     db_pages = {"column_scan_reads": {}}
+    joins = []
     i = 0
     while i < len(lines):
         ln = lines[i]
@@ -86,7 +134,9 @@ def main():
                     db_pages.setdefault("index_runs", []).append(
                         {"cmd": ln[2:].strip(), "col": toks[3], "kind": toks[4], "wrote": sets["Wrote"][0],
                          "line": sets["Wrote"][1]})
-        elif cmd == "bmj" and len(toks) >= 6 and toks[1] == "db":
+        if cmd in ("nlj", "bmj") and len(toks) >= 7:
+            joins.append(parse_join(cmd, ln[2:].strip(), toks, body, i + 1))
+        if cmd == "bmj" and len(toks) >= 6 and toks[1] == "db":
             outer, inner = split_cnf(toks[4]), split_cnf(toks[5])
             for k, b in enumerate(body):
                 for tag, cnf, raw in (("OuterConstraint", outer, toks[4]), ("InnerConstraint", inner, toks[5])):
@@ -130,6 +180,7 @@ def main():
         "full_constraint_counts": list(counts.values()),
         "indexes_query": iq,
         "db_pages": db_pages,
+        "joins": joins,
     }
     with open(OUT, "w") as f:
         json.dump(out, f, indent=1)
