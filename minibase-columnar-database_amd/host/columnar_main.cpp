@@ -11,6 +11,10 @@
 //                                                              (R/input/Query.java:35-361)
 //   indexes_query DBNAME COLUMNARFILENAME [TARGETCOLS] {(C,OP,V,BM|BT)|..}^{..} NUMBUF
 //                                                              (R/input/MultiIndexQuery.java:30-252)
+//   nlj DBNAME OUTERFILE INNERFILE OUTERCONST INNERCONST JOINCONST OUTERACCESS INNERACCESS
+//       [TARGETCOLUMNS] NUMBUF AMT_OF_MEMORY                   (R/input/NljQuery.java:30-230)
+//   bmj DBNAME OUTERFILE INNERFILE OUTERCONST INNERCONST EQUICONST [TARGETCOLUMNS] NUMBUF
+//                                                              (R/input/BitMapQuery.java:48-300)
 //   exit
 //
 // Output lines (column header, rows, "Total Results Count By Query: n")
@@ -18,12 +22,14 @@
 // Page-I/O counters (PCounter) do not exist here -- there is no buffer pool
 // on the GPU path; the driver prints the device time instead (stderr).
 #include <chrono>
+#include <cstring>
 #include <cstdio>
 #include <fstream>
 #include <iostream>
 #include <set>
 #include <sstream>
 
+#include "../../include/mbx_join.h"
 #include "minibase.hpp"
 
 namespace minibase {
@@ -289,6 +295,296 @@ void indexes_query(const std::vector<std::string>& a) {
   print_rows(scan, cf, t);
 }
 
+// ------------------------------------------------------------------ joins
+
+using Cnf = std::vector<std::vector<std::vector<std::string>>>;  // conjunct -> term -> (a, op, b)
+
+void ok(int rc, const std::string& what) {
+  if (rc < 0) throw std::runtime_error(what + ": " + mbx_last_error());
+}
+
+Cnf parse_cnf(const std::string& s) {
+  Cnf out;
+  for (const std::string& conj : split(s, '^')) {
+    if (conj.size() < 2 || conj.front() != '{' || conj.back() != '}') throw std::runtime_error("Invalid query format");
+    std::vector<std::vector<std::string>> terms;
+    for (const std::string& dis : split(conj.substr(1, conj.size() - 2), '|')) {
+      if (dis.size() < 2 || dis.front() != '(' || dis.back() != ')') throw std::runtime_error("Invalid query format");
+      auto c = split(trim(dis.substr(1, dis.size() - 2)), ',');
+      for (auto& x : c) x = trim(x);
+      if (c.size() != 3) throw std::runtime_error("Invalid VALUECONSTRAINT elements");
+      terms.push_back(c);
+    }
+    out.push_back(terms);
+  }
+  return out;
+}
+
+// CondExpr[] of `column OP literal` terms over conjuncts [from, to) (literals
+// typed from the column; index type per term)
+struct CondArray {
+  std::vector<std::unique_ptr<CondExpr>> pool;
+  std::vector<CondExpr*> heads;
+  std::vector<IndexType> itypes;
+  std::vector<std::string> inames;
+};
+
+CondArray conds(const columnar::Columnarfile& cf, const Cnf& cnf, size_t from, size_t to, int index_type) {
+  CondArray a;
+  for (size_t k = from; k < to; k++) {
+    CondExpr* head = nullptr;
+    CondExpr* tail = nullptr;
+    for (const auto& t : cnf[k]) {
+      a.pool.emplace_back(new CondExpr());
+      CondExpr* e = a.pool.back().get();
+      const int col = cf.colNameToIndex(t[0]);
+      e->op = AttrOperator::findOperator(t[1]);
+      set_literal(cf, col, t[2], *e);
+      e->operand1.symbol = FldSpec(RelSpec(RelSpec::outer), col + 1);
+      e->indexType = IndexType(index_type);
+      a.itypes.push_back(e->indexType);
+      a.inames.push_back(" ");
+      if (!head) head = e;
+      else tail->next = e;
+      tail = e;
+    }
+    a.heads.push_back(head);
+  }
+  a.heads.push_back(nullptr);
+  return a;
+}
+
+// the BitSet a PredEval scan of conjuncts [from, to) selects (ColumnarFileScan)
+columnar::BitSetPtr scan_sel(columnar::Columnarfile& cf, const Cnf& cnf, size_t from, size_t to) {
+  CondArray a = conds(cf, cnf, from, to, IndexType::None);
+  std::vector<FldSpec> proj{FldSpec(RelSpec(RelSpec::outer), 1)};
+  iterator::ColumnarFileScan fs(cf.get_fileName(), cf.getAttributeTypes(), cf.getStringSizes(),
+                                (short)cf.getFieldCount(), 1, proj, a.heads.data());
+  return fs.selection();
+}
+
+// the BitSet a ColumnarIndexScan over conjuncts [from, to) returns
+columnar::BitSetPtr index_sel(columnar::Columnarfile& cf, const Cnf& cnf, size_t from, size_t to, int index_type) {
+  CondArray a = conds(cf, cnf, from, to, index_type);
+  index::ColumnarIndexScan is(&cf, {}, a.itypes, a.inames, cf.getAttributeTypes(), cf.getStringSizes(),
+                              cf.getFieldCount(), 0, {}, {}, a.heads.data(), true);
+  return is.getOutputPositions();
+}
+
+columnar::BitSetPtr and_sel(const columnar::BitSetPtr& x, const columnar::BitSetPtr& y) {
+  mbx_bitmap* b = nullptr;
+  int64_t n = 0;
+  ok(mbx_bitmap_combine(global::SystemDefs::ctx(), MBX_BM_AND, x->get(), y->get(), &b, &n),
+                                      "BitSet.and");
+  return std::make_shared<columnar::DeviceBitSet>(b);
+}
+
+std::string java_bitset(const std::vector<int64_t>& pos) {
+  std::string s = "{";
+  for (size_t k = 0; k < pos.size(); k++) s += (k ? ", " : "") + std::to_string(pos[k]);
+  return s + "}";
+}
+
+struct JoinTargets {
+  std::vector<std::string> names;
+  std::vector<std::pair<int, int>> cols;  // (0 outer / 1 inner, column)
+  std::set<int> outer, inner;             // TreeSet<Integer> of target columns per side
+};
+
+JoinTargets join_targets(const std::string& s, const std::string& outer_name, const columnar::Columnarfile& O,
+                         const columnar::Columnarfile& I) {
+  if (s.size() < 2 || s.front() != '[' || s.back() != ']') throw std::runtime_error("[TARGETCOLUMNNAMES] format invalid.");
+  JoinTargets t;
+  for (auto& n : split(s.substr(1, s.size() - 2), ',')) {
+    const std::string name = trim(n);
+    auto rc = split(name, '.');
+    if (rc.size() != 2) throw std::runtime_error("Column " + name + " does not exist");
+    const bool outer = rc[0] == outer_name;
+    const int col = (outer ? O : I).colNameToIndex(rc[1]);
+    t.names.push_back(name);
+    t.cols.emplace_back(outer ? 0 : 1, col);
+    (outer ? t.outer : t.inner).insert(col);
+  }
+  return t;
+}
+
+std::vector<mbx_join_term> join_terms(const Cnf& jc, const columnar::Columnarfile& O, const columnar::Columnarfile& I,
+                                      std::vector<int32_t>& offs) {
+  std::vector<mbx_join_term> terms;
+  offs.assign(1, 0);
+  for (const auto& conj : jc) {
+    for (const auto& t : conj) {
+      mbx_join_term jt;
+      jt.op = AttrOperator::findOperator(t[1]).attrOperator;
+      jt.outer_col = O.colNameToIndex(t[0]);
+      jt.inner_col = I.colNameToIndex(t[2]);
+      jt.pad_ = 0;
+      if (O.getAttributeTypes()[(size_t)jt.outer_col].attrType != I.getAttributeTypes()[(size_t)jt.inner_col].attrType)
+        throw std::runtime_error("Invalid JOIN COLUMN ATTR TYPE NOT MATCH.");
+      terms.push_back(jt);
+    }
+    offs.push_back((int32_t)terms.size());
+  }
+  return terms;
+}
+
+// run the GPU join and print its rows (per pass for NLJ)
+int64_t join_and_print(columnar::Columnarfile& O, columnar::Columnarfile& I, const columnar::BitSetPtr& osel,
+                       const columnar::BitSetPtr& isel, const Cnf& jc, int32_t order, int64_t block,
+                       const JoinTargets& tg) {
+  std::vector<int32_t> offs;
+  std::vector<mbx_join_term> terms = join_terms(jc, O, I, offs);
+  mbx_join_cnf cnf{terms.data(), offs.data(), (int32_t)jc.size()};
+  mbx_ctx* c = global::SystemDefs::ctx();
+  mbx_join_result* r = nullptr;
+  ok(mbx_join(c, O.table(), osel->get(), I.table(), isel->get(), &cnf, order, block, &r),
+                                      "join");
+  int64_t n = 0, passes = 1;
+  mbx_join_info(r, &n, &passes);
+  std::vector<int64_t> op((size_t)n), ip((size_t)n);
+  std::vector<int32_t> ps((size_t)n);
+  const int rc = mbx_join_fetch(c, r, 0, n, op.data(), ip.data(), ps.data());
+  mbx_join_free(r);
+  ok(rc, "join fetch");
+  // late materialisation of every target column by position (GPU gather)
+  std::vector<std::vector<std::string>> text(tg.cols.size());
+  for (size_t j = 0; j < tg.cols.size(); j++) {
+    columnar::Columnarfile& F = tg.cols[j].first == 0 ? O : I;
+    const std::vector<int64_t>& pos = tg.cols[j].first == 0 ? op : ip;
+    const int col = tg.cols[j].second;
+    const auto at = F.getAttributeTypes()[(size_t)col].attrType;
+    const int w = at == AttrType::attrString ? F.getAttrSizes()[(size_t)col] : 4;
+    std::vector<uint8_t> buf((size_t)std::max<int64_t>(n, 1) * (size_t)w);
+    void* outp = buf.data();
+    int32_t pc = col;
+    ok(mbx_gather(c, F.table(), pos.data(), n, &pc, 1, &outp), "gather");
+    text[j].resize((size_t)n);
+    for (int64_t k = 0; k < n; k++) {
+      const uint8_t* v = buf.data() + (size_t)k * (size_t)w;
+      if (at == AttrType::attrInteger) {
+        int32_t x;
+        memcpy(&x, v, 4);
+        text[j][(size_t)k] = std::to_string(x);
+      } else if (at == AttrType::attrReal) {
+        float x;
+        memcpy(&x, v, 4);
+        text[j][(size_t)k] = std::to_string(x);
+      } else {
+        text[j][(size_t)k] = std::string((const char*)v, strnlen((const char*)v, (size_t)w));
+      }
+    }
+  }
+  auto pass_header = [](int64_t p) {
+    std::cout << "\n************************************************************************\n"
+              << "Next Pass Over Inner Table: " << p << "\n"
+              << "************************************************************************\n\n";
+  };
+  int64_t k = 0;
+  for (int64_t p = 0; p < passes; p++) {
+    if (order == MBX_JOIN_NLJ && p > 0) pass_header(p);
+    if (p == 0) {
+      for (size_t j = 0; j < tg.names.size(); j++) std::cout << (j ? ", " : "") << tg.names[j];
+      std::cout << "\n";
+    }
+    for (; k < n && (order != MBX_JOIN_NLJ || ps[(size_t)k] == p); k++) {
+      std::string line;
+      for (size_t j = 0; j < text.size(); j++) line += (j ? ", " : "") + text[j][(size_t)k];
+      std::cout << line << "\n";
+    }
+  }
+  return n;
+}
+
+void nlj_cmd(const std::vector<std::string>& a) {
+  if (a.size() < 12) throw std::runtime_error("Invalid number of attributes.");
+  if (!global::SystemDefs::exists(a[1])) throw std::runtime_error("Database does not exist.");
+  int numbuf = 0, amt = 0;
+  try {
+    numbuf = std::stoi(a[10]);
+  } catch (...) {
+    throw std::runtime_error("NUMBUF is not integer.");
+  }
+  if (numbuf < 1) throw std::runtime_error("NUMBUF is not integer.");
+  try {
+    amt = std::stoi(a[11]);
+  } catch (...) {
+    throw std::runtime_error("amt_of_memory is not integer.");
+  }
+  if (amt < 2) throw std::runtime_error("amt_of_memory is not integer.");
+  mbx_db* db = global::SystemDefs::open(a[1], 0);
+  columnar::Columnarfile O(db, a[2]), I(db, a[3]);
+  const std::string oacc = a[7], iacc = a[8];
+  auto valid = [](std::string x) {
+    for (auto& ch : x) ch = (char)toupper((unsigned char)ch);
+    return x == "FILESCAN" || x == "COLUMNSCAN" || x == "BTREE" || x == "BITMAP" ? x : std::string();
+  };
+  const std::string OA = valid(oacc), IA = valid(iacc);
+  if (OA.empty()) throw std::runtime_error("outerAccessType invalid.");
+  if (IA.empty()) throw std::runtime_error("innerAccessType invalid.");
+  JoinTargets tg = join_targets(a[9], a[2], O, I);
+  const Cnf oc = parse_cnf(a[4]), ic = parse_cnf(a[5]), jc = parse_cnf(a[6]);
+  // findConsTargetCols / findJoinTargetCols (NljQuery.java:406-470)
+  if (OA != "FILESCAN")
+    for (size_t k = 1; k < oc.size(); k++)
+      for (const auto& t : oc[k]) tg.outer.insert(O.colNameToIndex(t[0]));
+  if (IA != "FILESCAN")
+    for (size_t k = 1; k < ic.size(); k++)
+      for (const auto& t : ic[k]) tg.inner.insert(I.colNameToIndex(t[0]));
+  for (const auto& conj : jc)
+    for (const auto& t : conj) {
+      tg.outer.insert(O.colNameToIndex(t[0]));
+      tg.inner.insert(I.colNameToIndex(t[2]));
+    }
+  // access path selection + pending filter (getIterator, NljQuery.java:232-300;
+  // fillOuterBuffer / fillInnerBuffer, ColumnarNestedLoopJoins.java:120-158)
+  auto select = [](columnar::Columnarfile& F, const Cnf& cnf, const std::string& acc, columnar::BitSetPtr* it) {
+    if (acc == "FILESCAN") {
+      *it = scan_sel(F, cnf, 0, cnf.size());
+      return *it;
+    }
+    *it = acc == "COLUMNSCAN" ? scan_sel(F, cnf, 0, 1)
+                              : index_sel(F, cnf, 0, 1, acc == "BTREE" ? IndexType::B_Index : IndexType::Bitmap);
+    return cnf.size() > 1 ? and_sel(*it, scan_sel(F, cnf, 1, cnf.size())) : *it;
+  };
+  columnar::BitSetPtr o_iter, i_iter;
+  columnar::BitSetPtr osel = select(O, oc, OA, &o_iter);
+  columnar::BitSetPtr isel = select(I, ic, IA, &i_iter);
+  // the outer iterator's tuple (Tuple.setHdr over the TreeSet of outer
+  // target columns) sizes the outer block (ColumnarNestedLoopJoins.java:122)
+  int tsize = ((int)tg.outer.size() + 2) * 2;
+  for (int col : tg.outer)
+    tsize += O.getAttributeTypes()[(size_t)col].attrType == AttrType::attrString ? O.getAttrSizes()[(size_t)col] + 2 : 4;
+  const int64_t block = (int64_t)(amt - 1) * (1024 / tsize);
+  std::cout << "\n************************************************************************\n"
+            << "Next Pass Over Inner Table: 0\n"
+            << "************************************************************************\n\n";
+  const int64_t n = join_and_print(O, I, osel, isel, jc, MBX_JOIN_NLJ, block, tg);
+  std::cout << "\n************************************************************************\n"
+            << "Tuple Size: " << tsize << "\n"
+            << "Number of Tuples Buffer Can Hold: " << block << "\n"
+            << "Total Outer Tuples By Full Constraint: " << osel->cardinality() << "\n"
+            << "Total Outer Tuples By Iterator: " << o_iter->cardinality() << "\n"
+            << "************************************************************************\n\n";
+  print_results_footer(n);
+}
+
+void bmj_cmd(const std::vector<std::string>& a) {
+  if (a.size() < 9) throw std::runtime_error("Invalid number of attributes.");
+  if (!global::SystemDefs::exists(a[1])) throw std::runtime_error("Database does not exist.");
+  (void)std::stoi(a[8]);  // bufferSize
+  mbx_db* db = global::SystemDefs::open(a[1], 0);
+  columnar::Columnarfile O(db, a[2]), I(db, a[3]);
+  // getConstraintBitset: ColumnarIndexScan over bitmap indexes (BitMapQuery.java:300-330)
+  const Cnf oc = parse_cnf(a[4]), ic = parse_cnf(a[5]), jc = parse_cnf(a[6]);
+  columnar::BitSetPtr osel = index_sel(O, oc, 0, oc.size(), IndexType::Bitmap);
+  std::cout << "OuterConstraint Bitset After performing AND and ORs\n" << java_bitset(osel->positions()) << "\n";
+  columnar::BitSetPtr isel = index_sel(I, ic, 0, ic.size(), IndexType::Bitmap);
+  std::cout << "InnerConstraint Bitset After performing AND and ORs\n" << java_bitset(isel->positions()) << "\n";
+  JoinTargets tg = join_targets(a[7], a[2], O, I);
+  const int64_t n = join_and_print(O, I, osel, isel, jc, MBX_JOIN_BMJ, 0, tg);
+  print_results_footer(n);
+}
+
 }  // namespace
 
 int run() {
@@ -308,6 +604,8 @@ int run() {
       else if (a[0] == "index") index_cmd(a);
       else if (a[0] == "query") query(a);
       else if (a[0] == "indexes_query") indexes_query(a);
+      else if (a[0] == "nlj") nlj_cmd(a);
+      else if (a[0] == "bmj") bmj_cmd(a);
       else if (a[0] == "exit") break;
       else std::cout << "Command not supported by the GPU executor: " << a[0] << "\n";
     } catch (const std::exception& e) {

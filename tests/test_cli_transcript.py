@@ -118,3 +118,35 @@ def test_db_file_persists_across_processes(tmp_path):
     assert second[0][2] == GOLD["indexes_query"][0]["count"] and second[1][2] == 57 and second[2][2] == 57
     out = run_session(["query nodb cf [A] {C,=,6} 100 FILESCAN"], cwd=str(tmp_path), setup=False)
     assert "Database does not exist." in out
+
+
+def test_join_commands_replay_transcript(tmp_path):
+    """Every successful `nlj` / `bmj` run of the reference session
+    (R/phase3_output), replayed through the driver over cf, cf1, cf2 (all
+    `batchinsert minidata.txt`, bitmap indexes on every column): same rows in
+    the same order, same inner-table passes, same statistics (bar the
+    "Tuple Size: 10" runs an earlier ColumnarColumnsScan printed), same BitSets."""
+    import sys
+    sys.path.insert(0, os.path.join(helpers.ROOT, "tests", "golden"))
+    import make_golden
+    runs = [j for j in GOLD["joins"] if j["error"] is None and j["count"] is not None]
+    setup = [f"batchinsert {DATA} db {cf} 4" for cf in ("cf", "cf1", "cf2")]
+    setup += [f"index db {cf} {c} bitmap" for cf in ("cf", "cf1", "cf2") for c in "ABCD"]
+    out = run_session(setup + [r["raw"] for r in runs], cwd=str(tmp_path), setup=False)
+    chunks = out.split("> ")[1:]
+    assert len(chunks) >= len(setup) + len(runs)
+    for r, chunk in zip(runs, chunks[len(setup):]):
+        body = chunk.split("\n")
+        got = make_golden.parse_join(r["cmd"], r["raw"], r["raw"].split(), body, r["line"])
+        assert got["error"] is None, (r["raw"], chunk[:500])
+        assert got["header"] == r["header"], r["raw"]
+        assert got["rows"] == r["rows"], r["raw"]
+        assert got["count"] == r["count"]
+        if r["cmd"] == "nlj":
+            assert got["passes"] == r["passes"], r["raw"]
+            for k, v in r["stats"].items():
+                if r["stats"]["Tuple Size"] == 10 and k in ("Tuple Size", "Number of Tuples Buffer Can Hold"):
+                    continue
+                assert got["stats"][k] == v, (r["raw"], k)
+        else:
+            assert got["bitsets"] == r["bitsets"], r["raw"]
