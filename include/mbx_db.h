@@ -100,6 +100,20 @@ int mbx_db_columnar_info(mbx_db* db, const char* name, int32_t max_cols, int32_t
  * the position in cf.md and appends the TID record to cf.dtid. */
 int mbx_db_mark_deleted(mbx_db* db, const char* name, int64_t position);
 
+/* markTupleDeleted for n positions in order (one header read for the batch:
+ * DeleteQuery marks every position its scan returns, R/input/DeleteQuery.java:105-180). */
+int mbx_db_mark_deleted_many(mbx_db* db, const char* name, const int64_t* positions, int64_t n);
+
+/* Columnarfile.purgeAllDeletedTuples (R/columnar/Columnarfile.java:837-925):
+ * removes the record of every cf.dtid TID from every column heapfile
+ * (HFPage compaction; emptied data pages freed, emptied directory pages
+ * unlinked and freed -- which shifts the positions after them), clears the
+ * deleted positions from every bitmap index and drops the shifted position
+ * ranges (BitMapFile.purgeDelete), clears cf.md and recreates cf.dtid.
+ * Positions of the surviving rows are otherwise unchanged (holes stay holes,
+ * mbx_db_stage marks them deleted).  Not for files with B+-tree indexes. */
+int mbx_db_purge(mbx_db* db, const char* name);
+
 /* BitMapFile images (R/bitmap/BitMapFile.java:60-120, R/bitmap/BM.java:60-215).
  * write: creates `filename` (BMHEAD header page + one 1000-byte chunk page per
  * 8000 bits of BitSet.toByteArray(); MBX_E_INVALID if it exists or the

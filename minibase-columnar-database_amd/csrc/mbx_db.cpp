@@ -1281,3 +1281,332 @@ extern "C" int mbx_db_bitmap_stage(mbx_ctx* c, mbx_db* db, const char* filename,
   if (nbits & 63) words[(size_t)nw - 1] &= (1ull << (nbits & 63)) - 1ull;
   return mbx_bitmap_upload(c, nbits, words.data(), out);
 }
+
+// ------------------------------------------------------ delete lifecycle
+
+namespace {
+
+void free_page(mbx_db* db, int32_t pid) {
+  set_page_bit(db, pid, false);
+  if (pid < db->alloc_hint) db->alloc_hint = pid;
+}
+
+// HFPage.deleteRecord (R/heap/HFPage.java:398-450): close the hole by
+// shifting the records below it up, fix their offsets, empty the slot
+int hf_delete(uint8_t* pg, int32_t slot) {
+  const int32_t cnt = get16(pg + kSlotCnt);
+  const int32_t len = slot >= 0 && slot < cnt ? hf_slot_len(pg, slot) : -1;
+  if (len <= 0) return fail(MBX_E_INVALID, "InvalidSlotNumberException: HEAPFILE: INVALID_SLOTNO");
+  const int32_t off = hf_slot_off(pg, slot);
+  const int32_t used = get16(pg + kUsedPtr);
+  memmove(pg + used + len, pg + used, (size_t)(off - used));
+  for (int32_t i = 0; i < cnt; ++i) {
+    if (hf_slot_len(pg, i) >= 0) {
+      const int32_t o = hf_slot_off(pg, i);
+      if (o < off) put16(pg + kDpFixed + i * kSlotSize + 2, o + len);
+    }
+  }
+  put16(pg + kUsedPtr, used + len);
+  put16(pg + kFreeSpace, get16(pg + kFreeSpace) + len);
+  put16(pg + kDpFixed + slot * kSlotSize, -1);
+  put16(pg + kDpFixed + slot * kSlotSize + 2, 0);
+  return MBX_OK;
+}
+
+bool hf_empty(const uint8_t* pg) {
+  const int32_t cnt = get16(pg + kSlotCnt);
+  for (int32_t i = 0; i < cnt; ++i)
+    if (hf_slot_len(pg, i) != -1) return false;
+  return true;
+}
+
+// directory page -> its index in the chain (Heapfile.loadPositionBuffer's dirPageOffset)
+std::unordered_map<int32_t, int32_t> dir_offsets(mbx_db* db, int32_t first_dir) {
+  std::unordered_map<int32_t, int32_t> m;
+  int32_t d = first_dir, k = 0;
+  while (d != kInvalidPage && k <= db->num_pages) {
+    m[d] = k++;
+    d = get32(db->page(d) + kNext);
+  }
+  return m;
+}
+
+// Heapfile.deleteRecord (R/heap/Heapfile.java:523-600)
+int heap_delete(mbx_db* db, int32_t first_dir, int32_t pid, int32_t slot,
+                const std::unordered_map<int32_t, int32_t>& offsets, std::vector<int32_t>* freed_dir) {
+  int32_t dir = first_dir, dslot = -1;
+  for (int guard = 0; dir != kInvalidPage && guard <= db->num_pages; ++guard) {
+    const uint8_t* dp = db->page(dir);
+    const int32_t cnt = get16(dp + kSlotCnt);
+    for (int32_t s = 0; s < cnt && dslot < 0; ++s)
+      if (hf_slot_len(dp, s) != -1 && get32(dp + hf_slot_off(dp, s) + 4) == pid) dslot = s;
+    if (dslot >= 0) break;
+    dir = get32(dp + kNext);
+  }
+  if (dslot < 0) return fail(MBX_E_INVALID, "Heapfile.deleteRecord: record (%d, %d) not found", pid, slot);
+  uint8_t* dp = db->page(dir);
+  uint8_t* info = dp + hf_slot_off(dp, dslot);
+  uint8_t* pg = db->page(pid);
+  int rc = hf_delete(pg, slot);
+  if (rc) return rc;
+  const int32_t recct = get16(info + 2) - 1;
+  put16(info + 2, recct);
+  db->hints.erase(first_dir);
+  if (recct >= 1) {
+    put16(info, hf_available(pg));
+    return MBX_OK;
+  }
+  free_page(db, pid);
+  if ((rc = hf_delete(dp, dslot))) return rc;
+  const int32_t prev = get32(dp + kPrev);
+  if (hf_empty(dp) && prev != kInvalidPage) {
+    const int32_t next = get32(dp + kNext);
+    put32(db->page(prev) + kNext, next);
+    if (next != kInvalidPage) put32(db->page(next) + kPrev, prev);
+    auto it = offsets.find(dir);
+    if (it != offsets.end()) freed_dir->push_back(it->second);
+    free_page(db, dir);
+  }
+  return MBX_OK;
+}
+
+// a BitMapFile in memory: the BitSet bytes + the chain of its pages
+struct BmFile {
+  int32_t head = kInvalidPage;
+  std::vector<int32_t> pages;  // offsetToPage
+  std::vector<uint8_t> bytes;
+};
+
+int bm_load(mbx_db* db, const std::string& name, BmFile* f) {
+  f->head = get_file_entry(db, name);
+  if (f->head == kInvalidPage) return fail(MBX_E_INVALID, "The file %s does not exist.", name.c_str());
+  int rc = bm_read_bytes(db, f->head, &f->bytes);
+  if (rc) return rc;
+  f->pages.clear();
+  for (int32_t p = f->head; p != kInvalidPage; p = get32(db->page(p) + kNext)) f->pages.push_back(p);
+  return MBX_OK;
+}
+
+bool bm_get(const BmFile& f, int64_t pos) {
+  return (size_t)(pos >> 3) < f.bytes.size() && ((f.bytes[(size_t)(pos >> 3)] >> (pos & 7)) & 1);
+}
+
+int64_t bm_next_set(const BmFile& f, int64_t from) {
+  for (int64_t p = from; p < (int64_t)f.bytes.size() * 8; ++p)
+    if (bm_get(f, p)) return p;
+  return -1;
+}
+
+// rewrite chunk `k` (1000 bytes) of the in-memory BitSet into its page's record
+void bm_write_chunk(mbx_db* db, const BmFile& f, int64_t k) {
+  uint8_t* pg = db->page(f.pages[(size_t)k]);
+  const int32_t cnt = get16(pg + kSlotCnt);
+  int32_t s = 0;
+  while (s < cnt && hf_slot_len(pg, s) == -1) ++s;
+  if (s == cnt) return;
+  uint8_t* rec = pg + hf_slot_off(pg, s);
+  const int32_t len = hf_slot_len(pg, s);
+  // BitSet.toByteArray() stops at the last non-zero byte
+  int64_t nb = (int64_t)f.bytes.size();
+  while (nb > 0 && f.bytes[(size_t)nb - 1] == 0) --nb;
+  memset(rec, 0, (size_t)len);
+  const int64_t start = k * kBmRecord;
+  if (start < nb) memcpy(rec, f.bytes.data() + start, (size_t)std::min<int64_t>(len, nb - start));
+}
+
+// BitMapFile.delete(position) (R/bitmap/BitMapFile.java:245-290)
+void bm_delete(mbx_db* db, BmFile& f, int64_t pos) {
+  if (!bm_get(f, pos)) return;
+  f.bytes[(size_t)(pos >> 3)] &= (uint8_t)~(1u << (pos & 7));
+  const int64_t chunk = (int64_t)kBmRecord * 8;
+  const int64_t offset = pos / chunk;
+  if (bm_next_set(f, offset * chunk) == -1 && offset != 0) {
+    int64_t cur = offset;
+    while (bm_next_set(f, cur * chunk) == -1 && cur != 0) {
+      if ((size_t)cur < f.pages.size()) {
+        free_page(db, f.pages[(size_t)cur]);
+        f.pages.resize((size_t)cur);
+      }
+      --cur;
+    }
+    put32(db->page(f.pages[(size_t)cur]) + kNext, kInvalidPage);
+    return;
+  }
+  if ((size_t)offset < f.pages.size()) bm_write_chunk(db, f, offset);
+}
+
+// BitMapFile.purgeDelete (R/bitmap/BitMapFile.java:320-365) + BM.updateBitSet (R/bitmap/BM.java:216-290)
+void bm_purge(mbx_db* db, BmFile& f, const std::vector<int64_t>& list, const std::vector<int64_t>& ranges) {
+  if (ranges.empty()) {
+    for (int64_t p : list) bm_delete(db, f, p);
+    return;
+  }
+  for (int64_t p : list)
+    if (bm_get(f, p)) f.bytes[(size_t)(p >> 3)] &= (uint8_t)~(1u << (p & 7));
+  int64_t length = 0;  // BitSet.length(): highest set bit + 1
+  for (int64_t b = (int64_t)f.bytes.size() - 1; b >= 0 && !length; --b)
+    if (f.bytes[(size_t)b]) length = b * 8 + (32 - __builtin_clz((unsigned)f.bytes[(size_t)b]));
+  std::vector<uint8_t> out(f.bytes.size(), 0);
+  int64_t position = 0, start = 0;
+  auto copy = [&](int64_t from, int64_t to) {
+    for (int64_t j = from; j < to; ++j, ++position)
+      if (bm_get(f, j)) out[(size_t)(position >> 3)] |= (uint8_t)(1u << (position & 7));
+  };
+  for (size_t i = 0; i + 1 < ranges.size(); i += 2) {
+    copy(start, ranges[i]);
+    start = ranges[i + 1];
+  }
+  copy(start, length);
+  int64_t nb = (int64_t)out.size();
+  while (nb > 0 && out[(size_t)nb - 1] == 0) --nb;
+  if (nb == 0) return;  // BM.updateBitSet throws on an empty BitSet: the file keeps its old image
+  f.bytes.assign(out.begin(), out.begin() + nb);
+  const int64_t nchunks = (nb + kBmRecord - 1) / kBmRecord;
+  for (int64_t k = 0; k < nchunks && (size_t)k < f.pages.size(); ++k) bm_write_chunk(db, f, k);
+  for (size_t k = (size_t)nchunks; k < f.pages.size(); ++k) free_page(db, f.pages[k]);
+  if ((size_t)nchunks < f.pages.size()) f.pages.resize((size_t)nchunks);
+  put32(db->page(f.pages.back()) + kNext, kInvalidPage);
+}
+
+// DB.delete_file_entry (R/diskmgr/DB.java:510-560): pid -1, name "\0"
+void delete_file_entry(mbx_db* db, const std::string& name) {
+  for (int32_t hp = 0; hp != kInvalidPage;) {
+    uint8_t* pg = db->page(hp);
+    const int32_t n = get32(pg + 4);
+    for (int32_t e = 0; e < n; ++e) {
+      uint8_t* ent = pg + kStartEntries + e * kFileEntry;
+      if (get32(ent) != kInvalidPage && get_utf(ent + 4, kMaxName + 2) == name) {
+        put32(ent, kInvalidPage);
+        put_utf(ent + 4, std::string("\xC0\x80", 2));  // writeUTF("\0")
+        return;
+      }
+    }
+    hp = get32(pg);
+  }
+}
+
+// Heapfile.deleteFile (R/heap/Heapfile.java:1148-1204)
+void heap_delete_file(mbx_db* db, const std::string& name) {
+  const int32_t first = get_file_entry(db, name);
+  if (first == kInvalidPage) return;
+  for (int32_t d = first; d != kInvalidPage;) {
+    const uint8_t* dp = db->page(d);
+    const int32_t cnt = get16(dp + kSlotCnt);
+    for (int32_t s = 0; s < cnt; ++s)
+      if (hf_slot_len(dp, s) != -1) free_page(db, get32(dp + hf_slot_off(dp, s) + 4));
+    const int32_t next = get32(dp + kNext);
+    free_page(db, d);
+    d = next;
+  }
+  db->hints.erase(first);
+  delete_file_entry(db, name);
+}
+
+}  // namespace
+
+extern "C" int mbx_db_mark_deleted_many(mbx_db* db, const char* name, const int64_t* positions, int64_t n) {
+  NOTNULL(db);
+  NOTNULL(name);
+  if (n < 0) return fail(MBX_E_INVALID, "mark_deleted: n %lld", (long long)n);
+  if (n == 0) return MBX_OK;
+  NOTNULL(positions);
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  std::vector<ColumnPages> cps((size_t)sc.ncols);
+  for (int32_t i = 0; i < sc.ncols; ++i)
+    if ((rc = column_pages(db, std::string(name) + "." + std::to_string(i), record_len(sc.cols[(size_t)i]),
+                           &cps[(size_t)i])))
+      return rc;
+  const int32_t md = get_file_entry(db, std::string(name) + ".md");
+  if (md == kInvalidPage) return fail(MBX_E_INVALID, "%s.md is missing", name);
+  int32_t dtid;
+  if ((rc = heap_open(db, std::string(name) + ".dtid", true, &dtid))) return rc;
+  std::vector<uint8_t> tid((size_t)sc.ncols * 8);
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t position = positions[k];
+    if (position < 0) return fail(MBX_E_INVALID, "Invalid position");
+    for (int32_t i = 0; i < sc.ncols; ++i) {
+      const ColumnPages& cp = cps[(size_t)i];
+      const int64_t pi = position / cp.recs_per_page;
+      if (pi >= (int64_t)cp.page_of.size() || cp.page_of[(size_t)pi] == kInvalidPage)
+        return fail(MBX_E_INVALID, "Invalid Position %lld", (long long)position);
+      put32(tid.data() + 8 * i, (int32_t)(position - pi * cp.recs_per_page));  // RID.writeToByteArray: slotNo
+      put32(tid.data() + 8 * i + 4, cp.page_of[(size_t)pi]);                  // then pageNo
+    }
+    if ((rc = bm_set_bit(db, md, position))) return rc;
+    int32_t pid, slot;
+    if ((rc = heap_insert(db, dtid, tid.data(), (int32_t)tid.size(), &pid, &slot))) return rc;
+  }
+  return MBX_OK;
+}
+
+extern "C" int mbx_db_purge(mbx_db* db, const char* name) {
+  NOTNULL(db);
+  NOTNULL(name);
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  const std::string cf = name;
+  for (uint8_t b : sc.btree_exist)
+    if (b == 1) return fail(MBX_E_UNSUPPORTED, "purge of %s: B-tree indexes are out of scope", name);
+  std::vector<int32_t> heaps((size_t)sc.ncols);
+  std::vector<std::unordered_map<int32_t, int32_t>> offsets((size_t)sc.ncols);
+  std::vector<std::vector<int32_t>> freed((size_t)sc.ncols);
+  for (int32_t i = 0; i < sc.ncols; ++i) {
+    heaps[(size_t)i] = get_file_entry(db, cf + "." + std::to_string(i));
+    if (heaps[(size_t)i] == kInvalidPage) return fail(MBX_E_INVALID, "%s.%d is missing", name, i);
+    offsets[(size_t)i] = dir_offsets(db, heaps[(size_t)i]);
+  }
+  // 1. every TID of cf.dtid: delete its record from every column heapfile
+  const int32_t dtid = get_file_entry(db, cf + ".dtid");
+  std::vector<std::vector<uint8_t>> tids;
+  if (dtid != kInvalidPage && (rc = heap_scan(db, dtid, [&](const DataPage&, int32_t, const uint8_t* r, int32_t len) {
+        tids.emplace_back(r, r + len);
+        return true;
+      })))
+    return rc;
+  for (const auto& t : tids) {
+    if ((int64_t)t.size() < 8LL * sc.ncols) return fail(MBX_E_INVALID, "%s.dtid: short TID record", name);
+    for (int32_t i = 0; i < sc.ncols; ++i)
+      if ((rc = heap_delete(db, heaps[(size_t)i], get32(t.data() + 8 * i + 4), get32(t.data() + 8 * i),
+                            offsets[(size_t)i], &freed[(size_t)i])))
+        return rc;
+  }
+  // 2. the deleted positions (markedDeleted, ascending)
+  BmFile md;
+  if ((rc = bm_load(db, cf + ".md", &md))) return rc;
+  std::vector<int64_t> list;
+  for (int64_t p = bm_next_set(md, 0); p != -1; p = bm_next_set(md, p + 1)) list.push_back(p);
+  // 3. every bitmap index: clear them, drop the position ranges of removed
+  //    directory pages (values in HashSet iteration order)
+  for (int32_t i = 0; i < sc.ncols; ++i) {
+    std::vector<int32_t> offs = freed[(size_t)i];
+    std::sort(offs.begin(), offs.end());
+    const int64_t per_dir = (int64_t)kRecsPerDirPage * recs_per_data_page(record_len(sc.cols[(size_t)i]));
+    std::vector<int64_t> ranges;
+    for (int32_t o : offs) {
+      ranges.push_back((int64_t)o * per_dir);
+      ranges.push_back((int64_t)(o + 1) * per_dir);
+    }
+    const std::string prefix = std::to_string(i) + ".";
+    std::vector<std::string> vals;
+    std::vector<int32_t> hashes;
+    for (const std::string& r : sc.bm_values) {
+      if (r.compare(0, prefix.size(), prefix) != 0) continue;
+      vals.push_back(r.substr(prefix.size()));
+      hashes.push_back(sc.cols[(size_t)i].attr_type == MBX_ATTR_STRING ? java_string_hash(vals.back())
+                                                                      : (int32_t)atoi(vals.back().c_str()));
+    }
+    for (size_t k : hashmap_order(hashes)) {
+      BmFile f;
+      if (bm_load(db, cf + ".bm." + prefix + vals[k], &f)) continue;  // registered without a file
+      bm_purge(db, f, list, ranges);
+    }
+  }
+  // 4. markedDeleted.delete(position) for each; 5. a fresh cf.dtid
+  for (int64_t p : list) bm_delete(db, md, p);
+  heap_delete_file(db, cf + ".dtid");
+  int32_t fresh;
+  return heap_open(db, cf + ".dtid", true, &fresh);
+}

@@ -15,6 +15,8 @@
 //       [TARGETCOLUMNS] NUMBUF AMT_OF_MEMORY                   (R/input/NljQuery.java:30-230)
 //   bmj DBNAME OUTERFILE INNERFILE OUTERCONST INNERCONST EQUICONST [TARGETCOLUMNS] NUMBUF
 //                                                              (R/input/BitMapQuery.java:48-300)
+//   delete_query DBNAME COLUMNARFILENAME {C,OP,V} NUMBUF ACCESS md|pd
+//                                                              (R/input/DeleteQuery.java:28-215)
 //   exit
 //
 // Output lines (column header, rows, "Total Results Count By Query: n")
@@ -495,6 +497,52 @@ int64_t join_and_print(columnar::Columnarfile& O, columnar::Columnarfile& I, con
   return n;
 }
 
+// delete_query DB CF {C,OP,V} NUMBUF FILESCAN|COLUMNSCAN|BITMAP md|pd
+// (R/input/DeleteQuery.java:28-215): the scan picks the live positions on the
+// GPU, each one is marked deleted (cf.md + cf.dtid); `pd` then purges.
+void delete_query(const std::vector<std::string>& a) {
+  if (a.size() < 7) throw std::runtime_error("Invalid number of attributes.");
+  if (!global::SystemDefs::exists(a[1])) throw std::runtime_error("Database does not exist.");
+  const std::string& cons = a[3];
+  if (cons.size() < 2 || cons.front() != '{' || cons.back() != '}') throw std::runtime_error("VALUECONSTRAINT format invalid.");
+  int numbuf = 0;
+  try {
+    numbuf = std::stoi(a[4]);
+  } catch (...) {
+    throw std::runtime_error("NUMBUF is not integer.");
+  }
+  if (numbuf < 1) throw std::runtime_error("NUMBUF is not integer.");
+  std::string acc = a[5], kind = a[6];
+  for (auto& ch : acc) ch = (char)toupper((unsigned char)ch);
+  for (auto& ch : kind) ch = (char)tolower((unsigned char)ch);
+  if (acc != "FILESCAN" && acc != "COLUMNSCAN" && acc != "BTREE" && acc != "BITMAP")
+    throw std::runtime_error("access type invalid.");
+  if (kind != "md" && kind != "pd") throw std::runtime_error("delete type invalid.");
+  mbx_db* db = global::SystemDefs::open(a[1], 0);
+  columnar::Columnarfile cf(db, a[2]);
+  auto parts = split(trim(cons.substr(1, cons.size() - 2)), ',');
+  for (auto& x : parts) x = trim(x);
+  if (parts.size() != 3) throw std::runtime_error("Invalid VALUECONSTRAINT elements");
+  const int col = cf.colNameToIndex(parts[0]);
+  Cnf cnf{{parts}};
+  columnar::BitSetPtr sel;
+  if (acc == "BTREE") {
+    throw std::runtime_error("BTREE index does not exist on column " + parts[0]);
+  } else if (acc == "BITMAP") {
+    if (!cf.bitmapIndexExists(col)) throw std::runtime_error("Bitmap index does not exist on column " + parts[0]);
+    sel = index_sel(cf, cnf, 0, 1, IndexType::Bitmap);
+  } else {
+    sel = scan_sel(cf, cnf, 0, 1);  // FILESCAN and COLUMNSCAN: the same PredEval, live rows only
+  }
+  const std::vector<int64_t> pos = sel->positions();
+  ok(mbx_db_mark_deleted_many(db, cf.get_fileName().c_str(), pos.data(), (int64_t)pos.size()), "markTupleDeleted");
+  if (kind == "pd") ok(mbx_db_purge(db, cf.get_fileName().c_str()), "purgeAllDeletedTuples");
+  cf.invalidate();
+  std::cout << "=======================EXTRA METAINFO===============================\n" << cf.getTupleCnt() << "\n";
+  columnar::BitSetPtr md = cf.getMarkedDeleted();
+  std::cout << java_bitset(md ? md->positions() : std::vector<int64_t>()) << "\n";
+}
+
 void nlj_cmd(const std::vector<std::string>& a) {
   if (a.size() < 12) throw std::runtime_error("Invalid number of attributes.");
   if (!global::SystemDefs::exists(a[1])) throw std::runtime_error("Database does not exist.");
@@ -605,6 +653,7 @@ int run() {
       else if (a[0] == "query") query(a);
       else if (a[0] == "indexes_query") indexes_query(a);
       else if (a[0] == "nlj") nlj_cmd(a);
+      else if (a[0] == "delete_query") delete_query(a);
       else if (a[0] == "bmj") bmj_cmd(a);
       else if (a[0] == "exit") break;
       else std::cout << "Command not supported by the GPU executor: " << a[0] << "\n";

@@ -483,6 +483,8 @@ BitSetPtr Columnarfile::getMarkedDeleted() const {
   return I.deleted_bm;
 }
 
+void Columnarfile::invalidate() { impl_->invalidate(); }
+
 void Columnarfile::markTupleDeleted(int64_t position) {
   Impl& I = *impl_;
   chk<chainexception::ChainException>(mbx_db_mark_deleted(I.db, I.name.c_str(), position), "markTupleDeleted");

@@ -225,6 +225,7 @@ class Columnarfile {
   BitSetPtr getBitmapIndex(int colNo, const std::string& key) const;  // empty BitSet if absent
   BitSetPtr getMarkedDeleted() const;  // may be null (nothing deleted)
   void markTupleDeleted(int64_t position);
+  void invalidate();  // the DB file changed under this object: re-stage on next use
 
   struct Impl;
 

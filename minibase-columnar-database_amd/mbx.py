@@ -90,7 +90,8 @@ EXPORTS = [
     "mbx_db_create", "mbx_db_open", "mbx_db_close", "mbx_db_info", "mbx_db_file_entry", "mbx_db_columnar_create",
     "mbx_db_columnar_insert", "mbx_db_columnar_info", "mbx_db_mark_deleted", "mbx_db_bitmap_write",
     "mbx_db_bitmap_read", "mbx_db_stage", "mbx_db_allocate_pages", "mbx_db_add_file_entry",
-    "mbx_db_create_bitmap_index", "mbx_db_bitmap_values", "mbx_db_bitmap_stage",
+    "mbx_db_create_bitmap_index", "mbx_db_bitmap_values", "mbx_db_bitmap_stage", "mbx_db_mark_deleted_many",
+    "mbx_db_purge",
     # include/mbx_join.h
     "mbx_join", "mbx_join_info", "mbx_join_fetch", "mbx_join_free", "mbx_gather",
 ]
@@ -173,6 +174,8 @@ def lib():
         "mbx_db_create_bitmap_index": ([V, V, ctypes.c_char_p, V, I32, P(I32)], ctypes.c_int),
         "mbx_db_bitmap_values": ([V, ctypes.c_char_p, I32, V, I64, P(I32), P(I64)], ctypes.c_int),
         "mbx_db_bitmap_stage": ([V, V, ctypes.c_char_p, I64, P(V)], ctypes.c_int),
+        "mbx_db_mark_deleted_many": ([V, ctypes.c_char_p, V, I64], ctypes.c_int),
+        "mbx_db_purge": ([V, ctypes.c_char_p], ctypes.c_int),
         "mbx_join": ([V, V, V, V, V, P(JoinCnf), I32, I64, P(V)], ctypes.c_int),
         "mbx_join_info": ([V, P(I64), P(I64)], ctypes.c_int),
         "mbx_join_fetch": ([V, V, I64, I64, V, V, V], ctypes.c_int),
@@ -675,6 +678,14 @@ class Db:
 
     def mark_deleted(self, name, position):
         _chk(lib().mbx_db_mark_deleted(self.h, name.encode(), position))
+
+    def mark_deleted_many(self, name, positions):
+        p = np.ascontiguousarray(positions, dtype=np.int64)
+        _chk(lib().mbx_db_mark_deleted_many(self.h, name.encode(), p.ctypes.data if len(p) else None, len(p)))
+
+    def purge(self, name):
+        """Columnarfile.purgeAllDeletedTuples."""
+        _chk(lib().mbx_db_purge(self.h, name.encode()))
 
     def bitmap_write(self, filename, words):
         w = np.ascontiguousarray(words, dtype=np.uint64)

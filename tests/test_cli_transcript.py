@@ -150,3 +150,32 @@ def test_join_commands_replay_transcript(tmp_path):
                 assert got["stats"][k] == v, (r["raw"], k)
         else:
             assert got["bitsets"] == r["bitsets"], r["raw"]
+
+
+def test_delete_query_md_and_pd(tmp_path):
+    """delete_query (R/input/DeleteQuery.java): `md` marks the scan's positions
+    in cf.md, later queries skip them; `pd` purges (records and BitSets) and
+    clears cf.md.  Counts checked against the oracle over minidata."""
+    rows = helpers.load_minidata()
+    out = run_session(["delete_query db cf {C,=,6} 10 FILESCAN md",
+                       "query db cf [A,C] {C,!=,100} 100 FILESCAN",
+                       "query db cf [C] {C,=,6} 100 BITMAP",
+                       "delete_query db cf {D,=,3} 10 BITMAP pd",
+                       "query db cf [A,B,C,D] {D,!=,3} 100 FILESCAN",
+                       "indexes_query db cf [A,C,D] {(C,>=,0,BM)} 10"], cwd=str(tmp_path))
+    assert "java.lang.Exception" not in out, out[-3000:]
+    chunks = out.split("> ")
+    md_chunk = [c for c in chunks if "EXTRA METAINFO" in c]
+    assert len(md_chunk) == 2
+    n6 = sum(1 for r in rows if r[2] == 6)
+    six = [i for i, r in enumerate(rows) if r[2] == 6]
+    assert md_chunk[0].split("\n")[1].strip() == str(500 - n6)
+    assert md_chunk[0].split("\n")[2].strip() == "{" + ", ".join(map(str, six)) + "}"
+    (_, r1, n1), (_, r2, n2), (_, r3, n3), (_, r4, n4) = blocks(out)
+    assert n1 == 500 - n6 and n2 == 0
+    gone = {i for i, r in enumerate(rows) if r[2] == 6 or r[3] == 3}
+    assert md_chunk[1].split("\n")[1].strip() == str(500 - len(gone))
+    assert md_chunk[1].split("\n")[2].strip() == "{}"
+    assert n3 == 500 - len(gone)
+    assert r3 == [f"{a}, {b}, {c}, {d}" for i, (a, b, c, d) in enumerate(rows) if i not in gone]
+    assert n4 == 500 - len(gone)

@@ -365,3 +365,95 @@ def test_bitmap_index_large_and_deleted(m, ctx, tmp_path):
         w = mp.bitmap_words(img, "cf.bm.1." + oracle.java_mutf8(s).decode("utf-8", "surrogatepass"))
         k = min(len(w), len(w_o))
         assert np.array_equal(w[:k], w_o[:k]) and not w[k:].any()
+
+
+def test_purge_all_deleted_tuples(m, tmp_path):
+    """Columnarfile.purgeAllDeletedTuples (R/columnar/Columnarfile.java:837-925)
+    on a 3 x int32 file spanning 4 directory pages per column: a whole
+    directory page of rows, one whole data page and scattered rows deleted.
+    After the purge the records are gone, emptied data pages and the emptied
+    (non-first) directory page are freed, the positions after the removed
+    directory page shift down by 83 * 125, holes stay holes, cf.md is clear and
+    cf.dtid empty; a following insert reuses the holes first (HFPage slot
+    reuse), then the freed data page's directory slot."""
+    path = str(tmp_path / "db")
+    per_dir = 83 * 125
+    n = 3 * per_dir + 77
+    rng = np.random.Generator(np.random.PCG64(17))
+    vals = [rng.integers(-1000, 1000, n, dtype=np.int32) for _ in range(3)]
+    cols = [(oracle.INTEGER, 4, v) for v in vals]
+    scattered = list(range(3, 2000, 7))
+    page5 = list(range(5 * 125, 6 * 125))
+    dir1 = list(range(per_dir, 2 * per_dir))
+    dead = sorted(set(scattered + page5 + dir1))
+    with m.mbx.Db(path, 1 << 14) as db:
+        db.columnar_create("cf", [(oracle.INTEGER, 4)] * 3, ["a", "b", "c"])
+        db.columnar_insert("cf", cols)
+        before = db.info()[1]
+        db.mark_deleted_many("cf", dead)
+        assert db.columnar_info("cf")["live"] == n - len(dead)
+        db.purge("cf")
+        after = db.info()[1]
+        info = db.columnar_info("cf")
+    # freed: per column 83 data pages of dir 1 + page 5 + dir page 1; cf.dtid's
+    # pages are freed and one new directory page is allocated
+    img = mp.DbImage(path)
+    assert before - after >= 3 * (83 + 1 + 1) - 1
+    fe = mp.file_entries(img)
+    assert mp.heap_records(img, fe["cf.dtid"]) == []
+    assert not mp.bitmap_words(img, "cf.md").any()
+    nrows, got, dele = mp.columnar_table(img, "cf")
+    survivors = [p for p in range(n) if p not in set(dead)]
+
+    def shifted(p):
+        return p - per_dir if p >= 2 * per_dir else p
+    want_pos = [shifted(p) for p in survivors]
+    live = [int(x) for x in np.nonzero(~np.unpackbits(dele.view(np.uint8), bitorder="little")[:nrows].astype(bool))[0]]
+    assert live == want_pos and nrows == shifted(n - 1) + 1
+    for (t, s, a), v in zip(got, vals):
+        assert np.array_equal(a[want_pos], v[survivors])
+    assert info["live"] == len(survivors) and info["nrows"] == nrows
+    # appending refills the holes in position order, then the freed data page's slot
+    holes = [p for p in scattered if p not in set(page5)]
+    k = len(holes) + 125 + 10
+    extra = [rng.integers(5000, 6000, k, dtype=np.int32) for _ in range(3)]
+    with m.mbx.Db(path) as db:
+        db.columnar_insert("cf", [(oracle.INTEGER, 4, v) for v in extra])
+    nrows2, got2, dele2 = mp.columnar_table(mp.DbImage(path), "cf")
+    for (t, s, a), v in zip(got2, extra):
+        assert np.array_equal(a[holes], v[:len(holes)])
+        assert np.array_equal(a[page5], v[len(holes):len(holes) + 125])
+    live2 = np.count_nonzero(~np.unpackbits(dele2.view(np.uint8), bitorder="little")[:nrows2].astype(bool))
+    assert live2 == len(survivors) + k
+
+
+@pytest.mark.gpu
+def test_purge_updates_bitmap_indexes(m, ctx, tmp_path):
+    """Bitmap indexes through a purge (BitMapFile.purgeDelete): deleted
+    positions cleared and the removed directory page's position range cut out
+    of every BitSet, so each BitMapFile equals the value's positions in the
+    purged file; scans of the re-staged table agree with the files."""
+    path = str(tmp_path / "db")
+    per_dir = 83 * 125
+    n = 3 * per_dir + 77
+    rng = np.random.Generator(np.random.PCG64(23))
+    vals = [rng.integers(0, 10, n, dtype=np.int32) for _ in range(2)]
+    dead = sorted(set(list(range(3, 2000, 7)) + list(range(per_dir, 2 * per_dir))))
+    with m.mbx.Db(path, 1 << 14) as db:
+        db.columnar_create("cf", [(oracle.INTEGER, 4)] * 2, ["a", "b"])
+        db.columnar_insert("cf", [(oracle.INTEGER, 4, v) for v in vals])
+        t = ctx.stage_db(db, "cf")
+        assert ctx.create_bitmap_index(db, "cf", t, 0) == 10
+        db.mark_deleted_many("cf", dead)
+        db.purge("cf")
+        t2 = ctx.stage_db(db, "cf")
+        survivors = [p for p in range(n) if p not in set(dead)]
+        new_pos = np.array([p - per_dir if p >= 2 * per_dir else p for p in survivors])
+        for v in range(10):
+            want = new_pos[vals[0][survivors] == v]
+            w = db.bitmap_read(f"cf.bm.0.{v}")
+            assert list(oracle.words_to_positions(w)) == list(want), v
+            plan = ctx.compile(t2, [[(oracle.EQ, ("sym", 1), ("int", v))]])
+            assert ctx.scan_count(plan) == len(want)
+            bm = ctx.stage_db_bitmap(db, f"cf.bm.0.{v}", t2.nrows)
+            assert bm.count == len(want)
