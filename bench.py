@@ -6,6 +6,8 @@ One "step" = one ColumnarFileScan COUNT pass over the resident table:
 `query ... {(c0 < 2^19)} ^ {(c1 >= 2^19)} FILESCAN` -> Total Results Count,
 executed as ONE kernel launch (k_scan_fast<2, COUNT>; its last block folds the
 per-block partials).  Inputs are resident in HBM before the timed region.
+Consecutive steps alternate over --streams library contexts (each its own HIP
+stream and scratch), so one pass's tail overlaps the next pass's start.
 
 Multi-GPU (weak scaling): each rank owns its own 100M-row
 shard (rows [rank*N, (rank+1)*N) of one logical table); per step the ranks'
@@ -78,6 +80,9 @@ def main():
     ap.add_argument("--rows", type=int, default=100_000_000, help="rows per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="contexts (HIP streams) the steps alternate over: consecutive passes overlap at the "
+                         "kernel boundary instead of draining the GPU between them")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -100,7 +105,8 @@ def main():
         else:
             dist.init_process_group(backend)
     m = mbx_pkg.load()
-    ctx = m.Context(device)
+    ctxs = [m.Context(device) for _ in range(max(1, args.streams))]
+    ctx = ctxs[0]
     n = args.rows
 
     # synthetic C3 shard, generated in HBM: 4 x int32 uniform [0, 2^20)
@@ -110,9 +116,12 @@ def main():
         g.manual_seed(42 + j + 1000 * rank)
         cols.append(torch.randint(0, 1 << 20, (n,), dtype=torch.int32, device="cuda", generator=g))
     torch.cuda.synchronize()
-    table = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [c.data_ptr() for c in cols], n, None, row_offset=rank * n)
+    # one zero-copy table view + compiled plan per context (same HBM columns)
+    tables = [c.wrap([(m.mbx.INTEGER, 4)] * 4, [col.data_ptr() for col in cols], n, None, row_offset=rank * n)
+              for c in ctxs]
     cnf = [[(m.mbx.LT, ("sym", 1), ("int", THRESH))], [(m.mbx.GE, ("sym", 2), ("int", THRESH))]]
-    plan = ctx.compile(table, cnf)
+    plans = [c.compile(t, cnf) for c, t in zip(ctxs, tables)]
+    table, plan = tables[0], plans[0]
 
     # correctness gate before timing: the kernel's count vs a torch reduction
     # of the same device columns (the oracle cross-check lives in tests/)
@@ -122,22 +131,28 @@ def main():
 
     steps, warmup = args.steps, args.warmup
     counts = torch.zeros(steps + warmup, dtype=torch.int64, device="cuda")
-    ext = torch.cuda.ExternalStream(ctx.stream)
+    exts = [torch.cuda.ExternalStream(c.stream) for c in ctxs]
+    ext = exts[0]
     xs = torch.cuda.Stream() if world > 1 else None
     base = counts.data_ptr()
 
     def step(k):
-        ctx.scan_count_async(plan, base + 8 * k)
+        j = k % len(ctxs)
+        ctxs[j].scan_count_async(plans[j], base + 8 * k)
         if world > 1:  # the one exchange step: combine COUNT over ranks
             ev = torch.cuda.Event()
-            ev.record(ext)
+            ev.record(exts[j])
             xs.wait_event(ev)
             with torch.cuda.stream(xs):
                 dist.all_reduce(counts[k:k + 1])
 
+    def sync_all():
+        for c in ctxs:
+            c.sync()
+
     for k in range(warmup):
         step(k)
-    ctx.sync()
+    sync_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -147,7 +162,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(steps):
         step(warmup + k)
-    ctx.sync()
+    sync_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -200,6 +215,7 @@ def main():
                 "global_rows": n * world,
                 "parallelism": f"row-range shards x{world}" + (", RCCL all_reduce of COUNT per step" if world > 1
                                                               else ""),
+                "streams": len(ctxs),
             },
             "hbm_gbs": algo_bytes * world / (t_max / steps) / 1e9,
             "roofline": {
@@ -220,8 +236,10 @@ def main():
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
         print(json.dumps(out), flush=True)
 
-    table.close()
-    ctx.close()
+    for t in tables:
+        t.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -21,78 +21,101 @@
 
 namespace mbx {
 
-__device__ __forceinline__ uint32_t ld_be16(const uint8_t* p) { return ((uint32_t)p[0] << 8) | (uint32_t)p[1]; }
+// One wave per data page: lane l handles slots l, l+64, l+128 (<= 143 records
+// per page).  Slot entries are read as aligned big-endian words, 4-byte
+// records as aligned words (every record of a column page has the same size,
+// so offsets stay 4-aligned), outputs are written at consecutive positions;
+// the `present` bits of each 64-slot group come from one ballot and go out
+// with at most two atomicOr (page boundaries share words).
+__device__ __forceinline__ uint32_t ld_be32a(const uint8_t* p) {
+  return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(p));
+}
 
 __global__ __launch_bounds__(kBlock) void k_page_decode(PageDecodeArgs A) {
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * kWaves;
+  int32_t err = 0;
   for (int64_t pi = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); pi < A.npages; pi += nwaves) {
     const int32_t pid = A.page_of[pi];
     if (pid < 0) continue;
     if ((int64_t)pid >= A.image_pages) {
-      if (lane == 0) atomicOr(A.err, 1);
+      err |= 1;
       continue;
     }
     const uint8_t* pg = A.image + (int64_t)pid * kDbPage;
-    int32_t slots = (int32_t)(int16_t)ld_be16(pg);
+    int32_t slots = (int32_t)(int16_t)(ld_be32a(pg) >> 16);
     if (slots > A.recs_per_page || slots < 0) {
-      if (lane == 0) atomicOr(A.err, 2);
+      err |= 2;
       slots = slots < 0 ? 0 : A.recs_per_page;
     }
-    for (int32_t k = lane; k < slots; k += 64) {
-      const uint8_t* sp = pg + kDbSlotBase + 4 * k;
-      const int32_t len = (int32_t)(int16_t)ld_be16(sp);
-      const int32_t off = (int32_t)ld_be16(sp + 2);
-      if (len == -1) continue;  // EMPTY_SLOT
-      if (len != A.rec_len || off < kDbSlotBase || off + len > kDbPage) {
-        atomicOr(A.err, 4);
-        continue;
-      }
-      const int64_t pos = pi * A.recs_per_page + k;
-      if (pos >= A.nrows) {
-        atomicOr(A.err, 8);
-        continue;
-      }
-      const uint8_t* rec = pg + off;
-      if (A.kind != kStr) {
-        const uint32_t v = ((uint32_t)rec[0] << 24) | ((uint32_t)rec[1] << 16) | ((uint32_t)rec[2] << 8) | rec[3];
-        reinterpret_cast<uint32_t*>(A.out)[pos] = v;
-      } else {
-        // writeUTF image: u16 length + modified UTF-8; device image rewrites
-        // C0 80 (U+0000) as 00 01 and zero-pads to the stride
-        int32_t L = (int32_t)ld_be16(rec);
-        if (L > A.size) {
-          atomicOr(A.err, 16);
-          L = A.size;
-        }
-        uint32_t* dst = reinterpret_cast<uint32_t*>(A.out + pos * (int64_t)A.stride);
-        uint32_t acc = 0;
-        int32_t o = 0;
-        auto put = [&](uint32_t byte) {
-          acc |= byte << (8 * (o & 3));
-          if ((o & 3) == 3) {
-            dst[o >> 2] = acc;
-            acc = 0;
-          }
-          ++o;
-        };
-        int32_t i = 0;
-        while (i < L) {
-          const uint32_t byte = rec[2 + i];
-          if (byte == 0xC0u && i + 1 < L && rec[3 + i] == 0x80u) {
-            put(0u);
-            put(1u);
-            i += 2;
+    for (int32_t k0 = 0; k0 < slots; k0 += 64) {
+      const int32_t k = k0 + lane;
+      bool ok = false;
+      if (k < slots) {
+        const uint32_t se = ld_be32a(pg + kDbSlotBase + 4 * k);
+        const int32_t len = (int32_t)(int16_t)(se >> 16);
+        const int32_t off = (int32_t)(se & 0xFFFFu);
+        const int64_t pos = pi * A.recs_per_page + k;
+        if (len == -1) {
+          // EMPTY_SLOT: no record at this position
+        } else if (len != A.rec_len || off < kDbSlotBase || off + len > kDbPage) {
+          err |= 4;
+        } else if (pos >= A.nrows) {
+          err |= 8;
+        } else {
+          const uint8_t* rec = pg + off;
+          ok = true;
+          if (A.kind != kStr) {
+            const uint32_t v = (off & 3) == 0 ? ld_be32a(rec)
+                                              : ((uint32_t)rec[0] << 24) | ((uint32_t)rec[1] << 16) |
+                                                    ((uint32_t)rec[2] << 8) | rec[3];
+            reinterpret_cast<uint32_t*>(A.out)[pos] = v;
           } else {
-            put(byte);
-            ++i;
+            // writeUTF image: u16 length + modified UTF-8; device image rewrites
+            // C0 80 (U+0000) as 00 01 and zero-pads to the stride
+            int32_t L = (int32_t)(((uint32_t)rec[0] << 8) | rec[1]);
+            if (L > A.size) {
+              err |= 16;
+              L = A.size;
+            }
+            uint32_t* dst = reinterpret_cast<uint32_t*>(A.out + pos * (int64_t)A.stride);
+            uint32_t acc = 0;
+            int32_t o = 0;
+            auto put = [&](uint32_t byte) {
+              acc |= byte << (8 * (o & 3));
+              if ((o & 3) == 3) {
+                dst[o >> 2] = acc;
+                acc = 0;
+              }
+              ++o;
+            };
+            int32_t i = 0;
+            while (i < L) {
+              const uint32_t byte = rec[2 + i];
+              if (byte == 0xC0u && i + 1 < L && rec[3 + i] == 0x80u) {
+                put(0u);
+                put(1u);
+                i += 2;
+              } else {
+                put(byte);
+                ++i;
+              }
+            }
+            while (o < A.stride) put(0u);
           }
         }
-        while (o < A.stride) put(0u);
       }
-      atomicOr(reinterpret_cast<unsigned long long*>(A.present) + (pos >> 6), 1ull << (pos & 63));
+      const uint64_t m = __ballot(ok);
+      if (lane == 0 && m) {
+        const int64_t base = pi * A.recs_per_page + k0;
+        const int sh = (int)(base & 63);
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(A.present) + (base >> 6);
+        atomicOr(w, (unsigned long long)(m << sh));
+        if (sh && (m >> (64 - sh))) atomicOr(w + 1, (unsigned long long)(m >> (64 - sh)));
+      }
     }
   }
+  if (err) atomicOr(A.err, err);
 }
 
 __global__ __launch_bounds__(kBlock) void k_present_merge(const uint64_t* __restrict__ present0,
