@@ -215,6 +215,31 @@ int64_t orc_filescan(const orc_column *cols, int32_t ncols, int64_t nrows,
   return count;
 }
 
+/* The same COUNT with the rows split into `nthreads` contiguous ranges, each
+ * evaluated by one OpenMP thread exactly like orc_filescan (the CPU baseline
+ * bench.py reports: SURVEY 8(d)(ii), "the C++ CPU restatement across host
+ * cores").  Row order inside a range is the reference's. */
+int64_t orc_filescan_count_mt(const orc_column *cols, int32_t ncols, int64_t nrows,
+                              const uint64_t *deleted_words, const orc_cnf *cnf, int32_t nthreads) {
+  int64_t count = 0;
+  int err = 0;
+  if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for num_threads(nthreads) reduction(+ : count) reduction(| : err) schedule(static)
+  for (int32_t t = 0; t < nthreads; t++) {
+    const int64_t a = nrows * t / nthreads, b = nrows * (t + 1) / nthreads;
+    for (int64_t pos = a; pos < b; pos++) {
+      if (deleted(deleted_words, pos)) continue;
+      int r = orc_pred_eval(cnf, cols, ncols, pos);
+      if (r < 0) {
+        err |= 1;
+        break;
+      }
+      count += r;
+    }
+  }
+  return err ? ORC_E_TYPE : count;
+}
+
 int orc_aggregate(const orc_column *cols, int32_t ncols, int64_t nrows,
                   const uint64_t *deleted_words, const orc_cnf *cnf,
                   int32_t agg_col, orc_agg *out) {

@@ -105,6 +105,9 @@ int orc_string_compare(const char *a, int32_t alen, const char *b, int32_t blen)
 int64_t orc_filescan(const orc_column *cols, int32_t ncols, int64_t nrows,
                      const uint64_t *deleted_words, const orc_cnf *cnf,
                      uint64_t *out_words, int64_t *out_ids);
+/* orc_filescan's COUNT over nthreads OpenMP threads (contiguous row ranges) */
+int64_t orc_filescan_count_mt(const orc_column *cols, int32_t ncols, int64_t nrows,
+                              const uint64_t *deleted_words, const orc_cnf *cnf, int32_t nthreads);
 
 /* COUNT/SUM/MIN/MAX over the rows orc_filescan selects (no reference
  * equivalent; SURVEY.md 8(a) a20 defines it). */

@@ -98,6 +98,9 @@ def lib():
         L.orc_columnar_index_scan.argtypes = [P(_Column), ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
                                               P(_Cnf), ctypes.c_void_p]
         L.orc_columnar_index_scan.restype = ctypes.c_int64
+        L.orc_filescan_count_mt.argtypes = [P(_Column), ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
+                                            P(_Cnf), ctypes.c_int32]
+        L.orc_filescan_count_mt.restype = ctypes.c_int64
         L.orc_gather.argtypes = [P(_Column), ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
                                  P(ctypes.c_int32), ctypes.c_int32, P(ctypes.c_void_p)]
         _lib = L
@@ -210,6 +213,14 @@ def filescan_count(table, cnf):
     c = _cnf(cnf, keep)
     return _check(lib().orc_filescan(table._c, len(table.columns), table.nrows, table._del_ptr(),
                                      ctypes.byref(c), None, None), "filescan")
+
+
+def filescan_count_mt(table, cnf, nthreads):
+    """filescan_count over nthreads OpenMP threads (the multi-core CPU baseline)."""
+    keep = []
+    c = _cnf(cnf, keep)
+    return _check(lib().orc_filescan_count_mt(table._c, len(table.columns), table.nrows, table._del_ptr(),
+                                              ctypes.byref(c), nthreads), "filescan_count_mt")
 
 
 def pred_eval(table, cnf, row):
