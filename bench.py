@@ -223,8 +223,8 @@ def main():
                             "(ColumnarFileScan / PredEval), 1 kernel launch per step",
                 "rows_per_gpu": n,
                 "global_rows": n * world,
-                "parallelism": f"row-range shards x{world}" + (", RCCL all_reduce of COUNT per step" if world > 1
-                                                              else ""),
+                "parallelism": f"row-range shards x{world}" + (
+                    f", {'RCCL' if backend == 'nccl' else backend} all_reduce of COUNT per step" if world > 1 else ""),
                 "streams": len(ctxs),
             },
             "hbm_gbs": algo_bytes * world / (t_max / steps) / 1e9,

@@ -16,6 +16,8 @@
 // Term semantics are PredEval's (R/iterator/PredEval.java:137-162): signed int
 // compare, float compare (NaN flagged), String.compareTo order for char(n)
 // (big-endian word compare of the device string images, any two strides).
+#include <algorithm>
+
 #include "mbx_internal.hpp"
 
 namespace mbx {
@@ -63,32 +65,40 @@ __device__ __forceinline__ uint32_t eval_pair(const JoinArgs& A, int64_t orow, i
   return cb;
 }
 
+// Grid: blockIdx.y strides over the matrix words w (64 lane-side entries,
+// fixed per wave, so their positions are read once), blockIdx.x * 4 + wave
+// strides over rows.  The row side is wave-uniform: one scalar read per term
+// per row.
 __global__ __launch_bounds__(kBlock) void k_join_matrix(JoinArgs A) {
   const int lane = threadIdx.x & 63;
-  const int64_t nwaves = (int64_t)gridDim.x * kWaves;
-  const int64_t items = A.nrows * A.words_per_row;
+  const int64_t rstride = (int64_t)gridDim.x * kWaves;
   int32_t nan = 0;
-  for (int64_t it = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); it < items; it += nwaves) {
-    const int64_t r = it / A.words_per_row;          // matrix row within this launch
-    const int64_t w = it - r * A.words_per_row;      // word of the row
-    const int64_t row = A.row0 + r;
+  for (int64_t w = blockIdx.y; w < A.words_per_row; w += gridDim.y) {
     const int64_t col = w * 64 + lane;
-    int64_t oi, ii;  // indexes into the outer / inner selections
-    bool valid;
-    if (A.mode == 0) {  // BMJ: row = outer index, lanes = inner indexes
-      oi = row;
-      ii = col;
-      valid = ii < A.ni;
-    } else {            // NLJ: row = pass * ni + inner index, lanes = outer in the pass's block
-      const int64_t p = row / A.ni;
-      ii = row - p * A.ni;
-      oi = p * A.block + col;
-      valid = col < A.block && oi < A.no;
+    int64_t lane_pos = -1;  // BMJ: inner position of this lane; NLJ: outer, per pass
+    int64_t cached_pass = -1;
+    if (A.mode == 0 && col < A.ni) lane_pos = A.ipos[col];
+    for (int64_t r = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); r < A.nrows; r += rstride) {
+      const int64_t row = A.row0 + r;
+      int64_t orow, irow;
+      if (A.mode == 0) {  // BMJ: row = outer index (uniform), lanes = inner
+        orow = A.opos[row];
+        irow = lane_pos;
+      } else {            // NLJ: row = pass * ni + inner index (uniform), lanes = outer of the block
+        const int64_t p = row / A.ni;
+        irow = A.ipos[row - p * A.ni];
+        if (p != cached_pass) {
+          cached_pass = p;
+          const int64_t oi = p * A.block + col;
+          lane_pos = (col < A.block && oi < A.no) ? A.opos[oi] : -1;
+        }
+        orow = lane_pos;
+      }
+      bool hit = false;
+      if (lane_pos >= 0) hit = eval_pair(A, orow, irow, nan) == A.all_conj;
+      const uint64_t m = __ballot(hit);
+      if (lane == 0) A.out[r * A.words_per_row + w] = m;
     }
-    bool hit = false;
-    if (valid) hit = eval_pair(A, A.opos[oi], A.ipos[ii], nan) == A.all_conj;
-    const uint64_t m = __ballot(hit);
-    if (lane == 0) A.out[r * A.words_per_row + w] = m;
   }
   if (nan) atomicOr(A.nan, 1);
 }
@@ -135,9 +145,12 @@ static int64_t grid_for(int64_t work, int64_t per_block, int64_t cap) {
 }
 
 hipError_t launch_join_matrix(const JoinArgs& A, hipStream_t s) {
-  const int64_t items = A.nrows * A.words_per_row;
-  if (items <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_join_matrix, dim3((unsigned)grid_for(items, kWaves, 8192)), dim3(kBlock), 0, s, A);
+  if (A.nrows <= 0 || A.words_per_row <= 0) return hipSuccess;
+  // ~2048 blocks across the words of a row and the rows
+  const int64_t gy = std::min<int64_t>(A.words_per_row, 65535);
+  const int64_t want = std::max<int64_t>(1, 2048 / gy);
+  const int64_t gx = std::min<int64_t>(want, (A.nrows + kWaves - 1) / kWaves);
+  hipLaunchKernelGGL(k_join_matrix, dim3((unsigned)std::max<int64_t>(gx, 1), (unsigned)gy), dim3(kBlock), 0, s, A);
   return hipGetLastError();
 }
 

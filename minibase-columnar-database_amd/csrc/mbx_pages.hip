@@ -172,6 +172,8 @@ __device__ __forceinline__ bool rows_equal(const KCol& c, int64_t a, int64_t b) 
 }
 
 __global__ __launch_bounds__(kBlock) void k_distinct(DistinctArgs A) {
+  // keys / minpos are written only through atomics; every read below may be
+  // stale (see the loop) but never wrong
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   const uint64_t mask = (uint64_t)A.cap - 1;
   for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < A.nrows; row += stride) {
@@ -179,14 +181,15 @@ __global__ __launch_bounds__(kBlock) void k_distinct(DistinctArgs A) {
     uint64_t h = row_hash(A.col, row) & mask;
     bool placed = false;
     for (int64_t probe = 0; probe < A.cap; ++probe, h = (h + 1) & mask) {
-      unsigned long long k = __hip_atomic_load(A.keys + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // plain (cached) reads: a stale EMPTY only sends the row to the CAS,
+      // a stale minimum only costs one more atomicMin -- both still exact
+      unsigned long long k = A.keys[h];
       if (k == kEmptySlot) {
         k = atomicCAS(A.keys + h, kEmptySlot, (unsigned long long)row);
         if (k == kEmptySlot) k = (unsigned long long)row;
       }
       if (rows_equal(A.col, (int64_t)k, row)) {
-        const unsigned long long m =
-            __hip_atomic_load(A.minpos + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long m = A.minpos[h];
         if ((unsigned long long)row < m) atomicMin(A.minpos + h, (unsigned long long)row);
         placed = true;
         break;

@@ -13,3 +13,8 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o c3 --output-format
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o c3 --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/write.log 2>&1 || { echo WRITE_FAIL; exit 1; }
 python tools/pmc_summary.py $OUT/kt $OUT/fetch $OUT/write --rows 100000000 --algo-bytes 800000000 --out $OUT/c3_scan_pmc.json > $OUT/summary.log 2>&1 || { echo SUMMARY_FAIL; exit 1; }
 echo ROUND_OK
+# N>1 flow rehearsal on this one GPU: 2 ranks, gloo for the combine (RCCL
+# refuses two ranks on one device), short run
+MBX_BENCH_BACKEND=gloo MBX_BENCH_SAME_DEVICE=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --rows 20000000 > $OUT/bench_2rank_gloo.json 2> $OUT/bench_2rank_gloo.err || { echo REHEARSAL_FAIL; exit 1; }
+cat $OUT/bench_2rank_gloo.json
+echo REHEARSAL_OK
