@@ -429,3 +429,46 @@ def test_index_build_float_column(ctx):
     for v, bm in zip([0.0, 0.25, 0.5, 3.0], ctx.index_build(t, 1, [("real", x) for x in [0.0, 0.25, 0.5, 3.0]])):
         n_o, w_o = oracle.bitmap_eq(ot, 1, ("real", v))
         assert bm.count == n_o and np.array_equal(bm.download(), w_o)
+
+
+def test_c4_full_size_bitmap_and_gather(ctx, m):
+    """C4 at BASELINE size: 100M rows, bm(c2=3) AND bm(c3=7) built on the GPU,
+    compacted to positions and gathered (c0, c1) -- checked against numpy."""
+    n = 100_000_000
+    c0, c1 = (np.random.Generator(np.random.PCG64(42 + j)).integers(0, 1 << 20, n, dtype=np.int32) for j in range(2))
+    c2, c3 = (np.random.Generator(np.random.PCG64(44 + j)).integers(0, 10, n, dtype=np.int32) for j in range(2))
+    t = ctx.stage([(oracle.INTEGER, 4, c) for c in (c0, c1, c2, c3)])
+    (b2,) = ctx.index_build(t, 2, [("int", 3)])
+    (b3,) = ctx.index_build(t, 3, [("int", 7)])
+    sel = ctx.bitmap_combine(m.mbx.BM_AND, b2, b3)
+    want = np.nonzero((c2 == 3) & (c3 == 7))[0]
+    assert sel.count == len(want)
+    ids, (x, y) = ctx.materialize(t, sel, [0, 1])
+    assert np.array_equal(ids, want)
+    assert np.array_equal(x, c0[want]) and np.array_equal(y, c1[want])
+
+
+def test_c5_shard_full_size(ctx):
+    """One GPU's C5 shard at BASELINE size (125M rows of the 1B-row table over
+    8 GPUs): 3-conjunct int/float/char(16) filter + COUNT/SUM/MIN/MAX vs numpy
+    (count, min, max exact; SUM within 1e-6 relative), and the complement
+    identity count(P) + count(not P) = N."""
+    n = 125_000_000
+    cols, names = mixed_table(n, seed=77)
+    c0, c1, c2 = (a for _, _, a in cols)
+    t = ctx.stage(cols)
+    plan = ctx.compile(t, C5_CNF)
+    agg = ctx.scan_aggregate(plan, 1)
+    m_mask = np.array([oracle.java_mutf8(s) >= b"M" for s in names])  # ASCII names: byte order = Java order
+    idx = np.frombuffer(c2.tobytes(), dtype="S16")
+    keep = (c0 < (1 << 19)) & (c1 >= np.float32(0.25))
+    name_ok = np.isin(idx, np.frombuffer(helpers.encode_strings([s for s, ok in zip(names, m_mask) if ok], 16)
+                                         .tobytes(), dtype="S16"))
+    sel = keep & name_ok
+    vals = c1[sel]
+    assert agg["count"] == int(sel.sum())
+    assert agg["min"] == float(vals.min()) and agg["max"] == float(vals.max())
+    assert abs(agg["sum"] - float(vals.astype(np.float64).sum())) <= 1e-6 * abs(float(vals.astype(np.float64).sum()))
+    neg = [[(oracle.GE, ("sym", 1), ("int", 1 << 19)), (oracle.LT, ("sym", 2), ("real", 0.25)),
+            (oracle.LT, ("sym", 3), ("str", "M"))]]
+    assert ctx.scan_count(plan) + ctx.scan_count(ctx.compile(t, neg)) == n
