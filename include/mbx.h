@@ -241,6 +241,15 @@ int mbx_cursor_next(mbx_cursor *c, int64_t max_rows, int64_t *host_ids, void *co
 int mbx_cursor_restart(mbx_cursor *c); /* Iterator.restart() */
 int mbx_cursor_close(mbx_cursor *c);   /* Iterator.close(), idempotent via free */
 
+/* ---- diagnostics (no reference counterpart): the scan's load pattern with
+ * the predicate removed, over the 4-byte columns cols[0..ncols) (ncols <= 4)
+ * of t's full 256-row tiles, enqueued on mbx_stream(ctx).  Timed by the
+ * caller; it is the measured read ceiling the scan's roofline is set beside.
+ * tiles_per_block <= 0: the scan's own segment size; interleave != 0:
+ * grid-stride over `grid` blocks instead of segments. */
+int mbx_probe_read(mbx_ctx *ctx, const mbx_table *t, const int32_t *cols, int32_t ncols,
+                   int64_t tiles_per_block, int32_t interleave, int64_t grid);
+
 #ifdef __cplusplus
 }
 #endif

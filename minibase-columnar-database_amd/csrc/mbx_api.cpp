@@ -199,6 +199,33 @@ extern "C" int mbx_sync(mbx_ctx* c) {
 
 extern "C" void* mbx_stream(mbx_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+extern "C" int mbx_probe_read(mbx_ctx* c, const mbx_table* t, const int32_t* cols, int32_t ncols,
+                              int64_t tiles_per_block, int32_t interleave, int64_t grid) {
+  NOTNULL(c);
+  NOTNULL(t);
+  NOTNULL(cols);
+  if (ncols < 1 || ncols > kMaxProbeCols) return fail(MBX_E_INVALID, "probe: ncols %d not in 1..%d", ncols, kMaxProbeCols);
+  ProbeArgs A{};
+  for (int i = 0; i < ncols; ++i) {
+    if (cols[i] < 0 || cols[i] >= (int32_t)t->cols.size() || t->cols[cols[i]].stride_w != 1)
+      return fail(MBX_E_INVALID, "probe: column %d is not a 4-byte column of the table", cols[i]);
+    A.cols[i] = (const int32_t*)t->cols[cols[i]].dev;
+  }
+  A.ncols = ncols;
+  A.interleave = interleave ? 1 : 0;
+  A.nrows = t->nrows;
+  A.tiles_per_block = tiles_per_block > 0 ? tiles_per_block : tiles_per_block_for(t->nrows);
+  const int64_t ntiles = t->nrows / kTileRows;
+  A.grid = interleave ? (grid > 0 ? grid : 1024) : (ntiles + A.tiles_per_block - 1) / A.tiles_per_block;
+  if (A.grid < 1) A.grid = 1;
+  if (A.grid > (1 << 20)) return fail(MBX_E_INVALID, "probe: grid %lld too large", (long long)A.grid);
+  if (int rc = ensure_partials(c, A.grid)) return rc;
+  A.sink = (uint32_t*)c->partials;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(launch_read_probe(A, c->stream));
+  return MBX_OK;
+}
+
 // ------------------------------------------------------------------ tables
 
 int mbx::check_cols(const mbx_col_desc* cols, int32_t ncols) {
@@ -677,6 +704,7 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.nan_out = nan_out;
   const char* var = getenv("MBX_SCAN_VARIANT");
   L.variant = var ? atoi(var) : 0;
+  L.nterms_host = p->host.nterms;
   const char* fm = getenv("MBX_FIN_MODE");
   L.fin_mode = fm ? atoi(fm) : kFinWriteThrough;
   if (L.fin_mode == kFinSeparate) L.ticket = nullptr;

@@ -113,6 +113,7 @@ struct ScanLaunch {
   AggOut* agg_out;            // device or null
   int32_t* nan_out;           // device or null
   int32_t variant;            // 0: default kernel; >0: tuning variant (MBX_SCAN_VARIANT)
+  int32_t nterms_host;        // the plan's term count, for launch-time kernel choice
   int32_t fin_mode;           // FinMode (MBX_FIN_MODE): how the last block sees the partials
 };
 
@@ -174,6 +175,7 @@ hipError_t launch_present_merge(const uint64_t* present0, const uint64_t* other,
 
 constexpr unsigned long long kEmptySlot = ~0ull;
 
+constexpr int kLdsProbes = 16;   // k_distinct's default LDS probe bound
 struct DistinctArgs {
   KCol col;
   int64_t nrows;
@@ -182,6 +184,7 @@ struct DistinctArgs {
   unsigned long long* minpos;   // cap slots, kEmptySlot initially; smallest row with the value
   int64_t cap;                  // power of two
   int32_t* overflow;
+  int32_t lds_probes;           // LDS pre-fold probe bound (0: every row goes to the global table)
 };
 
 hipError_t launch_distinct(const DistinctArgs& A, hipStream_t s);
@@ -235,6 +238,19 @@ hipError_t launch_join_decode(const int64_t* ids, const int64_t* n, int64_t max_
                               hipStream_t s);
 hipError_t launch_gather_pos(const int64_t* pos, int64_t n, int64_t row_offset, const void* col, int32_t stride_w,
                              void* out, hipStream_t s);
+
+// read-bandwidth probe (k_read_probe): the scan's loads without a predicate
+constexpr int kMaxProbeCols = 4;
+struct ProbeArgs {
+  const int32_t* cols[kMaxProbeCols];
+  int32_t ncols;
+  int32_t interleave;       // 0: segments of tiles_per_block tiles; 1: grid-stride over `grid` blocks
+  int64_t nrows;
+  int64_t tiles_per_block;
+  int64_t grid;
+  uint32_t* sink;           // one word per block
+};
+hipError_t launch_read_probe(const ProbeArgs& A, hipStream_t s);
 
 int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block);
 int64_t choose_tiles_per_block(int64_t nrows);

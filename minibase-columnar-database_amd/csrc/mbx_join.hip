@@ -17,6 +17,8 @@
 // compare, float compare (NaN flagged), String.compareTo order for char(n)
 // (big-endian word compare of the device string images, any two strides).
 #include <algorithm>
+#include <cstdint>
+#include <cstdlib>
 
 #include "mbx_internal.hpp"
 
@@ -103,6 +105,113 @@ __global__ __launch_bounds__(kBlock) void k_join_matrix(JoinArgs A) {
   if (nan) atomicOr(A.nan, 1);
 }
 
+// Fast form for CNFs of at most kFastJoinTerms int / float terms.  A wave
+// owns 64 matrix rows x one word: lane k loads row k's side (position and the
+// term values, one coalesced load per term) and the lanes' side is held in
+// registers; the 64 rows are then swept with v_readlane, so the dependent
+// row-side loads of the plain form become one batch per 64 ballots.  Each
+// term is reduced to a 3-bit outcome mask {x<y, x==y, x>y} over x = lane
+// value, y = row value (the BMJ masks are mirrored host-side since the row
+// is the outer side there).  Lane k keeps ballot k; one store per lane.
+constexpr int kFastJoinTerms = 4;
+
+struct FastJoin {
+  const int32_t* lane_col[kFastJoinTerms];
+  const int32_t* row_col[kFastJoinTerms];
+  int32_t is_real[kFastJoinTerms];
+  uint32_t mask[kFastJoinTerms];   // bit0: x<y, bit1: x==y, bit2: x>y
+  uint32_t bit[kFastJoinTerms];
+};
+
+__device__ __forceinline__ void lane_values(const JoinArgs& A, const FastJoin& F, int64_t pos, int32_t* lv) {
+#pragma unroll
+  for (int t = 0; t < kFastJoinTerms; ++t) lv[t] = (t < A.nterms && pos >= 0) ? F.lane_col[t][pos] : 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_join_matrix_fast(JoinArgs A, FastJoin F) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nchunks = (A.nrows + 63) >> 6;
+  const int64_t cstride = (int64_t)gridDim.x * kWaves;
+  int32_t nan = 0;
+  for (int64_t w = blockIdx.y; w < A.words_per_row; w += gridDim.y) {
+    const int64_t col = w * 64 + lane;
+    int64_t lane_pos = -1;
+    int32_t lv[kFastJoinTerms];
+    int64_t pass = -1;                        // NLJ: the pass the lane values belong to
+    if (A.mode == 0) {
+      lane_pos = col < A.ni ? A.ipos[col] : -1;
+      lane_values(A, F, lane_pos, lv);
+    }
+    for (int64_t ch = (int64_t)blockIdx.x * kWaves + wave; ch < nchunks; ch += cstride) {
+      const int64_t r0 = ch * 64;
+      // row side of rows r0 .. r0 + 63 (lane k holds row r0 + k)
+      const int64_t rr = r0 + lane;
+      const bool rvalid = rr < A.nrows;
+      const int64_t row = A.row0 + rr;
+      int64_t rpos = -1;
+      if (rvalid) {
+        if (A.mode == 0) {
+          rpos = A.opos[row];
+        } else {
+          const int64_t p = row / A.ni;
+          rpos = A.ipos[row - p * A.ni];
+        }
+      }
+      int32_t rv[kFastJoinTerms];
+#pragma unroll
+      for (int t = 0; t < kFastJoinTerms; ++t) rv[t] = (t < A.nterms && rpos >= 0) ? F.row_col[t][rpos] : 0;
+      // NLJ: matrix row -> pass changes at multiples of ni
+      int64_t next_pass_row = INT64_MAX;
+      if (A.mode == 1) {
+        const int64_t p = (A.row0 + r0) / A.ni;
+        if (p != pass) {
+          pass = p;
+          const int64_t oi = p * A.block + col;
+          lane_pos = (col < A.block && oi < A.no) ? A.opos[oi] : -1;
+          lane_values(A, F, lane_pos, lv);
+        }
+        next_pass_row = (p + 1) * A.ni - A.row0;  // launch-local row where the next pass starts
+      }
+      const int kmax = (int)min<int64_t>(64, A.nrows - r0);
+      uint64_t mine = 0;
+      for (int k = 0; k < kmax; ++k) {
+        if (A.mode == 1 && r0 + k == next_pass_row) {  // uniform: the block of outer rows moves on
+          ++pass;
+          const int64_t oi = pass * A.block + col;
+          lane_pos = (col < A.block && oi < A.no) ? A.opos[oi] : -1;
+          lane_values(A, F, lane_pos, lv);
+          next_pass_row += A.ni;
+        }
+        uint32_t cb = 0;
+#pragma unroll
+        for (int t = 0; t < kFastJoinTerms; ++t) {
+          if (t < A.nterms) {
+            const int32_t y = __builtin_amdgcn_readlane(rv[t], k);
+            bool lt, gt;
+            if (F.is_real[t]) {
+              const float xf = __int_as_float(lv[t]), yf = __int_as_float(y);
+              lt = xf < yf;
+              gt = xf > yf;
+              nan |= (lane_pos >= 0) && ((xf != xf) || (yf != yf));
+            } else {
+              lt = lv[t] < y;
+              gt = lv[t] > y;
+            }
+            const uint32_t m = F.mask[t];
+            const bool r = lt ? (m & 1u) : (gt ? (m & 4u) : (m & 2u));
+            cb |= r ? F.bit[t] : 0u;
+          }
+        }
+        const uint64_t b = __ballot(lane_pos >= 0 && cb == A.all_conj);
+        mine = lane == k ? b : mine;
+      }
+      if (lane < kmax) A.out[(r0 + lane) * A.words_per_row + w] = mine;
+    }
+  }
+  if (nan) atomicOr(A.nan, 1);
+}
+
 __global__ __launch_bounds__(kBlock) void k_join_decode(const int64_t* __restrict__ ids, const int64_t* __restrict__ n,
                                                         JoinDecode D) {
   const int64_t total = *n;
@@ -146,8 +255,41 @@ static int64_t grid_for(int64_t work, int64_t per_block, int64_t cap) {
 
 hipError_t launch_join_matrix(const JoinArgs& A, hipStream_t s) {
   if (A.nrows <= 0 || A.words_per_row <= 0) return hipSuccess;
-  // ~2048 blocks across the words of a row and the rows
+  bool fast = A.nterms <= kFastJoinTerms && !getenv("MBX_JOIN_PLAIN");
+  for (int t = 0; t < A.nterms; ++t) fast = fast && A.terms[t].kind != kStr;
   const int64_t gy = std::min<int64_t>(A.words_per_row, 65535);
+  if (fast) {
+    FastJoin F{};
+    for (int t = 0; t < A.nterms; ++t) {
+      const JoinTerm& T = A.terms[t];
+      // lanes: inner side (BMJ) / outer side (NLJ)
+      F.lane_col[t] = (const int32_t*)(A.mode == 0 ? T.icol : T.ocol);
+      F.row_col[t] = (const int32_t*)(A.mode == 0 ? T.ocol : T.icol);
+      F.is_real[t] = T.kind == kReal;
+      // outcome of cmp(outer, inner) per op
+      uint32_t m = 0;
+      switch (T.op) {
+        case kLT: m = 1; break;
+        case kLE: m = 3; break;
+        case kGT: m = 4; break;
+        case kGE: m = 6; break;
+        case kEQ: m = 2; break;
+        case kNE: m = 5; break;
+        default: m = 0;
+      }
+      // x = lane value: in BMJ x is the inner side, so mirror < and >
+      if (A.mode == 0) m = (m & 2u) | ((m & 1u) << 2) | ((m & 4u) >> 2);
+      F.mask[t] = m;
+      F.bit[t] = T.conj_bit;
+    }
+    const int64_t nchunks = (A.nrows + 63) / 64;
+    const int64_t want = std::max<int64_t>(1, 8192 / gy);
+    const int64_t gx = std::min<int64_t>(want, (nchunks + kWaves - 1) / kWaves);
+    hipLaunchKernelGGL(k_join_matrix_fast, dim3((unsigned)std::max<int64_t>(gx, 1), (unsigned)gy), dim3(kBlock), 0,
+                       s, A, F);
+    return hipGetLastError();
+  }
+  // ~2048 blocks across the words of a row and the rows
   const int64_t want = std::max<int64_t>(1, 2048 / gy);
   const int64_t gx = std::min<int64_t>(want, (A.nrows + kWaves - 1) / kWaves);
   hipLaunchKernelGGL(k_join_matrix, dim3((unsigned)std::max<int64_t>(gx, 1), (unsigned)gy), dim3(kBlock), 0, s, A);

@@ -340,16 +340,21 @@ __device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const u
 
 // per-tile body shared by every unroll depth: folds the CNF, applies deleted
 // rows and emits the requested output.
-template <int K, int KS, int MODE, bool DEL>
+// TQ > 0: the first TQ terms were hoisted into registers (th) before the
+// tile loop and the term loop is unrolled over them (nterms <= TQ); TQ = 0:
+// terms are read from the plan per tile.
+template <int K, int KS, int MODE, bool DEL, int TQ = 0>
 __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, KS>& D,
                                           int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
-                                          Acc& acc, uint64_t& wave_count) {
+                                          Acc& acc, uint64_t& wave_count, const KTerm* th = nullptr) {
   const int64_t nrows = L.nrows;
   const int64_t nwords = (nrows + 63) >> 6;
   const int64_t row0 = t * kTileRows + lane * 4;
   uint32_t cb[4] = {0u, 0u, 0u, 0u};
-  for (int ti = 0; ti < nterms; ++ti) {
-    const KTerm& T = P->terms[ti];
+#pragma unroll
+  for (int ti = 0; ti < (TQ > 0 ? TQ : nterms); ++ti) {
+    if (TQ > 0 && ti >= nterms) break;
+    const KTerm& T = TQ > 0 ? th[ti] : P->terms[ti];
     const int lhs = T.lhs;
     bool r[4];
     if (KS > 0 && T.kind == kStr) {
@@ -445,11 +450,107 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
 }
 
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4i gv4i;
+typedef __attribute__((address_space(1))) const int32_t gi32;
 
+// Column loads through global (address space 1) pointers: global_load, not
+// flat_load -- a flat load also counts on lgkmcnt, which forces a full
+// s_waitcnt before the first compare and so defeats the load pipeline below.
 template <bool NT>
 __device__ __forceinline__ v4i load16(const int32_t* p) {
-  if (NT) return __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
-  return *reinterpret_cast<const v4i*>(p);
+  gv4i* q = (gv4i*)p;
+  if (NT) return __builtin_nontemporal_load(q);
+  return *q;
+}
+
+__device__ __forceinline__ int32_t load4(const int32_t* p) { return *(gi32*)p; }
+
+// The full tiles base + u * ustep (u < U, below tf) of one wave into
+// registers.  Loads only, no else path: a branch that also wrote the
+// registers would make the compiler join the two and wait for the loads
+// right where they are issued.
+template <int K, int KS, int U, bool NT>
+__device__ __forceinline__ void load_tiles(TileRegs<K, KS> (&D)[U], int64_t base, int64_t ustep, int64_t tf,
+                                           const int32_t* const (&colp)[K > 0 ? K : 1],
+                                           const int32_t* const (&strp)[KS > 0 ? KS : 1], int lane) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t t = base + (int64_t)u * ustep;
+    if (t < tf) {
+#pragma unroll
+      for (int s = 0; s < K; ++s) {
+        const v4i q = load16<NT>(colp[s] + t * kTileRows + lane * 4);
+        D[u].v[s][0] = q.x;
+        D[u].v[s][1] = q.y;
+        D[u].v[s][2] = q.z;
+        D[u].v[s][3] = q.w;
+      }
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const v4i q = load16<NT>(strp[s] + (t * kTileRows + j * 64 + lane) * 4);
+          D[u].s[s][j][0] = (uint32_t)q.x;
+          D[u].s[s][j][1] = (uint32_t)q.y;
+          D[u].s[s][j][2] = (uint32_t)q.z;
+          D[u].s[s][j][3] = (uint32_t)q.w;
+        }
+    }
+  }
+}
+
+// Pipeline form: the same loads, unconditional -- a tile index past tf is
+// clamped to tf - 1 (a re-read of a tile in flight anyway, served by L2), so
+// every path issues the same number of loads and the waitcnt pass can wait
+// for exactly the older group (vmcnt(N)) instead of draining all loads.
+template <int K, int KS, int U, bool NT>
+__device__ __forceinline__ void load_tiles_clamped(TileRegs<K, KS> (&D)[U], int64_t base, int64_t ustep, int64_t tf,
+                                                   const int32_t* const (&colp)[K > 0 ? K : 1],
+                                                   const int32_t* const (&strp)[KS > 0 ? KS : 1], int lane) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    int64_t t = base + (int64_t)u * ustep;
+    t = t < tf ? t : tf - 1;
+#pragma unroll
+    for (int s = 0; s < K; ++s) {
+      const v4i q = load16<NT>(colp[s] + t * kTileRows + lane * 4);
+      D[u].v[s][0] = q.x;
+      D[u].v[s][1] = q.y;
+      D[u].v[s][2] = q.z;
+      D[u].v[s][3] = q.w;
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const v4i q = load16<NT>(strp[s] + (t * kTileRows + j * 64 + lane) * 4);
+        D[u].s[s][j][0] = (uint32_t)q.x;
+        D[u].s[s][j][1] = (uint32_t)q.y;
+        D[u].s[s][j][2] = (uint32_t)q.z;
+        D[u].s[s][j][3] = (uint32_t)q.w;
+      }
+  }
+}
+
+// The table's one partial tile t (rows t * 256 .. nrows - 1): guarded loads.
+template <int K, int KS>
+__device__ __forceinline__ void load_partial(TileRegs<K, KS>& D, int64_t t, int64_t nrows,
+                                             const int32_t* const (&colp)[K > 0 ? K : 1],
+                                             const int32_t* const (&strp)[KS > 0 ? KS : 1], int lane) {
+  const int64_t row0 = t * kTileRows + lane * 4;
+#pragma unroll
+  for (int s = 0; s < K; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) D.v[s][j] = row0 + j < nrows ? load4(colp[s] + row0 + j) : 0;
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t r = t * kTileRows + j * 64 + lane;
+        D.s[s][j][i] = r < nrows ? (uint32_t)load4(strp[s] + r * 4 + i) : 0u;
+      }
 }
 
 // U tiles per wave iteration: all loads of the U tiles are issued before the
@@ -459,7 +560,10 @@ __device__ __forceinline__ v4i load16(const int32_t* p) {
 // IL = true:  grid-stride interleave -- at any moment the whole grid reads one
 //   contiguous window of each column; partial counts are then per block, not
 //   per segment (COUNT / aggregate only).  Measured equal on MI355X.
-template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false>
+// PIPE = true: two register sets; the loads of the next U tiles are issued
+//   before the compares of the current ones, so a wave keeps its loads in
+//   flight while it computes.
+template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false, bool PIPE = false, int TQ = 0>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
@@ -484,54 +588,51 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   Acc acc;
   acc_init(acc);
   uint64_t wave_count = 0;
+  KTerm th[TQ > 0 ? TQ : 1];
+#pragma unroll
+  for (int ti = 0; ti < TQ; ++ti)
+    if (ti < nterms) th[ti] = P->terms[ti];
 
-  for (int64_t base = t0 + wave; base < t1; base += ustep * U) {
-    TileRegs<K, KS> D[U];
+  // full tiles in the main loop; the partial last tile (if any) after it
+  const int64_t tf = min(t1, nrows / kTileRows);
+  auto compute = [&](TileRegs<K, KS>(&D)[U], int64_t base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t t = base + (int64_t)u * ustep;
-      const int64_t row0 = t * kTileRows + lane * 4;
-      if (t < t1 && (t + 1) * kTileRows <= nrows) {
-#pragma unroll
-        for (int s = 0; s < K; ++s) {
-          const v4i q = load16<NT>(colp[s] + row0);
-          D[u].v[s][0] = q.x;
-          D[u].v[s][1] = q.y;
-          D[u].v[s][2] = q.z;
-          D[u].v[s][3] = q.w;
-        }
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const v4i q = load16<NT>(strp[s] + (t * kTileRows + j * 64 + lane) * 4);
-            D[u].s[s][j][0] = (uint32_t)q.x;
-            D[u].s[s][j][1] = (uint32_t)q.y;
-            D[u].s[s][j][2] = (uint32_t)q.z;
-            D[u].s[s][j][3] = (uint32_t)q.w;
-          }
-      } else {
-#pragma unroll
-        for (int s = 0; s < K; ++s)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) D[u].v[s][j] = (t < t1 && row0 + j < nrows) ? colp[s][row0 + j] : 0;
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int64_t r = t * kTileRows + j * 64 + lane;
-              D[u].s[s][j][i] = (t < t1 && r < nrows) ? (uint32_t)strp[s][r * 4 + i] : 0u;
-            }
+      if (t < tf)
+        fast_tile<K, KS, MODE, DEL, TQ>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+    }
+  };
+  const int64_t step = ustep * U;
+  if (!PIPE) {
+    for (int64_t base = t0 + wave; base < tf; base += step) {
+      TileRegs<K, KS> D[U];
+      load_tiles<K, KS, U, NT>(D, base, ustep, tf, colp, strp, lane);
+      compute(D, base);
+    }
+  } else {
+    TileRegs<K, KS> A[U], B[U];
+    int64_t base = t0 + wave;
+    if (base < tf) {
+      load_tiles_clamped<K, KS, U, NT>(A, base, ustep, tf, colp, strp, lane);
+      for (;;) {
+        const int64_t nb = base + step;
+        load_tiles_clamped<K, KS, U, NT>(B, nb, ustep, tf, colp, strp, lane);
+        compute(A, base);
+        if (nb >= tf) break;
+        const int64_t nb2 = nb + step;
+        load_tiles_clamped<K, KS, U, NT>(A, nb2, ustep, tf, colp, strp, lane);
+        compute(B, nb);
+        if (nb2 >= tf) break;
+        base = nb2;
       }
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t t = base + (int64_t)u * ustep;
-      if (t < t1)
-        fast_tile<K, KS, MODE, DEL>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count);
-    }
+  }
+  const int64_t tp = nrows / kTileRows;  // the partial tile, owned like any other tile of [t0, t1)
+  if ((nrows % kTileRows) != 0 && tp >= t0 + wave && tp < t1 && (tp - t0 - wave) % ustep == 0) {
+    TileRegs<K, KS> D;
+    load_partial<K, KS>(D, tp, nrows, colp, strp, lane);
+    fast_tile<K, KS, MODE, DEL, TQ>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
   }
   acc.count = lane == 0 ? (int64_t)wave_count : 0;
   block_reduce_store<MODE == kModeAgg>(acc, L);
@@ -958,6 +1059,53 @@ __global__ __launch_bounds__(kBlock) void k_index_build4(const int32_t* __restri
   }
 }
 
+// ------------------------------------------------------------ read probe
+//
+// The scan's load pattern with the predicate removed: the same 256-row tiles,
+// U tiles in flight per wave, non-temporal dwordx4 loads, the same segment
+// (or grid-stride) mapping; the words are XOR-folded and one word per block
+// is stored.  Its time is the read-bandwidth ceiling the scan is held to
+// ("measured read peak").
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_read_probe(ProbeArgs A) {
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  const int64_t ntiles = A.nrows / kTileRows;  // full tiles only
+  const bool il = A.interleave != 0;
+  const int64_t t0 = il ? (int64_t)blockIdx.x * kWaves : (int64_t)blockIdx.x * A.tiles_per_block;
+  const int64_t t1 = il ? ntiles : min(t0 + A.tiles_per_block, ntiles);
+  const int64_t ustep = il ? (int64_t)gridDim.x * kWaves : kWaves;
+  v4i acc = {0, 0, 0, 0};
+  for (int64_t base = t0 + wave; base < t1; base += ustep * U) {
+    v4i q[U][kMaxProbeCols];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t t = base + (int64_t)u * ustep;
+#pragma unroll
+      for (int c = 0; c < kMaxProbeCols; ++c)
+        q[u][c] = (t < t1 && c < A.ncols) ? load16<true>(A.cols[c] + t * kTileRows + lane * 4) : v4i{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < kMaxProbeCols; ++c) acc ^= q[u][c];
+  }
+  int32_t x = acc.x ^ acc.y ^ acc.z ^ acc.w;
+  for (int off = 32; off > 0; off >>= 1) x ^= __shfl_xor(x, off);
+  __shared__ int32_t red[kWaves];
+  if (lane == 0) red[wave] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) A.sink[blockIdx.x] = (uint32_t)(red[0] ^ red[1] ^ red[2] ^ red[3]);
+}
+
+hipError_t launch_read_probe(const ProbeArgs& A, hipStream_t s) {
+  const int64_t ntiles = A.nrows / kTileRows;
+  if (ntiles <= 0) return hipSuccess;
+  const int64_t g = A.interleave ? A.grid : (ntiles + A.tiles_per_block - 1) / A.tiles_per_block;
+  hipLaunchKernelGGL(k_read_probe<2>, dim3((unsigned)g), dim3(kBlock), 0, s, A);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- launchers
 
 constexpr int kDefaultU = 2;
@@ -994,6 +1142,27 @@ static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
       case 6: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 4, true>), grid, dim3(kBlock), 0, s, L); return;
       case 11:
         hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, true>), grid, dim3(kBlock), 0, s, L);
+        return;
+      case 12:  // software-pipelined U=2
+        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, true>), grid, dim3(kBlock), 0, s, L);
+        return;
+      case 13:  // software-pipelined U=1
+        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 1, true, false, true>), grid, dim3(kBlock), 0, s, L);
+        return;
+      case 15:  // terms hoisted into registers
+        if (L.nterms_host <= 4) {
+          hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, false, 4>), grid, dim3(kBlock), 0, s, L);
+          return;
+        }
+        break;
+      case 16:  // terms hoisted + grid-stride interleave
+        if (L.nterms_host <= 4) {
+          hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, true, false, 4>), grid, dim3(kBlock), 0, s, L);
+          return;
+        }
+        break;
+      case 14:  // software-pipelined U=4
+        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 4, true, false, true>), grid, dim3(kBlock), 0, s, L);
         return;
       default: break;
     }

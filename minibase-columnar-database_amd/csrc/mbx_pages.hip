@@ -171,31 +171,71 @@ __device__ __forceinline__ bool rows_equal(const KCol& c, int64_t a, int64_t b) 
   return true;
 }
 
-__global__ __launch_bounds__(kBlock) void k_distinct(DistinctArgs A) {
-  // keys / minpos are written only through atomics; every read below may be
-  // stale (see the loop) but never wrong
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
+// Global table insert of `row`: find or claim the slot of its value, lower
+// the slot's first position to `row`.  keys / minpos are written only through
+// atomics; plain (cached) reads may be stale but never wrong: a stale EMPTY
+// only sends the row to the CAS, a stale minimum costs one more atomicMin.
+__device__ __forceinline__ void distinct_insert(const DistinctArgs& A, int64_t row, uint64_t h) {
   const uint64_t mask = (uint64_t)A.cap - 1;
-  for (int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x; row < A.nrows; row += stride) {
+  h &= mask;
+  for (int64_t probe = 0; probe < A.cap; ++probe, h = (h + 1) & mask) {
+    unsigned long long k = A.keys[h];
+    if (k == kEmptySlot) {
+      k = atomicCAS(A.keys + h, kEmptySlot, (unsigned long long)row);
+      if (k == kEmptySlot) k = (unsigned long long)row;
+    }
+    if (rows_equal(A.col, (int64_t)k, row)) {
+      if ((unsigned long long)row < A.minpos[h]) atomicMin(A.minpos + h, (unsigned long long)row);
+      return;
+    }
+  }
+  atomicOr(A.overflow, 1);
+}
+
+// Two levels: each block first folds its rows into an LDS table (value ->
+// smallest row of the block with it), so a low-cardinality column touches
+// the global table once per value per block instead of once per row; rows
+// whose value finds no LDS slot within kLdsProbes go to the global table
+// directly (A.lds_probes, kLdsProbes by default).  4-byte columns keep the value itself as the LDS key (no column
+// re-reads); wider ones keep a representative row.
+constexpr int kLdsSlots = 2048;
+
+template <bool V1>
+__global__ __launch_bounds__(kBlock) void k_distinct(DistinctArgs A, int64_t rows_per_block) {
+  __shared__ unsigned long long skey[kLdsSlots];
+  __shared__ unsigned long long smin[kLdsSlots];
+  for (int i = threadIdx.x; i < kLdsSlots; i += kBlock) {
+    skey[i] = kEmptySlot;
+    smin[i] = kEmptySlot;
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(r0 + rows_per_block, A.nrows);
+  for (int64_t row = r0 + threadIdx.x; row < r1; row += kBlock) {
     if (A.del && ((A.del[row >> 6] >> (row & 63)) & 1ull)) continue;
-    uint64_t h = row_hash(A.col, row) & mask;
+    const uint64_t h = row_hash(A.col, row);
+    const unsigned long long mine =
+        V1 ? (unsigned long long)((const uint32_t*)A.col.base)[row] : (unsigned long long)row;
+    uint32_t slot = (uint32_t)h & (kLdsSlots - 1);
     bool placed = false;
-    for (int64_t probe = 0; probe < A.cap; ++probe, h = (h + 1) & mask) {
-      // plain (cached) reads: a stale EMPTY only sends the row to the CAS,
-      // a stale minimum only costs one more atomicMin -- both still exact
-      unsigned long long k = A.keys[h];
+    for (int probe = 0; probe < A.lds_probes; ++probe, slot = (slot + 1) & (kLdsSlots - 1)) {
+      unsigned long long k = skey[slot];
       if (k == kEmptySlot) {
-        k = atomicCAS(A.keys + h, kEmptySlot, (unsigned long long)row);
-        if (k == kEmptySlot) k = (unsigned long long)row;
+        k = atomicCAS(skey + slot, kEmptySlot, mine);
+        if (k == kEmptySlot) k = mine;
       }
-      if (rows_equal(A.col, (int64_t)k, row)) {
-        const unsigned long long m = A.minpos[h];
-        if ((unsigned long long)row < m) atomicMin(A.minpos + h, (unsigned long long)row);
+      if (V1 ? k == mine : rows_equal(A.col, (int64_t)k, row)) {
+        atomicMin(smin + slot, (unsigned long long)row);
         placed = true;
         break;
       }
     }
-    if (!placed) atomicOr(A.overflow, 1);
+    if (!placed) distinct_insert(A, row, h);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kLdsSlots; i += kBlock) {
+    const unsigned long long row = smin[i];
+    if (row != kEmptySlot) distinct_insert(A, (int64_t)row, row_hash(A.col, (int64_t)row));
   }
 }
 
@@ -211,9 +251,15 @@ __global__ __launch_bounds__(kBlock) void k_rows_fetch(KCol c, const int64_t* __
 
 hipError_t launch_distinct(const DistinctArgs& A, hipStream_t s) {
   if (A.nrows <= 0) return hipSuccess;
-  int64_t g = (A.nrows + kBlock - 1) / kBlock;
-  if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(k_distinct, dim3((unsigned)g), dim3(kBlock), 0, s, A);
+  // ~1024 blocks of contiguous row ranges (multiples of the block size)
+  int64_t rpb = (A.nrows + 1023) / 1024;
+  rpb = (rpb + kBlock - 1) / kBlock * kBlock;
+  if (rpb < 4 * kBlock) rpb = 4 * kBlock;
+  const int64_t g = (A.nrows + rpb - 1) / rpb;
+  if (A.col.stride_w == 1)
+    hipLaunchKernelGGL(k_distinct<true>, dim3((unsigned)g), dim3(kBlock), 0, s, A, rpb);
+  else
+    hipLaunchKernelGGL(k_distinct<false>, dim3((unsigned)g), dim3(kBlock), 0, s, A, rpb);
   return hipGetLastError();
 }
 

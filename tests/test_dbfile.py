@@ -367,6 +367,49 @@ def test_bitmap_index_large_and_deleted(m, ctx, tmp_path):
         assert np.array_equal(w[:k], w_o[:k]) and not w[k:].any()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("lds_probes", [None, "0", "1"])
+def test_bitmap_index_many_values(m, ctx, tmp_path, monkeypatch, lds_probes):
+    """k_distinct with thousands of distinct values: blocks whose LDS table
+    overflows (and, with MBX_DISTINCT_LDS_PROBES=0 / 1, rows sent to the global
+    table directly or after one LDS probe) still give every live value once, in
+    first-live-occurrence order; BitMapFiles of sampled values equal the
+    oracle's.  All values print at one width, so the .hdr registry records are
+    equal-sized and Heapfile's first-fit insert keeps them in insertion order
+    (with mixed widths a shorter later record can fill an earlier page)."""
+    if lds_probes is not None:
+        monkeypatch.setenv("MBX_DISTINCT_LDS_PROBES", lds_probes)
+    path = str(tmp_path / "db")
+    n = 40_000
+    rng = np.random.Generator(np.random.PCG64(31))
+    vals = rng.integers(1000, 4000, n, dtype=np.int32)
+    pool = [f"v{k:04d}" for k in range(1200)]
+    svals = [pool[i] for i in rng.integers(0, len(pool), n)]
+    cols = [(oracle.INTEGER, 4, vals), (oracle.STRING, 8, helpers.encode_strings(svals, 8))]
+    with m.mbx.Db(path, 1 << 17) as db:
+        db.columnar_create("cf", [(oracle.INTEGER, 4), (oracle.STRING, 8)], ["v", "s"])
+        db.columnar_insert("cf", cols)
+        dead = sorted(set(int(x) for x in rng.integers(0, n, 300)))
+        db.mark_deleted_many("cf", dead)
+        t = ctx.stage_db(db, "cf")
+        live = np.ones(n, dtype=bool)
+        live[dead] = False
+        want_i = first_occurrence(vals[live].tolist())
+        want_s = first_occurrence([s for s, l in zip(svals, live) if l])
+        assert ctx.create_bitmap_index(db, "cf", t, 0) == len(want_i) > 2048
+        assert ctx.create_bitmap_index(db, "cf", t, 1) == len(want_s) == 1200
+        assert db.bitmap_values("cf", 0) == [str(v).encode() for v in want_i]
+        assert db.bitmap_values("cf", 1) == [v.encode() for v in want_s]
+        for v in want_i[::97]:
+            w = db.bitmap_read(f"cf.bm.0.{v}")
+            pos = np.nonzero((vals == v) & live)[0]
+            assert list(oracle.words_to_positions(w)) == list(pos), v
+        for v in want_s[::53]:
+            w = db.bitmap_read(f"cf.bm.1.{v}")
+            pos = np.nonzero(np.array([s == v for s in svals]) & live)[0]
+            assert list(oracle.words_to_positions(w)) == list(pos), v
+
+
 def test_purge_all_deleted_tuples(m, tmp_path):
     """Columnarfile.purgeAllDeletedTuples (R/columnar/Columnarfile.java:837-925)
     on a 3 x int32 file spanning 4 directory pages per column: a whole

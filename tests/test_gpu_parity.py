@@ -472,3 +472,21 @@ def test_c5_shard_full_size(ctx):
     neg = [[(oracle.GE, ("sym", 1), ("int", 1 << 19)), (oracle.LT, ("sym", 2), ("real", 0.25)),
             (oracle.LT, ("sym", 3), ("str", "M"))]]
     assert ctx.scan_count(plan) + ctx.scan_count(ctx.compile(t, neg)) == n
+
+
+@pytest.mark.gpu
+def test_probe_read_runs_and_checks_arguments(m, ctx):
+    """mbx_probe_read (bench.py's secondary roofline denominator) launches on
+    4-byte columns in every mapping and rejects what it cannot read."""
+    n = 1 << 20
+    cols = [(oracle.INTEGER, 4, np.arange(n, dtype=np.int32)), (oracle.REAL, 4, np.ones(n, np.float32)),
+            (oracle.STRING, 16, helpers.encode_strings(["ab"] * n, 16))]
+    t = ctx.stage(cols)
+    ctx.probe_read(t, [0, 1])
+    ctx.probe_read(t, [0], tiles_per_block=3)
+    ctx.probe_read(t, [1, 0, 1, 0], interleave=True, grid=64)
+    ctx.sync()
+    for bad in ([2], [], [0, 1, 0, 1, 0], [7]):
+        with pytest.raises(m.MbxError) as e:
+            ctx.probe_read(t, bad)
+        assert e.value.code == m.mbx.E_INVALID

@@ -187,3 +187,63 @@ def test_gpu_join_edges(m, ctx):
     with pytest.raises(m.MbxError) as e:
         ctx.join(t, full, s, full, [[(m.mbx.EQ, 0, 0)]], m.mbx.JOIN_BMJ)
     assert e.value.code == m.mbx.E_TYPE
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["bmj", "nlj"])
+@pytest.mark.parametrize("jc", ["{(x,<=,x)}^{(f,>,f)|(y,=,y)}", "{(x,!=,y)}^{(f,>=,f)}^{(y,<,x)|(x,=,y)}", "{(x,=,x)}",
+                                "{(x,!=,y)}^{(f,>=,f)}^{(y,<,x)|(x,=,y)}^{(f,<,f)|(x,>,x)}"])
+def test_gpu_join_numeric_fast_path(m, ctx, order, jc, monkeypatch):
+    """CNFs of <= 4 int / float terms take k_join_matrix_fast (row side swept
+    by v_readlane; the 6-term CNF stays on the plain kernel).  Ragged selections (not multiples of 64) and an NLJ block
+    whose passes start inside a 64-row chunk; pairs == oracle pairs and ==
+    the plain kernel (MBX_JOIN_PLAIN)."""
+    rng = np.random.Generator(np.random.PCG64(len(jc) + (order == "nlj")))
+    no, ni = 1500, 1300
+
+    def table(n):
+        return [(oracle.INTEGER, 4, rng.integers(-20, 20, n, dtype=np.int32)),
+                (oracle.REAL, 4, (rng.integers(-10, 10, n) * 0.25).astype(np.float32)),
+                (oracle.INTEGER, 4, rng.integers(-20, 20, n, dtype=np.int32))]
+    oc, ic = table(no), table(ni)
+    O = joins.Rel("o", ["x", "f", "y"], oracle.Table(oc))
+    I = joins.Rel("i", ["x", "f", "y"], oracle.Table(ic))
+    osel = sorted(int(p) for p in rng.choice(no, 333, replace=False))
+    isel = sorted(int(p) for p in rng.choice(ni, 203, replace=False))   # 203 = 3 * 64 + 11
+    block = 45
+    cnf = joins.parse_cnf(jc)
+    want = []
+    if order == "bmj":
+        want = [(o, i, 0) for o in osel for i in isel if joins.join_ok(O, I, cnf, o, i)]
+    else:
+        for p in range((len(osel) + block - 1) // block):
+            for i in isel:
+                want += [(o, i, p) for o in osel[p * block:(p + 1) * block] if joins.join_ok(O, I, cnf, o, i)]
+    to, ti = ctx.stage(oc), ctx.stage(ic)
+    so, si = ctx.bitmap_upload(no, words_of(osel, no)), ctx.bitmap_upload(ni, words_of(isel, ni))
+    kind = m.mbx.JOIN_BMJ if order == "bmj" else m.mbx.JOIN_NLJ
+    op_, ip_, ps, _ = ctx.join(to, so, ti, si, join_cnf(O, I, jc), kind, block)
+    got = list(zip(op_.tolist(), ip_.tolist(), ps.tolist()))
+    assert got == want
+    monkeypatch.setenv("MBX_JOIN_PLAIN", "1")
+    op_, ip_, ps, _ = ctx.join(to, so, ti, si, join_cnf(O, I, jc), kind, block)
+    assert list(zip(op_.tolist(), ip_.tolist(), ps.tolist())) == got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("plain", [False, True])
+def test_gpu_join_float_nan_raises(m, ctx, monkeypatch, plain):
+    """A NaN reaching a float join compare is an error (TupleUtils' float
+    branch falls through), in both kernels; NaN outside the selections is not."""
+    if plain:
+        monkeypatch.setenv("MBX_JOIN_PLAIN", "1")
+    f = np.arange(100, dtype=np.float32)
+    f[70] = np.nan
+    t = ctx.stage([(oracle.REAL, 4, f)])
+    some = ctx.bitmap_upload(100, words_of(range(60), 100))
+    op_, _, _, _ = ctx.join(t, some, t, some, [[(m.mbx.EQ, 0, 0)]], m.mbx.JOIN_NLJ, 7)
+    assert list(op_) == list(range(60))
+    full = ctx.bitmap_upload(100, words_of(range(100), 100))
+    with pytest.raises(m.MbxError) as e:
+        ctx.join(t, full, t, some, [[(m.mbx.LT, 0, 0)]], m.mbx.JOIN_BMJ)
+    assert e.value.code == m.mbx.E_TYPE
