@@ -705,6 +705,10 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   const char* var = getenv("MBX_SCAN_VARIANT");
   L.variant = var ? atoi(var) : 0;
   L.nterms_host = p->host.nterms;
+  {
+    const char* mf = getenv("MBX_SCAN_HOIST");  // 0: terms read from the plan per tile (A/B tuning)
+    L.hoist_terms = p->host.nterms >= 1 && p->host.nterms <= kHoistTerms && !(mf && mf[0] == '0');
+  }
   const char* fm = getenv("MBX_FIN_MODE");
   L.fin_mode = fm ? atoi(fm) : kFinWriteThrough;
   if (L.fin_mode == kFinSeparate) L.ticket = nullptr;

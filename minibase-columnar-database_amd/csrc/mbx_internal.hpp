@@ -18,6 +18,7 @@
 
 namespace mbx {
 
+constexpr int kHoistTerms = 4;        // literal terms the fast scan hoists into registers
 constexpr int kTileRows = 256;       // rows per wave tile
 constexpr int kWordsPerTile = 4;     // bitmap words per tile
 constexpr int kBlock = 256;          // threads per block (4 waves)
@@ -114,6 +115,7 @@ struct ScanLaunch {
   int32_t* nan_out;           // device or null
   int32_t variant;            // 0: default kernel; >0: tuning variant (MBX_SCAN_VARIANT)
   int32_t nterms_host;        // the plan's term count, for launch-time kernel choice
+  int32_t hoist_terms;        // 1..kHoistTerms literal terms: hoisted into registers
   int32_t fin_mode;           // FinMode (MBX_FIN_MODE): how the last block sees the partials
 };
 

@@ -256,7 +256,12 @@ static int64_t grid_for(int64_t work, int64_t per_block, int64_t cap) {
 hipError_t launch_join_matrix(const JoinArgs& A, hipStream_t s) {
   if (A.nrows <= 0 || A.words_per_row <= 0) return hipSuccess;
   bool fast = A.nterms <= kFastJoinTerms && !getenv("MBX_JOIN_PLAIN");
-  for (int t = 0; t < A.nterms; ++t) fast = fast && A.terms[t].kind != kStr;
+  uint32_t covered = 0;  // an empty conjunct is never true: leave it to the plain kernel
+  for (int t = 0; t < A.nterms; ++t) {
+    fast = fast && A.terms[t].kind != kStr;
+    covered |= A.terms[t].conj_bit;
+  }
+  fast = fast && covered == A.all_conj;
   const int64_t gy = std::min<int64_t>(A.words_per_row, 65535);
   if (fast) {
     FastJoin F{};

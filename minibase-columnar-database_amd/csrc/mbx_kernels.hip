@@ -158,18 +158,41 @@ __device__ __forceinline__ Partial load_partial_sc1(const Partial* src) {
   return p;
 }
 
+// COUNT / BitSet scans (no aggregate): only the count and nan words of a
+// Partial are stored and read back -- 2 of its 6 words
+__device__ __forceinline__ void store_count_sc1(Partial* dst, const Partial& p) {
+  const uint64_t* s = reinterpret_cast<const uint64_t*>(&p);
+  uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+  __hip_atomic_store(d, s[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(d + kSegStride - 1, s[kSegStride - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ Acc load_count_sc1(const Partial* src) {
+  uint64_t* s = reinterpret_cast<uint64_t*>(const_cast<Partial*>(src));
+  Partial p;
+  uint64_t* d = reinterpret_cast<uint64_t*>(&p);
+  d[0] = __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  d[kSegStride - 1] = __hip_atomic_load(s + kSegStride - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  Acc b;
+  acc_init(b);
+  b.count = p.count;
+  b.nan = p.nan_seen;
+  return b;
+}
+
 // Reduce n partials with one block in a fixed order (thread i folds i, i+256,
 // ... sequentially, then a fixed xor tree and wave order) and write the
 // results.  Bit-reproducible for a given grid.  SC1: the partials were
-// stored write-through in this launch and are read with sc1 loads.
-template <bool SC1>
+// stored write-through in this launch and are read with sc1 loads; LITE: only
+// their count and nan words were stored.
+template <bool SC1, bool LITE = false>
 __device__ __forceinline__ void finalize_block(const Partial* parts, int64_t n, int32_t agg_kind, AggOut* out,
                                                int64_t* count_out, int32_t* nan_flag) {
   __shared__ Acc fsh[kWaves];
   Acc a;
   acc_init(a);
   for (int64_t i = threadIdx.x; i < n; i += kBlock)
-    acc_merge(a, from_partial(SC1 ? load_partial_sc1(parts + i) : parts[i]));
+    acc_merge(a, LITE ? load_count_sc1(parts + i) : from_partial(SC1 ? load_partial_sc1(parts + i) : parts[i]));
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
     Acc b = shfl_xor_acc(a, m);
@@ -265,7 +288,10 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
     if (L.ticket && L.fin_mode == kFinWriteThrough) {
       // write-through (sc1) partial, drained, then the ticket: no L2
       // write-back fence needed (MI355X_MICROARCH.md, Valid forms row 1)
-      store_partial_sc1(L.partials + blockIdx.x, p);
+      if (FULL)
+        store_partial_sc1(L.partials + blockIdx.x, p);
+      else
+        store_count_sc1(L.partials + blockIdx.x, p);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       is_last = arrive(L.ticket, L.ticket_groups);
     } else if (L.ticket) {
@@ -286,7 +312,7 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
   __syncthreads();
   if (is_last) {
     if (L.fin_mode == kFinWriteThrough)
-      finalize_block<true>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
+      finalize_block<true, !FULL>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
     else
       finalize_block<false>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
   }
@@ -353,7 +379,7 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
   uint32_t cb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int ti = 0; ti < (TQ > 0 ? TQ : nterms); ++ti) {
-    if (TQ > 0 && ti >= nterms) break;
+    if (TQ > 0 && ti > 0 && ti >= nterms) break;  // TQ > 0 implies nterms >= 1
     const KTerm& T = TQ > 0 ? th[ti] : P->terms[ti];
     const int lhs = T.lhs;
     bool r[4];
@@ -449,6 +475,141 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
   }
 }
 
+// Hoisted literal-term program for the mask form of the tile body: per term
+// the slot, the literal, the outcome mask {a<lit, a==lit, a>lit} of its
+// operator and whether it opens a conjunct (terms come conjunct by conjunct
+// from the plan compiler).
+struct TermProg {
+  int32_t lhs;
+  int32_t is_real;
+  int32_t ilit;
+  float flit;
+  uint64_t m_lt, m_eq, m_gt;  // all-ones / zero lane masks
+  int32_t first;
+};
+
+__device__ __forceinline__ uint32_t outcome_mask(int op) {
+  switch (op) {
+    case kLT: return 1u;
+    case kLE: return 3u;
+    case kGT: return 4u;
+    case kGE: return 6u;
+    case kEQ: return 2u;
+    case kNE: return 5u;
+    default: return 0u;
+  }
+}
+
+// Mask form (KS == 0, <= TQ hoisted literal terms): every compare's wave
+// ballot is a lane mask in SGPRs (bit l = row 4l + j of the tile); operator,
+// OR within a conjunct and AND across conjuncts run on the scalar unit, so a
+// term costs 2 v_cmp per row group and no branches on the operator.
+template <int K, int MODE, bool DEL, int TQ>
+__device__ __forceinline__ void mask_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, 0>& D,
+                                          int64_t t, int lane, int nterms, bool cnf_live, bool partial, bool tile_valid,
+                                          const TermProg (&tp)[TQ], int agg_slot, bool agg_real, Acc& acc,
+                                          uint64_t& wave_count) {
+  const int64_t nrows = L.nrows;
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t row0 = t * kTileRows + lane * 4;
+  uint64_t word[4], cur[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    word[j] = cnf_live && tile_valid ? ~0ull : 0ull;
+    cur[j] = 0ull;
+  }
+#pragma unroll
+  for (int ti = 0; ti < TQ; ++ti) {
+    if (ti > 0 && ti >= nterms) break;  // nterms >= 1: term 0 always runs (keeps the loads unsunk)
+    const TermProg& T = tp[ti];
+    int32_t a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
+#pragma unroll
+    for (int s = 1; s < K; ++s)
+      if (T.lhs == s) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
+      }
+    if (T.first && ti > 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        word[j] &= cur[j];
+        cur[j] = 0ull;
+      }
+    }
+    uint64_t lt[4], gt[4];
+    if (T.is_real) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float f = __int_as_float(a[j]);
+        lt[j] = __ballot(f < T.flit);
+        gt[j] = __ballot(f > T.flit);
+        acc.nan |= (f != f) && tile_valid && (!partial || row0 + j < nrows);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lt[j] = __ballot(a[j] < T.ilit);
+        gt[j] = __ballot(a[j] > T.ilit);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cur[j] |= (lt[j] & T.m_lt) | (~(lt[j] | gt[j]) & T.m_eq) | (gt[j] & T.m_gt);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) word[j] &= cur[j];
+  if (partial) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) word[j] &= __ballot(row0 + j < nrows);
+  }
+  const int64_t wd = t * kWordsPerTile + (lane >> 4);
+  if (DEL) {
+    const uint64_t dw = wd < nwords ? L.deleted[wd] : 0ull;
+    const uint32_t dn = (uint32_t)(dw >> ((lane & 15) * 4)) & 0xFu;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) word[j] &= ~__ballot((dn >> j) & 1u);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wave_count += __popcll(word[j]);
+  if (MODE == kModeBitmap || MODE == kModeAgg) {
+    bool p[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[j] = (word[j] >> lane) & 1ull;
+    if (MODE == kModeBitmap) {
+      const uint32_t nib = (uint32_t)p[0] | ((uint32_t)p[1] << 1) | ((uint32_t)p[2] << 2) | ((uint32_t)p[3] << 3);
+      const uint64_t w = pack_word16(nib, lane);
+      if (tile_valid && (lane & 15) == 0 && wd < nwords) L.out_words[wd] = w;
+    } else if (K > 0) {
+      int32_t g[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) g[j] = D.v[0][j];
+#pragma unroll
+      for (int s = 1; s < K; ++s)
+        if (agg_slot == s) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) g[j] = D.v[s][j];
+        }
+      if (agg_real) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float f = __int_as_float(g[j]);
+          acc.fsum += p[j] ? (double)f : 0.0;
+          acc.fmin = p[j] && f < acc.fmin ? f : acc.fmin;
+          acc.fmax = p[j] && f > acc.fmax ? f : acc.fmax;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc.isum += p[j] ? (int64_t)g[j] : 0;
+          acc.imin = p[j] && g[j] < acc.imin ? g[j] : acc.imin;
+          acc.imax = p[j] && g[j] > acc.imax ? g[j] : acc.imax;
+        }
+      }
+    }
+  }
+}
+
 typedef int32_t v4i __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const v4i gv4i;
 typedef __attribute__((address_space(1))) const int32_t gi32;
@@ -499,7 +660,7 @@ __device__ __forceinline__ void load_tiles(TileRegs<K, KS> (&D)[U], int64_t base
   }
 }
 
-// Pipeline form: the same loads, unconditional -- a tile index past tf is
+// Clamped form: the same loads, unconditional -- a tile index past tf is
 // clamped to tf - 1 (a re-read of a tile in flight anyway, served by L2), so
 // every path issues the same number of loads and the waitcnt pass can wait
 // for exactly the older group (vmcnt(N)) instead of draining all loads.
@@ -560,10 +721,8 @@ __device__ __forceinline__ void load_partial(TileRegs<K, KS>& D, int64_t t, int6
 // IL = true:  grid-stride interleave -- at any moment the whole grid reads one
 //   contiguous window of each column; partial counts are then per block, not
 //   per segment (COUNT / aggregate only).  Measured equal on MI355X.
-// PIPE = true: two register sets; the loads of the next U tiles are issued
-//   before the compares of the current ones, so a wave keeps its loads in
-//   flight while it computes.
-template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false, bool PIPE = false, int TQ = 0>
+// TQ > 0: the mask form (mask_tile) over <= TQ hoisted literal terms.
+template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false, int TQ = 0, bool MB = true>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
@@ -592,6 +751,30 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
 #pragma unroll
   for (int ti = 0; ti < TQ; ++ti)
     if (ti < nterms) th[ti] = P->terms[ti];
+  constexpr bool kMask = TQ > 0 && KS == 0 && MB;
+  TermProg tprog[TQ > 0 ? TQ : 1];
+  bool cnf_live = true;
+  if (kMask) {
+    uint32_t covered = 0, prev = 0;
+#pragma unroll
+    for (int ti = 0; ti < TQ; ++ti) {
+      if (ti < nterms) {
+        const KTerm& T = th[ti];
+        const uint32_t m = outcome_mask(T.op);
+        tprog[ti].lhs = T.lhs;
+        tprog[ti].is_real = T.kind == kReal;
+        tprog[ti].ilit = T.ilit;
+        tprog[ti].flit = T.flit;
+        tprog[ti].m_lt = (m & 1u) ? ~0ull : 0ull;
+        tprog[ti].m_eq = (m & 2u) ? ~0ull : 0ull;
+        tprog[ti].m_gt = (m & 4u) ? ~0ull : 0ull;
+        tprog[ti].first = T.conj_bit != prev;
+        prev = T.conj_bit;
+        covered |= T.conj_bit;
+      }
+    }
+    cnf_live = covered == all;  // a conjunct without a live term is never true
+  }
 
   // full tiles in the main loop; the partial last tile (if any) after it
   const int64_t tf = min(t1, nrows / kTileRows);
@@ -599,40 +782,38 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t t = base + (int64_t)u * ustep;
-      if (t < tf)
+      if constexpr (kMask) {
+        // unconditional: a clamped (duplicate) tile is evaluated with an empty
+        // result and writes nothing, so no branch separates the loads from
+        // their compares
+        const bool valid = t < tf;
+        mask_tile<K, MODE, DEL, (TQ > 0 ? TQ : 1)>(L, P, D[u], valid ? t : tf - 1, lane, nterms, cnf_live, false,
+                                                   valid, tprog, agg_slot, agg_real, acc, wave_count);
+      } else if (t < tf) {
         fast_tile<K, KS, MODE, DEL, TQ>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+      }
     }
   };
   const int64_t step = ustep * U;
-  if (!PIPE) {
+  {
     for (int64_t base = t0 + wave; base < tf; base += step) {
       TileRegs<K, KS> D[U];
-      load_tiles<K, KS, U, NT>(D, base, ustep, tf, colp, strp, lane);
+      if (TQ > 0)  // every path issues all U loads: exact vmcnt waits
+        load_tiles_clamped<K, KS, U, NT>(D, base, ustep, tf, colp, strp, lane);
+      else
+        load_tiles<K, KS, U, NT>(D, base, ustep, tf, colp, strp, lane);
       compute(D, base);
-    }
-  } else {
-    TileRegs<K, KS> A[U], B[U];
-    int64_t base = t0 + wave;
-    if (base < tf) {
-      load_tiles_clamped<K, KS, U, NT>(A, base, ustep, tf, colp, strp, lane);
-      for (;;) {
-        const int64_t nb = base + step;
-        load_tiles_clamped<K, KS, U, NT>(B, nb, ustep, tf, colp, strp, lane);
-        compute(A, base);
-        if (nb >= tf) break;
-        const int64_t nb2 = nb + step;
-        load_tiles_clamped<K, KS, U, NT>(A, nb2, ustep, tf, colp, strp, lane);
-        compute(B, nb);
-        if (nb2 >= tf) break;
-        base = nb2;
-      }
     }
   }
   const int64_t tp = nrows / kTileRows;  // the partial tile, owned like any other tile of [t0, t1)
   if ((nrows % kTileRows) != 0 && tp >= t0 + wave && tp < t1 && (tp - t0 - wave) % ustep == 0) {
     TileRegs<K, KS> D;
     load_partial<K, KS>(D, tp, nrows, colp, strp, lane);
-    fast_tile<K, KS, MODE, DEL, TQ>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+    if constexpr (kMask)
+      mask_tile<K, MODE, DEL, (TQ > 0 ? TQ : 1)>(L, P, D, tp, lane, nterms, cnf_live, true, true, tprog, agg_slot,
+                                                 agg_real, acc, wave_count);
+    else
+      fast_tile<K, KS, MODE, DEL, TQ>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
   }
   acc.count = lane == 0 ? (int64_t)wave_count : 0;
   block_reduce_store<MODE == kModeAgg>(acc, L);
@@ -1131,8 +1312,18 @@ int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block) {
 
 template <int K, int KS, int MODE>
 static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
+  // 4-byte slots only and 1..kHoistTerms literal terms (L.hoist_terms): the terms
+  // are hoisted into registers (TQ) and the per-row tile body is unrolled over
+  // them -- measured 2.5 % faster than reading them from the plan per tile
+  // and than the SGPR-mask body (variant 16), profiles/r01/an3
+  constexpr int TQ = KS == 0 ? kHoistTerms : 0;
+  const bool hoist = KS == 0 && L.hoist_terms;
   if (L.deleted) {
-    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, true, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
+    if (hoist)
+      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, true, kDefaultU, kDefaultNT, false, TQ, false>), grid,
+                         dim3(kBlock), 0, s, L);
+    else
+      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, true, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
     return;
   }
   if constexpr (K == 2 && KS == 0 && MODE == kModeCount) {  // tuning variants of the C3 kernel
@@ -1140,34 +1331,26 @@ static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
       case 1: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 1, false>), grid, dim3(kBlock), 0, s, L); return;
       case 4: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 1, true>), grid, dim3(kBlock), 0, s, L); return;
       case 6: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 4, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 11:
+      case 11:  // per-row form, grid-stride interleave
         hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, true>), grid, dim3(kBlock), 0, s, L);
         return;
-      case 12:  // software-pipelined U=2
-        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, true>), grid, dim3(kBlock), 0, s, L);
+      case 12:  // per-row form, U=2 (the round-B kernel)
+        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true>), grid, dim3(kBlock), 0, s, L);
         return;
-      case 13:  // software-pipelined U=1
-        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 1, true, false, true>), grid, dim3(kBlock), 0, s, L);
-        return;
-      case 15:  // terms hoisted into registers
-        if (L.nterms_host <= 4) {
-          hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, false, 4>), grid, dim3(kBlock), 0, s, L);
+      case 16:  // mask form (mask_tile): CNF on SGPR lane masks
+        if (hoist) {
+          hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, TQ, true>), grid, dim3(kBlock), 0, s, L);
           return;
         }
         break;
-      case 16:  // terms hoisted + grid-stride interleave
-        if (L.nterms_host <= 4) {
-          hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, true, false, 4>), grid, dim3(kBlock), 0, s, L);
-          return;
-        }
-        break;
-      case 14:  // software-pipelined U=4
-        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 4, true, false, true>), grid, dim3(kBlock), 0, s, L);
-        return;
       default: break;
     }
   }
-  hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
+  if (hoist)
+    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, kDefaultU, kDefaultNT, false, TQ, false>), grid, dim3(kBlock),
+                       0, s, L);
+  else
+    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
 }
 
 // fast_k = number of 4-byte slots, fast_ks = number of 16-byte string slots;

@@ -17,7 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--launches", type=int, default=50)
-    ap.add_argument("--variants", default="0,11,15,16")
+    ap.add_argument("--variants", default="0,12,16,17")
     args = ap.parse_args()
     import torch
     import mbx_pkg
