@@ -708,6 +708,8 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   {
     const char* mf = getenv("MBX_SCAN_HOIST");  // 0: terms read from the plan per tile (A/B tuning)
     L.hoist_terms = p->host.nterms >= 1 && p->host.nterms <= kHoistTerms && !(mf && mf[0] == '0');
+    L.diag_terms = L.hoist_terms && v.fast_ks == 0 && p->host.nterms == v.fast_k;
+    for (int i = 0; i < p->host.nterms && L.diag_terms; ++i) L.diag_terms = p->host.terms[i].lhs == i;
   }
   const char* fm = getenv("MBX_FIN_MODE");
   L.fin_mode = fm ? atoi(fm) : kFinWriteThrough;

@@ -116,6 +116,7 @@ struct ScanLaunch {
   int32_t variant;            // 0: default kernel; >0: tuning variant (MBX_SCAN_VARIANT)
   int32_t nterms_host;        // the plan's term count, for launch-time kernel choice
   int32_t hoist_terms;        // 1..kHoistTerms literal terms: hoisted into registers
+  int32_t diag_terms;         // term i compares slot i, for every term
   int32_t fin_mode;           // FinMode (MBX_FIN_MODE): how the last block sees the partials
 };
 

@@ -369,7 +369,7 @@ __device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const u
 // TQ > 0: the first TQ terms were hoisted into registers (th) before the
 // tile loop and the term loop is unrolled over them (nterms <= TQ); TQ = 0:
 // terms are read from the plan per tile.
-template <int K, int KS, int MODE, bool DEL, int TQ = 0>
+template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool DG = false>
 __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, KS>& D,
                                           int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
                                           Acc& acc, uint64_t& wave_count, const KTerm* th = nullptr) {
@@ -404,14 +404,20 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
       for (int j = 0; j < 4; ++j) r[j] = (nib >> j) & 1u;
     } else {
       int32_t a[4];
+      if (DG) {  // term ti reads slot ti (host-checked): a compile-time register choice
+        constexpr int kLast = K > 0 ? K - 1 : 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
+        for (int j = 0; j < 4; ++j) a[j] = D.v[ti < kLast ? ti : kLast][j];
+      } else {
 #pragma unroll
-      for (int s = 1; s < K; ++s)
-        if (lhs == s) {
+        for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
-        }
+        for (int s = 1; s < K; ++s)
+          if (lhs == s) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
+          }
+      }
       if (T.kind == kInt) {
         cmp4<int32_t>(T.op, a, T.ilit, r);
       } else {
@@ -722,7 +728,7 @@ __device__ __forceinline__ void load_partial(TileRegs<K, KS>& D, int64_t t, int6
 //   contiguous window of each column; partial counts are then per block, not
 //   per segment (COUNT / aggregate only).  Measured equal on MI355X.
 // TQ > 0: the mask form (mask_tile) over <= TQ hoisted literal terms.
-template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false, int TQ = 0, bool MB = true>
+template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false, int TQ = 0, bool MB = true, bool DG = false>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
@@ -790,7 +796,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
         mask_tile<K, MODE, DEL, (TQ > 0 ? TQ : 1)>(L, P, D[u], valid ? t : tf - 1, lane, nterms, cnf_live, false,
                                                    valid, tprog, agg_slot, agg_real, acc, wave_count);
       } else if (t < tf) {
-        fast_tile<K, KS, MODE, DEL, TQ>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+        fast_tile<K, KS, MODE, DEL, TQ, DG>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
       }
     }
   };
@@ -813,7 +819,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
       mask_tile<K, MODE, DEL, (TQ > 0 ? TQ : 1)>(L, P, D, tp, lane, nterms, cnf_live, true, true, tprog, agg_slot,
                                                  agg_real, acc, wave_count);
     else
-      fast_tile<K, KS, MODE, DEL, TQ>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+      fast_tile<K, KS, MODE, DEL, TQ, DG>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
   }
   acc.count = lane == 0 ? (int64_t)wave_count : 0;
   block_reduce_store<MODE == kModeAgg>(acc, L);
@@ -1337,6 +1343,13 @@ static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
       case 12:  // per-row form, U=2 (the round-B kernel)
         hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true>), grid, dim3(kBlock), 0, s, L);
         return;
+      case 19:  // hoisted terms, term i on slot i (compile-time register choice)
+        if (hoist && L.diag_terms) {
+          hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, TQ, false, true>), grid, dim3(kBlock), 0,
+                             s, L);
+          return;
+        }
+        break;
       case 16:  // mask form (mask_tile): CNF on SGPR lane masks
         if (hoist) {
           hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, TQ, true>), grid, dim3(kBlock), 0, s, L);
