@@ -913,6 +913,8 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const Partial* __restrict__
 // ---------------------------------------------------------- bitmap kernels
 
 // result = AND_c OR_{k in c} bms[k], AND NOT deleted; two words per thread.
+constexpr int kCnfBatch = 4;  // operand bitmaps whose loads k_bitmap_cnf issues together
+
 __global__ __launch_bounds__(kBlock) void k_bitmap_cnf(BitmapCnf C, const uint64_t* __restrict__ del,
                                                        int64_t nwords, uint64_t tail_mask,
                                                        int64_t words_per_block, uint64_t* __restrict__ out,
@@ -920,24 +922,44 @@ __global__ __launch_bounds__(kBlock) void k_bitmap_cnf(BitmapCnf C, const uint64
   const int64_t w0 = (int64_t)blockIdx.x * words_per_block;
   const int64_t w1 = min(w0 + words_per_block, nwords);
   int64_t cnt = 0;
+  const int nbm = C.conj_off[C.nconj];
   for (int64_t w = w0 + 2 * threadIdx.x; w < w1; w += 2 * kBlock) {
     const bool two = w + 1 < w1;
     uint64_t r0 = ~0ull, r1 = ~0ull;
-    for (int c = 0; c < C.nconj; ++c) {
-      uint64_t o0 = 0, o1 = 0;
-      for (int k = C.conj_off[c]; k < C.conj_off[c + 1]; ++k) {
-        const uint64_t* b = C.bms[k];
-        if (two && ((w & 1) == 0)) {
-          const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(b + w);
-          o0 |= q.x;
-          o1 |= q.y;
-        } else {
-          o0 |= b[w];
-          if (two) o1 |= b[w + 1];
-        }
+    if (nbm <= kCnfBatch && two && (w & 1) == 0) {
+      // every operand's 16 bytes in flight at once, then the CNF in registers
+      ulonglong2 q[kCnfBatch];
+#pragma unroll
+      for (int k = 0; k < kCnfBatch; ++k)
+        if (k < nbm) q[k] = *reinterpret_cast<const ulonglong2*>(C.bms[k] + w);
+      for (int c = 0; c < C.nconj; ++c) {
+        uint64_t o0 = 0, o1 = 0;
+#pragma unroll
+        for (int k = 0; k < kCnfBatch; ++k)
+          if (k >= C.conj_off[c] && k < C.conj_off[c + 1]) {
+            o0 |= q[k].x;
+            o1 |= q[k].y;
+          }
+        r0 &= o0;
+        r1 &= o1;
       }
-      r0 &= o0;
-      r1 &= o1;
+    } else {
+      for (int c = 0; c < C.nconj; ++c) {
+        uint64_t o0 = 0, o1 = 0;
+        for (int k = C.conj_off[c]; k < C.conj_off[c + 1]; ++k) {
+          const uint64_t* b = C.bms[k];
+          if (two && ((w & 1) == 0)) {
+            const ulonglong2 q = *reinterpret_cast<const ulonglong2*>(b + w);
+            o0 |= q.x;
+            o1 |= q.y;
+          } else {
+            o0 |= b[w];
+            if (two) o1 |= b[w + 1];
+          }
+        }
+        r0 &= o0;
+        r1 &= o1;
+      }
     }
     if (del) {
       r0 &= ~del[w];
@@ -1020,6 +1042,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_popcount(const uint64_t* __restr
 // A block's output offset is the sum of the segment counts before it (read
 // straight from the producers' per-segment counts -- no separate scan
 // launch); the last block also writes the total.
+constexpr int kSelRegs = 8;  // a wave's words (x64) held in registers between the count and the write pass
+
 __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restrict__ words, int64_t nwords,
                                                        int64_t words_per_block,
                                                        const Partial* __restrict__ seg_parts,
@@ -1034,8 +1058,22 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
   const int64_t a0 = min(s0 + wave * per, s1);
   const int64_t a1 = min(a0 + per, s1);
+  // a wave range of <= 64 * kSelRegs words is loaded once, all loads in
+  // flight together, and kept in registers for the write pass
+  const bool cached = a1 - a0 <= 64 * kSelRegs;
+  uint64_t wr[kSelRegs];
   int64_t c = 0;
-  for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(words[w]);
+  if (cached) {
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t w = a0 + r * 64 + lane;
+      wr[r] = w < a1 ? words[w] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) c += __popcll(wr[r]);
+  } else {
+    for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(words[w]);
+  }
   int64_t pre = 0;
   for (int64_t i = threadIdx.x; i < (int64_t)blockIdx.x; i += kBlock) pre += seg_parts[i].count;
 #pragma unroll
@@ -1056,8 +1094,8 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
     *total = all;
   }
   for (int k = 0; k < wave; ++k) off += wcount[k];
-  for (int64_t base = a0; base < a1; base += 64) {
-    const uint64_t mw = base + lane < a1 ? words[base + lane] : 0ull;
+  // one step = 64 consecutive words, lane = word
+  auto step = [&](int64_t base, uint64_t mw) {
     const uint32_t pc = (uint32_t)__popcll(mw);
     uint32_t incl = pc;
 #pragma unroll
@@ -1095,6 +1133,16 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
       }
     }
     off += total;
+  };
+  if (cached) {
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t base = a0 + r * 64;
+      if (base >= a1) break;
+      step(base, wr[r]);
+    }
+  } else {
+    for (int64_t base = a0; base < a1; base += 64) step(base, base + lane < a1 ? words[base + lane] : 0ull);
   }
 }
 
@@ -1108,6 +1156,11 @@ struct MatArgs {
   int32_t nproj;
 };
 
+// Late materialisation.  G4 > 0: every projected column is 4 bytes wide and
+// there are at most G4 of them -- all their loads are issued before the
+// first store (4 rows x G4 columns in flight per thread: the row reads are
+// random, so this is a request-rate-bound kernel).
+template <int G4>
 __global__ __launch_bounds__(kBlock) void k_gather(const int64_t* __restrict__ ids, const int64_t* __restrict__ total,
                                                    int64_t row_offset, MatArgs M) {
   const int64_t n = *total;
@@ -1119,22 +1172,40 @@ __global__ __launch_bounds__(kBlock) void k_gather(const int64_t* __restrict__ i
       const int64_t i = i0 + u * stride;
       row[u] = i < n ? ids[i] - row_offset : -1;
     }
-    for (int p = 0; p < M.nproj; ++p) {
-      const int sw = M.proj[p].stride_w;
-      const uint32_t* src = (const uint32_t*)M.proj[p].base;
-      uint32_t* dst = (uint32_t*)M.out[p];
-      if (sw == 1) {
-        uint32_t v[4];
+    if constexpr (G4 > 0) {
+      uint32_t v[G4][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = row[u] >= 0 ? src[row[u]] : 0u;
+      for (int p = 0; p < G4; ++p) {
+        const gi32* src = (const gi32*)M.proj[p].base;
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (row[u] >= 0) dst[i0 + u * stride] = v[u];
-      } else {
+        for (int u = 0; u < 4; ++u) v[p][u] = (p < M.nproj && row[u] >= 0) ? (uint32_t)src[row[u]] : 0u;
+      }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (row[u] >= 0)
-            for (int k = 0; k < sw; ++k) dst[(i0 + u * stride) * sw + k] = src[row[u] * sw + k];
+      for (int p = 0; p < G4; ++p)
+        if (p < M.nproj) {
+          uint32_t* dst = (uint32_t*)M.out[p];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (row[u] >= 0) dst[i0 + u * stride] = v[p][u];
+        }
+    } else {
+      for (int p = 0; p < M.nproj; ++p) {
+        const int sw = M.proj[p].stride_w;
+        const uint32_t* src = (const uint32_t*)M.proj[p].base;
+        uint32_t* dst = (uint32_t*)M.out[p];
+        if (sw == 1) {
+          uint32_t v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = row[u] >= 0 ? src[row[u]] : 0u;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (row[u] >= 0) dst[i0 + u * stride] = v[u];
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            if (row[u] >= 0)
+              for (int k = 0; k < sw; ++k) dst[(i0 + u * stride) * sw + k] = src[row[u] * sw + k];
+        }
       }
     }
   }
@@ -1452,7 +1523,12 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
       M.proj[j] = proj[j];
       M.out[j] = out[j];
     }
-    hipLaunchKernelGGL(k_gather, dim3(1024), dim3(kBlock), 0, s, ids, total, row_offset, M);
+    bool all4 = nproj <= 4;
+    for (int j = 0; j < nproj && j < kMaxProj; ++j) all4 = all4 && proj[j].stride_w == 1;
+    if (all4)
+      hipLaunchKernelGGL(k_gather<4>, dim3(1024), dim3(kBlock), 0, s, ids, total, row_offset, M);
+    else
+      hipLaunchKernelGGL(k_gather<0>, dim3(1024), dim3(kBlock), 0, s, ids, total, row_offset, M);
   }
   return hipGetLastError();
 }
