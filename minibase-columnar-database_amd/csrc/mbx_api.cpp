@@ -711,6 +711,13 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
     L.diag_terms = L.hoist_terms && v.fast_ks == 0 && p->host.nterms == v.fast_k;
     for (int i = 0; i < p->host.nterms && L.diag_terms; ++i) L.diag_terms = p->host.terms[i].lhs == i;
   }
+  {
+    // tile layout: row-interleaved for BitSet output (the ballots are the
+    // words); MBX_SCAN_RI=0 never, 1 BitSet output only, 2 always (A/B tuning)
+    const char* ri = getenv("MBX_SCAN_RI");
+    const int pol = ri ? atoi(ri) : 1;
+    L.ri = pol == 2 || (pol == 1 && mode == kModeBitmap);
+  }
   const char* fm = getenv("MBX_FIN_MODE");
   L.fin_mode = fm ? atoi(fm) : kFinWriteThrough;
   if (L.fin_mode == kFinSeparate) L.ticket = nullptr;

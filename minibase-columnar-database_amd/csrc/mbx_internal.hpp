@@ -118,6 +118,7 @@ struct ScanLaunch {
   int32_t hoist_terms;        // 1..kHoistTerms literal terms: hoisted into registers
   int32_t diag_terms;         // term i compares slot i, for every term
   int32_t fin_mode;           // FinMode (MBX_FIN_MODE): how the last block sees the partials
+  int32_t ri;                 // 1: row-interleaved tile layout (register j of lane l = row 64j + l)
 };
 
 // Arrival tickets of the in-launch finalize.  Blocks arrive on the ticket of

@@ -369,13 +369,19 @@ __device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const u
 // TQ > 0: the first TQ terms were hoisted into registers (th) before the
 // tile loop and the term loop is unrolled over them (nterms <= TQ); TQ = 0:
 // terms are read from the plan per tile.
-template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool DG = false>
+// RI (row-interleaved tile layout): register j of lane l holds row 64j + l of
+// the tile instead of row 4l + j, so the wave ballot of row group j *is*
+// BitSet word j of the tile -- no cross-lane packing for BitSet output, the
+// deleted words apply as they are, string compares need no re-layout.
+template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool DG = false, bool RI = false>
 __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, KS>& D,
                                           int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
-                                          Acc& acc, uint64_t& wave_count, const KTerm* th = nullptr) {
+                                          Acc& acc, uint64_t& wave_count, const KTerm* th = nullptr,
+                                          uint64_t* ws = nullptr) {
   const int64_t nrows = L.nrows;
   const int64_t nwords = (nrows + 63) >> 6;
-  const int64_t row0 = t * kTileRows + lane * 4;
+  const int64_t row0 = t * kTileRows + lane * (RI ? 1 : 4);
+  constexpr int kRowStep = RI ? 64 : 1;  // row of register j = row0 + j * kRowStep
   uint32_t cb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int ti = 0; ti < (TQ > 0 ? TQ : nterms); ++ti) {
@@ -396,12 +402,17 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
       bool rs[4];
       cmp4<int32_t>(T.op, c, 0, rs);
       // rs[j] is row 64j + lane; ballot j is BitSet word j of the tile
+      if (RI) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) r[j] = rs[j];
+      } else {
       const uint64_t w0 = __ballot(rs[0]), w1 = __ballot(rs[1]), w2 = __ballot(rs[2]), w3 = __ballot(rs[3]);
       const int q = lane >> 4;
       const uint64_t w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
       const uint32_t nib = (uint32_t)(w >> ((lane & 15) * 4));
 #pragma unroll
       for (int j = 0; j < 4; ++j) r[j] = (nib >> j) & 1u;
+      }
     } else {
       int32_t a[4];
       if (DG) {  // term ti reads slot ti (host-checked): a compile-time register choice
@@ -425,7 +436,7 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           f[j] = __int_as_float(a[j]);
-          acc.nan |= (f[j] != f[j]) && (row0 + j < nrows);
+          acc.nan |= (f[j] != f[j]) && (row0 + j * kRowStep < nrows);
         }
         cmp4<float>(T.op, f, T.flit, r);
       }
@@ -437,15 +448,32 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
 
   bool p[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) p[j] = (cb[j] == all) && (row0 + j < nrows);
-  const int64_t word = t * kWordsPerTile + (lane >> 4);
-  if (DEL) {
+  for (int j = 0; j < 4; ++j) p[j] = (cb[j] == all) && (row0 + j * kRowStep < nrows);
+  const int64_t word = t * kWordsPerTile + (RI ? 0 : (lane >> 4));
+  if (DEL && RI) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t dw = word + j < nwords ? L.deleted[word + j] : 0ull;  // uniform: one scalar load
+      p[j] = p[j] && !((dw >> lane) & 1ull);
+    }
+  } else if (DEL) {
     const uint64_t dw = word < nwords ? L.deleted[word] : 0ull;
     const uint32_t dn = (uint32_t)(dw >> ((lane & 15) * 4)) & 0xFu;
 #pragma unroll
     for (int j = 0; j < 4; ++j) p[j] = p[j] && !((dn >> j) & 1u);
   }
-  if (MODE == kModeBitmap) {
+  if (MODE == kModeBitmap && RI) {
+    const uint64_t w0 = __ballot(p[0]), w1 = __ballot(p[1]), w2 = __ballot(p[2]), w3 = __ballot(p[3]);
+    if (ws) {  // the caller buffers the words (BitSink)
+      ws[0] = w0;
+      ws[1] = w1;
+      ws[2] = w2;
+      ws[3] = w3;
+    } else {
+      const uint64_t w = lane == 0 ? w0 : (lane == 1 ? w1 : (lane == 2 ? w2 : w3));
+      if (lane < 4 && word + lane < nwords) L.out_words[word + lane] = w;
+    }
+  } else if (MODE == kModeBitmap) {
     const uint32_t nib = (uint32_t)p[0] | ((uint32_t)p[1] << 1) | ((uint32_t)p[2] << 2) | ((uint32_t)p[3] << 3);
     const uint64_t w = pack_word16(nib, lane);
     if ((lane & 15) == 0 && word < nwords) L.out_words[word] = w;
@@ -632,11 +660,33 @@ __device__ __forceinline__ v4i load16(const int32_t* p) {
 
 __device__ __forceinline__ int32_t load4(const int32_t* p) { return *(gi32*)p; }
 
+template <bool NT>
+__device__ __forceinline__ int32_t load4n(const int32_t* p) {
+  if (NT) return __builtin_nontemporal_load((gi32*)p);
+  return *(gi32*)p;
+}
+
+// One full tile's 4-byte slot s: dwordx4 rows 4l..4l+3 (RI = false) or four
+// 256-byte wave loads, register j = row 64j + l (RI = true).
+template <int K, int KS, bool NT, bool RI>
+__device__ __forceinline__ void load_slot(TileRegs<K, KS>& D, int s, const int32_t* col, int64_t t, int lane) {
+  if (RI) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) D.v[s][j] = load4n<NT>(col + t * kTileRows + j * 64 + lane);
+  } else {
+    const v4i q = load16<NT>(col + t * kTileRows + lane * 4);
+    D.v[s][0] = q.x;
+    D.v[s][1] = q.y;
+    D.v[s][2] = q.z;
+    D.v[s][3] = q.w;
+  }
+}
+
 // The full tiles base + u * ustep (u < U, below tf) of one wave into
 // registers.  Loads only, no else path: a branch that also wrote the
 // registers would make the compiler join the two and wait for the loads
 // right where they are issued.
-template <int K, int KS, int U, bool NT>
+template <int K, int KS, int U, bool NT, bool RI = false>
 __device__ __forceinline__ void load_tiles(TileRegs<K, KS> (&D)[U], int64_t base, int64_t ustep, int64_t tf,
                                            const int32_t* const (&colp)[K > 0 ? K : 1],
                                            const int32_t* const (&strp)[KS > 0 ? KS : 1], int lane) {
@@ -645,13 +695,7 @@ __device__ __forceinline__ void load_tiles(TileRegs<K, KS> (&D)[U], int64_t base
     const int64_t t = base + (int64_t)u * ustep;
     if (t < tf) {
 #pragma unroll
-      for (int s = 0; s < K; ++s) {
-        const v4i q = load16<NT>(colp[s] + t * kTileRows + lane * 4);
-        D[u].v[s][0] = q.x;
-        D[u].v[s][1] = q.y;
-        D[u].v[s][2] = q.z;
-        D[u].v[s][3] = q.w;
-      }
+      for (int s = 0; s < K; ++s) load_slot<K, KS, NT, RI>(D[u], s, colp[s], t, lane);
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -670,7 +714,7 @@ __device__ __forceinline__ void load_tiles(TileRegs<K, KS> (&D)[U], int64_t base
 // clamped to tf - 1 (a re-read of a tile in flight anyway, served by L2), so
 // every path issues the same number of loads and the waitcnt pass can wait
 // for exactly the older group (vmcnt(N)) instead of draining all loads.
-template <int K, int KS, int U, bool NT>
+template <int K, int KS, int U, bool NT, bool RI = false>
 __device__ __forceinline__ void load_tiles_clamped(TileRegs<K, KS> (&D)[U], int64_t base, int64_t ustep, int64_t tf,
                                                    const int32_t* const (&colp)[K > 0 ? K : 1],
                                                    const int32_t* const (&strp)[KS > 0 ? KS : 1], int lane) {
@@ -679,13 +723,7 @@ __device__ __forceinline__ void load_tiles_clamped(TileRegs<K, KS> (&D)[U], int6
     int64_t t = base + (int64_t)u * ustep;
     t = t < tf ? t : tf - 1;
 #pragma unroll
-    for (int s = 0; s < K; ++s) {
-      const v4i q = load16<NT>(colp[s] + t * kTileRows + lane * 4);
-      D[u].v[s][0] = q.x;
-      D[u].v[s][1] = q.y;
-      D[u].v[s][2] = q.z;
-      D[u].v[s][3] = q.w;
-    }
+    for (int s = 0; s < K; ++s) load_slot<K, KS, NT, RI>(D[u], s, colp[s], t, lane);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -700,15 +738,17 @@ __device__ __forceinline__ void load_tiles_clamped(TileRegs<K, KS> (&D)[U], int6
 }
 
 // The table's one partial tile t (rows t * 256 .. nrows - 1): guarded loads.
-template <int K, int KS>
+template <int K, int KS, bool RI = false>
 __device__ __forceinline__ void load_partial(TileRegs<K, KS>& D, int64_t t, int64_t nrows,
                                              const int32_t* const (&colp)[K > 0 ? K : 1],
                                              const int32_t* const (&strp)[KS > 0 ? KS : 1], int lane) {
-  const int64_t row0 = t * kTileRows + lane * 4;
+  const int64_t row0 = t * kTileRows + lane * (RI ? 1 : 4);
+  constexpr int kRowStep = RI ? 64 : 1;
 #pragma unroll
   for (int s = 0; s < K; ++s)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) D.v[s][j] = row0 + j < nrows ? load4(colp[s] + row0 + j) : 0;
+    for (int j = 0; j < 4; ++j)
+      D.v[s][j] = row0 + j * kRowStep < nrows ? load4(colp[s] + row0 + j * kRowStep) : 0;
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -728,8 +768,10 @@ __device__ __forceinline__ void load_partial(TileRegs<K, KS>& D, int64_t t, int6
 //   contiguous window of each column; partial counts are then per block, not
 //   per segment (COUNT / aggregate only).  Measured equal on MI355X.
 // TQ > 0: the mask form (mask_tile) over <= TQ hoisted literal terms.
-template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false, int TQ = 0, bool MB = true, bool DG = false>
+template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false, int TQ = 0, bool MB = true, bool DG = false,
+          bool RI = false>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
+  static_assert(!(RI && TQ > 0 && KS == 0 && MB), "the mask form keeps the 4-rows-per-lane layout");
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
@@ -784,6 +826,24 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
 
   // full tiles in the main loop; the partial last tile (if any) after it
   const int64_t tf = min(t1, nrows / kTileRows);
+  // BitSink (BitSet output, RI layout): a wave's full tiles come in the order
+  // t0 + wave + i * ustep; the 4 words of its i-th tile go to lanes
+  // 4 (i % 16) .. 4 (i % 16) + 3 of one register, stored with ONE store per
+  // 16 tiles -- a store in every tile iteration holds up the next loads
+  // (their registers wait for the store's data to be read), 91 vs 70 us at
+  // 100M rows.
+  constexpr bool kSink = MODE == kModeBitmap && RI;
+  uint64_t sink = 0;
+  int64_t sink_t = t0 + wave;  // tile of slot 0 of the current 16-tile chunk
+  int sink_n = 0;              // tiles captured in the chunk (uniform)
+  auto sink_flush = [&]() {
+    if (sink_n > 0) {
+      const int sl = lane >> 2;
+      if (sl < sink_n) L.out_words[(sink_t + (int64_t)sl * ustep) * kWordsPerTile + (lane & 3)] = sink;
+      sink_t += 16 * ustep;
+      sink_n = 0;
+    }
+  };
   auto compute = [&](TileRegs<K, KS>(&D)[U], int64_t base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -796,7 +856,19 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
         mask_tile<K, MODE, DEL, (TQ > 0 ? TQ : 1)>(L, P, D[u], valid ? t : tf - 1, lane, nterms, cnf_live, false,
                                                    valid, tprog, agg_slot, agg_real, acc, wave_count);
       } else if (t < tf) {
-        fast_tile<K, KS, MODE, DEL, TQ, DG>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+        if constexpr (kSink) {
+          uint64_t w[4];
+          fast_tile<K, KS, MODE, DEL, TQ, DG, RI>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc,
+                                                  wave_count, th, w);
+          if ((lane >> 2) == sink_n) {
+            const int j = lane & 3;
+            sink = j == 0 ? w[0] : (j == 1 ? w[1] : (j == 2 ? w[2] : w[3]));
+          }
+          if (++sink_n == 16) sink_flush();
+        } else {
+          fast_tile<K, KS, MODE, DEL, TQ, DG, RI>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc,
+                                                  wave_count, th);
+        }
       }
     }
   };
@@ -805,21 +877,22 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
     for (int64_t base = t0 + wave; base < tf; base += step) {
       TileRegs<K, KS> D[U];
       if (TQ > 0)  // every path issues all U loads: exact vmcnt waits
-        load_tiles_clamped<K, KS, U, NT>(D, base, ustep, tf, colp, strp, lane);
+        load_tiles_clamped<K, KS, U, NT, RI>(D, base, ustep, tf, colp, strp, lane);
       else
-        load_tiles<K, KS, U, NT>(D, base, ustep, tf, colp, strp, lane);
+        load_tiles<K, KS, U, NT, RI>(D, base, ustep, tf, colp, strp, lane);
       compute(D, base);
     }
   }
+  if constexpr (kSink) sink_flush();
   const int64_t tp = nrows / kTileRows;  // the partial tile, owned like any other tile of [t0, t1)
   if ((nrows % kTileRows) != 0 && tp >= t0 + wave && tp < t1 && (tp - t0 - wave) % ustep == 0) {
     TileRegs<K, KS> D;
-    load_partial<K, KS>(D, tp, nrows, colp, strp, lane);
+    load_partial<K, KS, RI>(D, tp, nrows, colp, strp, lane);
     if constexpr (kMask)
       mask_tile<K, MODE, DEL, (TQ > 0 ? TQ : 1)>(L, P, D, tp, lane, nterms, cnf_live, true, true, tprog, agg_slot,
                                                  agg_real, acc, wave_count);
     else
-      fast_tile<K, KS, MODE, DEL, TQ, DG>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+      fast_tile<K, KS, MODE, DEL, TQ, DG, RI>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
   }
   acc.count = lane == 0 ? (int64_t)wave_count : 0;
   block_reduce_store<MODE == kModeAgg>(acc, L);
@@ -1387,20 +1460,38 @@ int64_t grid_blocks(int64_t nrows, int64_t tiles_per_block) {
   return g < 1 ? 1 : g;
 }
 
-template <int K, int KS, int MODE>
-static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
+// the production kernel of one (K, KS, MODE, DEL) class in either tile layout
+template <int K, int KS, int MODE, bool DEL, bool RI>
+static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   // 4-byte slots only and 1..kHoistTerms literal terms (L.hoist_terms): the terms
   // are hoisted into registers (TQ) and the per-row tile body is unrolled over
   // them -- measured 2.5 % faster than reading them from the plan per tile
   // and than the SGPR-mask body (variant 16), profiles/r01/an3
   constexpr int TQ = KS == 0 ? kHoistTerms : 0;
+  // one 4-byte column: 4 tiles in flight per wave (the same bytes in flight as
+  // two columns at U=2); 100M rows: COUNT 69.7 -> 67.3 us, BitSet 87.5 -> 81.0 us
+  constexpr int kU = K == 1 && KS == 0 ? 4 : kDefaultU;
+  if (KS == 0 && L.hoist_terms)
+    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, false, TQ, false, false, RI>), grid,
+                       dim3(kBlock), 0, s, L);
+  else
+    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, false, 0, false, false, RI>), grid,
+                       dim3(kBlock), 0, s, L);
+}
+
+template <int K, int KS, int MODE>
+static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
+  constexpr int TQ = KS == 0 ? kHoistTerms : 0;
   const bool hoist = KS == 0 && L.hoist_terms;
   if (L.deleted) {
-    if (hoist)
-      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, true, kDefaultU, kDefaultNT, false, TQ, false>), grid,
-                         dim3(kBlock), 0, s, L);
+    if (L.ri)
+      prod_launch<K, KS, MODE, true, true>(L, grid, s);
     else
-      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, true, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
+      prod_launch<K, KS, MODE, true, false>(L, grid, s);
+    return;
+  }
+  if (L.ri) {
+    prod_launch<K, KS, MODE, false, true>(L, grid, s);
     return;
   }
   if constexpr (K == 2 && KS == 0 && MODE == kModeCount) {  // tuning variants of the C3 kernel
@@ -1430,11 +1521,7 @@ static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
       default: break;
     }
   }
-  if (hoist)
-    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, kDefaultU, kDefaultNT, false, TQ, false>), grid, dim3(kBlock),
-                       0, s, L);
-  else
-    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, kDefaultU, kDefaultNT>), grid, dim3(kBlock), 0, s, L);
+  prod_launch<K, KS, MODE, false, false>(L, grid, s);
 }
 
 // fast_k = number of 4-byte slots, fast_ks = number of 16-byte string slots;

@@ -7,10 +7,12 @@ HBM table is staged with row_offset = start so positions it returns are
 global.  Rows are independent, so scans need no communication; the only
 collective combines the per-rank results:
 
-  COUNT / SUM(int)  -> all_reduce(SUM) on int64
-  MIN / MAX         -> all_reduce(MIN / MAX)
-  SUM(float)        -> all_gather of the per-rank double partials, summed in
-                       rank order (bit-reproducible for a given world size)
+  COUNT             -> all_reduce(SUM) on int64
+  COUNT/SUM/MIN/MAX -> ONE all_gather of every rank's 48-byte aggregate
+                       record (the kernel's mbx_agg, straight from device
+                       memory), folded in rank order: int64 sums exact, the
+                       double SUM of the per-rank partials in rank order
+                       (bit-reproducible for a given world size), MIN / MAX
   positions / rows  -> all_gather, concatenated in rank order (= ascending
                        global position order, the reference's nextSetBit order)
 
@@ -48,32 +50,73 @@ def combine_count(count, device=None, group=None):
     return int(t.item())
 
 
-def combine_aggregate(agg, device=None, group=None):
-    """agg: dict(count, sum, min, max) of one rank (mbx_agg / oracle layout)."""
+# one rank's aggregate in the C-ABI's mbx_agg layout (48 bytes = 6 int64),
+# the unit the combine step exchanges
+AGG_RECORD = np.dtype([("count", "<i8"), ("agg_type", "<i4"), ("pad", "<i4"), ("isum", "<i8"), ("imin", "<i4"),
+                       ("imax", "<i4"), ("fsum", "<f8"), ("fmin", "<f4"), ("fmax", "<f4")])
+AGG_WORDS = AGG_RECORD.itemsize // 8
+_INTEGER = 1  # AttrType.attrInteger
+
+
+def pack_aggregate(agg, integer):
+    """dict(count, sum, min, max) -> one AGG_RECORD (the kernel's AggOut)."""
+    r = np.zeros(1, dtype=AGG_RECORD)
+    r["count"] = int(agg["count"])
+    r["agg_type"] = _INTEGER if integer else 2
+    if integer:
+        r["isum"], r["imin"], r["imax"] = int(agg["sum"]), int(agg["min"]), int(agg["max"])
+    else:
+        r["fsum"], r["fmin"], r["fmax"] = float(agg["sum"]), float(agg["min"]), float(agg["max"])
+    return r
+
+
+def fold_aggregates(recs):
+    """Rank-ordered AGG_RECORDs -> the global dict(count, sum, min, max).
+    COUNT / int SUM add exactly; the double SUM adds the per-rank partials
+    in rank order (bit-reproducible for a given world size); MIN / MAX fold
+    the per-rank values, whose empty-shard values are the identities
+    (INT32_MAX / INT32_MIN, +inf / -inf, like the oracle)."""
+    recs = np.asarray(recs).view(AGG_RECORD).reshape(-1)
+    integer = int(recs["agg_type"][0]) == _INTEGER
+    count = int(recs["count"].sum())
+    if integer:
+        return dict(count=count, sum=int(recs["isum"].sum()), min=int(recs["imin"].min()),
+                    max=int(recs["imax"].max()))
+    total = 0.0
+    for v in recs["fsum"]:
+        total += float(v)
+    return dict(count=count, sum=total, min=float(recs["fmin"].min()), max=float(recs["fmax"].max()))
+
+
+def _all_gather_words(t, group):
+    """ONE collective: every rank's int64 vector, concatenated in rank order."""
     import torch
     import torch.distributed as dist
-    dev = _dev(device)
-    is_float = isinstance(agg["sum"], float)
-    cnt = torch.tensor([int(agg["count"])], dtype=torch.int64, device=dev)
-    dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
-    if is_float:
-        mn = torch.tensor([agg["min"]], dtype=torch.float32, device=dev)
-        mx = torch.tensor([agg["max"]], dtype=torch.float32, device=dev)
-        parts = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(dist.get_world_size(group))]
-        dist.all_gather(parts, torch.tensor([agg["sum"]], dtype=torch.float64, device=dev), group=group)
-        total = 0.0
-        for p in parts:  # rank order: deterministic
-            total += float(p.item())
-    else:
-        mn = torch.tensor([agg["min"]], dtype=torch.int64, device=dev)
-        mx = torch.tensor([agg["max"]], dtype=torch.int64, device=dev)
-        s = torch.tensor([int(agg["sum"])], dtype=torch.int64, device=dev)
-        dist.all_reduce(s, op=dist.ReduceOp.SUM, group=group)
-        total = int(s.item())
-    dist.all_reduce(mn, op=dist.ReduceOp.MIN, group=group)
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-    cast = float if is_float else int
-    return dict(count=int(cnt.item()), sum=total, min=cast(mn.item()), max=cast(mx.item()))
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=group)
+        return out
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    return torch.cat(parts)
+
+
+def combine_aggregate(agg, device=None, group=None):
+    """agg: dict(count, sum, min, max) of one rank (mbx_agg / oracle layout).
+    The exchange is one all_gather of the 48-byte record."""
+    import torch
+    integer = not isinstance(agg["sum"], float)
+    rec = pack_aggregate(agg, integer)
+    t = torch.from_numpy(rec.view(np.int64).copy()).to(_dev(device))
+    return fold_aggregates(_all_gather_words(t, group).cpu().numpy())
+
+
+def combine_aggregate_device(rec_words, group=None):
+    """rec_words: the int64[6] device tensor mbx_scan_aggregate_async wrote
+    (RCCL over xGMI when the group is "nccl").  Returns the rank-ordered
+    AGG_RECORDs gathered on the device; fold_aggregates() reads them."""
+    return _all_gather_words(rec_words, group)
 
 
 def gather_positions(ids, device=None, group=None):

@@ -187,6 +187,41 @@ def test_deleted_rows(ctx, generic, monkeypatch):
     assert ctx.scan_count(ctx.compile(t, None)) == n - int(sum(bin(int(x)).count("1") for x in dele))
 
 
+def _np_words(mask):
+    n = mask.size
+    w = np.zeros(((n + 63) // 64) * 64, dtype=bool)
+    w[:n] = mask
+    return np.packbits(w, bitorder="little").view(np.uint64)
+
+
+@pytest.mark.parametrize("tpb", [0, 4, 63, 64, 65, 200, 1000])
+@pytest.mark.parametrize("ri", ["0", "1"])
+@pytest.mark.parametrize("deleted", [False, True])
+def test_bitset_segments_and_tile_layouts(ctx, tpb, ri, deleted, monkeypatch):
+    """BitSet output over segment sizes that give each wave 1..250 tiles (the
+    RI layout buffers 16 tiles' words per store) and a ragged tail, both tile
+    layouts (MBX_SCAN_RI), with and without deleted rows; numpy is the check
+    (the same predicate, bit for bit)."""
+    if tpb:
+        monkeypatch.setenv("MBX_TILES_PER_BLOCK", str(tpb))
+    monkeypatch.setenv("MBX_SCAN_RI", ri)
+    n = 2_000_003
+    cols, dele = int_table(n, hi=1000, deleted_frac=0.05 if deleted else None)
+    t = ctx.stage(cols, dele)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", 700))], [(oracle.GE, ("sym", 2), ("int", 100)),
+                                                       (oracle.EQ, ("sym", 3), ("int", 7))]]
+    c0, c1, c2 = cols[0][2], cols[1][2], cols[2][2]
+    mask = (c0 < 700) & ((c1 >= 100) | (c2 == 7))
+    want = _np_words(mask)
+    if deleted:
+        want &= ~dele
+    bm, words = gpu_select(ctx, t, cnf)
+    assert np.array_equal(words, want)
+    assert bm.count == int(np.unpackbits(want.view(np.uint8)).sum())
+    ids = ctx.select(bm)
+    assert np.array_equal(ids, np.nonzero(np.unpackbits(want.view(np.uint8), bitorder="little"))[0][:bm.count])
+
+
 @pytest.mark.parametrize("op", [oracle.EQ, oracle.LT, oracle.GT, oracle.NE, oracle.LE, oracle.GE, oracle.NOT,
                                 oracle.NOP, oracle.RANGE])
 @pytest.mark.parametrize("lit_left", [False, True])

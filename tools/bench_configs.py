@@ -1,38 +1,39 @@
 #!/usr/bin/env python3
-"""Per-config throughput of the other BASELINE.json workloads on ONE MI355X
-(the bench line itself is C3, bench.py).  Each config is timed with HIP
-events on the library stream over K async steps (inputs resident in HBM),
-its result checked against a torch reduction of the same device data.
+"""Per-config throughput of the other BASELINE.json workloads (the bench line
+itself is C3, bench.py).  Inputs resident in HBM; each query is timed with
+HIP events on the library stream over K async steps, and its result checked
+against a torch reduction of the same device data.
 
-  C2  10M rows x 4 int32, c0 < 104858 -> BitSet + positions + COUNT
+  C2  10M rows x 4 int32, c0 < 104858 -> BitSet + positions + COUNT (1 GPU)
   C4  100M rows, AND of BitMapFiles bm(c2=3), bm(c3=7) -> positions + c0, c1
-  C5  mixed i32 / f32 / char(16), (c0<2^19) ^ (c1>=0.25) ^ (c2>="M") -> COUNT, SUM/MIN/MAX(c1)
-      at the 8-GPU per-rank share (125M rows) and at the full 1B rows
+  C5  mixed i32 / f32 / char(16), (c0<2^19) ^ (c1>=0.25) ^ (c2>="M") -> COUNT,
+      SUM/MIN/MAX(c1)
 
-Prints one JSON line per config.
+One process per GPU: launched by torch.distributed.run, C4
+and C5 shard the global table by 64-aligned row ranges (dist.shard_bounds,
+positions global through row_offset) and run with no data-path collective;
+the one exchange step per query is on a side stream:
+  C4  all_gather of the per-rank selected counts (the concatenation offsets
+      of the per-rank outputs, shard order = ascending positions)
+  C5  all_gather of every rank's 48-byte aggregate record straight from
+      device memory (dist.combine_aggregate_device), folded in rank order
+Reported per config (rank 0, one JSON line): max-over-ranks wall time per
+query with the exchange included (barrier + synchronize around K queries),
+the per-phase kernel times (max over ranks) and global rows/s.
+
+  python tools/bench_configs.py [--configs C2,C4,C5] [--c5-rows 125000000,1000000000]
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_configs.py \\
+      --configs C4,C5 --c4-rows 100000000 --c5-rows 1000000000
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-
-
-def timed(ctx, ext, fn, steps, warmup):
-    import torch
-    for _ in range(warmup):
-        fn()
-    ctx.sync()
-    a = torch.cuda.Event(enable_timing=True)
-    b = torch.cuda.Event(enable_timing=True)
-    a.record(ext)
-    for _ in range(steps):
-        fn()
-    b.record(ext)
-    ctx.sync()
-    return a.elapsed_time(b) / steps
 
 
 def main():
@@ -40,23 +41,104 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--configs", default="C2,C4,C5")
-    ap.add_argument("--c5-rows", default="125000000,1000000000")
+    ap.add_argument("--c4-rows", type=int, default=100_000_000, help="global rows")
+    ap.add_argument("--c5-rows", default="125000000,1000000000", help="global rows, comma separated")
     args = ap.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
     import torch
+    import torch.distributed as dist
+
     import mbx_pkg
 
+    # rehearsal knobs, as in bench.py: MBX_BENCH_BACKEND=gloo,
+    # MBX_BENCH_SAME_DEVICE=1 run N ranks on one GPU
+    backend = os.environ.get("MBX_BENCH_BACKEND", "nccl")
+    device = 0 if os.environ.get("MBX_BENCH_SAME_DEVICE") == "1" else local_rank
+    torch.cuda.set_device(device)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
     m = mbx_pkg.load()
     M = m.mbx
-    ctx = m.Context(0)
+    D = m.dist
+    L = M.lib()
+    ctx = m.Context(device)
     ext = torch.cuda.ExternalStream(ctx.stream)
+    xs = torch.cuda.Stream() if world > 1 else None
+
+    def rmax(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def kernel_ms(fn, steps, warmup):
+        """HIP events on the library stream around `steps` calls, max over ranks."""
+        for _ in range(warmup):
+            fn()
+        ctx.sync()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(ext)
+        for _ in range(steps):
+            fn()
+        b.record(ext)
+        ctx.sync()
+        return rmax(a.elapsed_time(b) / steps)
+
+    def wall_ms(step, steps, warmup):
+        """Whole queries incl. the exchange: barrier + synchronize on both sides."""
+        for k in range(warmup):
+            step(k)
+        ctx.sync()
+        barrier()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(warmup + k)
+        ctx.sync()
+        barrier()
+        return rmax((time.perf_counter() - t0) * 1e3 / steps)
+
+    def exchange(k, src_words, out_rows):
+        """The one collective of a query, on the side stream after the library
+        stream's work: all_gather of `src_words` (int64) into out_rows[k]."""
+        if world == 1:
+            return
+        ev = torch.cuda.Event()
+        ev.record(ext)
+        xs.wait_event(ev)
+        with torch.cuda.stream(xs):
+            if backend == "nccl":
+                dist.all_gather_into_tensor(out_rows[k], src_words)
+            else:  # gloo rehearsal: host copies
+                parts = [torch.empty_like(src_words, device="cpu") for _ in range(world)]
+                dist.all_gather(parts, src_words.cpu())
+                out_rows[k].copy_(torch.cat(parts))
 
     def gen_int(n, hi, seed):
         g = torch.Generator(device="cuda")
         g.manual_seed(seed)
         return torch.randint(0, hi, (n,), dtype=torch.int32, device="cuda", generator=g)
 
-    if "C2" in args.configs:
+    def emit(d):
+        if rank == 0:
+            print(json.dumps(d), flush=True)
+
+    if "C2" in args.configs and world == 1:
         n = 10_000_000
         cols = [gen_int(n, 1 << 20, 42 + j) for j in range(4)]
         t = ctx.wrap([(M.INTEGER, 4)] * 4, [c.data_ptr() for c in cols], n)
@@ -64,99 +146,143 @@ def main():
         bm = ctx.bitmap_alloc(n)
         ids = torch.zeros(n, dtype=torch.int64, device="cuda")
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        import ctypes
-        L = M.lib()
 
-        def step():
+        def step(k=0):
             ctx.scan_bitmap_async(plan, bm)
             M._chk(L.mbx_materialize_async(ctx.h, t.h, bm.h, None, 0, ids.data_ptr(), None, cnt.data_ptr()))
 
-        ms = timed(ctx, ext, step, args.steps, args.warmup)
+        ms = kernel_ms(step, args.steps, args.warmup)
         want = int((cols[0] < 104858).sum().item())
         got = int(cnt.item())
         assert got == want, (got, want)
         assert bool((ids[:got] == torch.nonzero(cols[0] < 104858).flatten()).all())
-        scan_ms = timed(ctx, ext, lambda: ctx.scan_bitmap_async(plan, bm), args.steps, args.warmup)
+        scan_ms = kernel_ms(lambda: ctx.scan_bitmap_async(plan, bm), args.steps, args.warmup)
         byts = n * 4 + n / 8 + got * 8
-        print(json.dumps({"config": "C2", "rows": n, "selected": got, "ms_per_query": ms, "rows_per_s": n / ms * 1e3,
-                          "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
-                          "scan_gbs": (n * 4 + n / 8) / scan_ms / 1e6}), flush=True)
+        emit({"config": "C2", "rows": n, "gpus": 1, "selected": got, "ms_per_query": ms, "rows_per_s": n / ms * 1e3,
+              "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
+              "scan_gbs": (n * 4 + n / 8) / scan_ms / 1e6})
         del cols, t, plan, bm, ids
         torch.cuda.empty_cache()
 
     if "C4" in args.configs:
-        n = 100_000_000
-        c0, c1 = gen_int(n, 1 << 20, 42), gen_int(n, 1 << 20, 43)
-        c2, c3 = gen_int(n, 10, 44), gen_int(n, 10, 45)
-        t = ctx.wrap([(M.INTEGER, 4)] * 4, [x.data_ptr() for x in (c0, c1, c2, c3)], n)
+        N = args.c4_rows
+        s, e = D.shard_bounds(N, world, rank)
+        n = e - s
+        seed = 42 + 1000 * rank
+        c0, c1 = gen_int(n, 1 << 20, seed), gen_int(n, 1 << 20, seed + 1)
+        c2, c3 = gen_int(n, 10, seed + 2), gen_int(n, 10, seed + 3)
+        t = ctx.wrap([(M.INTEGER, 4)] * 4, [x.data_ptr() for x in (c0, c1, c2, c3)], n, row_offset=s)
         bm2 = ctx.index_build(t, 2, [("int", v) for v in range(10)])
         bm3 = ctx.index_build(t, 3, [("int", v) for v in range(10)])
         a, b = bm2[3], bm3[7]
         out = ctx.bitmap_alloc(n)
-        cap = n // 50
+        cap = max(1, n // 50)
         ids = torch.zeros(cap, dtype=torch.int64, device="cuda")
         o0 = torch.zeros(cap, dtype=torch.int32, device="cuda")
         o1 = torch.zeros(cap, dtype=torch.int32, device="cuda")
-        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        import ctypes
-        L = M.lib()
+        steps, warmup = args.steps, args.warmup
+        cnts = torch.zeros(steps + warmup, dtype=torch.int64, device="cuda")
+        counts_all = torch.zeros(steps + warmup, world, dtype=torch.int64, device="cuda")
         proj = (ctypes.c_int32 * 2)(0, 1)
         outs = (ctypes.c_void_p * 2)(o0.data_ptr(), o1.data_ptr())
+        bms = (ctypes.c_void_p * 2)(a.h.value, b.h.value)
+        offs = (ctypes.c_int32 * 3)(0, 1, 2)
 
-        def step():
-            ctx.bitmap_cnf_async([[a], [b]], out)
-            M._chk(L.mbx_materialize_async(ctx.h, t.h, out.h, proj, 2, ids.data_ptr(), outs, cnt.data_ptr()))
+        def and_():
+            M._chk(L.mbx_bitmap_cnf_async(ctx.h, bms, offs, 2, None, out.h))
 
-        ms = timed(ctx, ext, step, args.steps, args.warmup)
+        def query(k):
+            and_()
+            M._chk(L.mbx_materialize_async(ctx.h, t.h, out.h, proj, 2, ids.data_ptr(), outs, cnts.data_ptr() + 8 * k))
+            exchange(k, cnts[k:k + 1], counts_all)
+
+        ms = wall_ms(query, steps, warmup)
         sel = (c2 == 3) & (c3 == 7)
         want = int(sel.sum().item())
-        got = int(cnt.item())
+        got = int(cnts[-1].item())
         assert got == want and got <= cap, (got, want)
         assert bool((o0[:got] == c0[sel]).all()) and bool((o1[:got] == c1[sel]).all())
-        cnf_ms = timed(ctx, ext, lambda: ctx.bitmap_cnf_async([[a], [b]], out), args.steps, args.warmup)
-        byts = 3 * n / 8 + got * (8 + 8)
-        print(json.dumps({"config": "C4", "rows": n, "selected": got, "ms_per_query": ms, "rows_per_s": n / ms * 1e3,
-                          "algorithmic_gbs": byts / ms / 1e6, "bitmap_and_ms": cnf_ms,
-                          "bitmap_and_gbs": 3 * n / 8 / cnf_ms / 1e6, "gpus": 1,
-                          "note": "single-GPU; the 8-GPU config shards rows 1/8 per rank"}), flush=True)
+        assert bool((ids[:got] == torch.nonzero(sel).flatten() + s).all())
+        glob = got if world == 1 else int(D.combine_count(want, device="cuda" if backend == "nccl" else None))
+        if world > 1:
+            assert bool((counts_all[:, rank] == want).all()) and int(counts_all[-1].sum().item()) == glob
+        and_ms = kernel_ms(and_, steps, warmup)
+        sel_ms = kernel_ms(lambda: M._chk(L.mbx_materialize_async(ctx.h, t.h, out.h, proj, 2, ids.data_ptr(), outs,
+                                                                   cnts.data_ptr())), steps, warmup)
+        byts = 3 * N / 8 + glob * (8 + 8)
+        emit({"config": "C4", "rows": N, "gpus": world, "rows_per_gpu": n, "selected": glob,
+              "ms_per_query": ms, "rows_per_s": N / ms * 1e3, "algorithmic_gbs": byts / ms / 1e6,
+              "phases_ms": {"bitmap_and": and_ms, "positions_and_gather": sel_ms},
+              "bitmap_and_gbs": 3 * n / 8 / and_ms / 1e6,
+              "exchange": "none" if world == 1 else "all_gather of per-rank counts (side stream)",
+              "backend": backend if world > 1 else None})
         del c0, c1, c2, c3, t, bm2, bm3, a, b, out, ids, o0, o1
         torch.cuda.empty_cache()
 
     if "C5" in args.configs:
         names = [f"{chr(65 + (i * 7) % 26)}{'abcdefghijklmnop'[:(i % 15) + 1]}"[:16] for i in range(50)]
         dic = torch.zeros(50, 16, dtype=torch.uint8)
-        for i, s in enumerate(names):
-            dic[i, :len(s)] = torch.tensor(list(s.encode()), dtype=torch.uint8)
+        for i, nm in enumerate(names):
+            dic[i, :len(nm)] = torch.tensor(list(nm.encode()), dtype=torch.uint8)
         dic = dic.cuda()
-        for n in map(int, args.c5_rows.split(",")):
+        for N in map(int, args.c5_rows.split(",")):
+            s, e = D.shard_bounds(N, world, rank)
+            n = e - s
             g = torch.Generator(device="cuda")
-            g.manual_seed(5)
+            g.manual_seed(5 + 1000 * rank)
             c0 = torch.randint(0, 1 << 20, (n,), dtype=torch.int32, device="cuda", generator=g)
             c1 = torch.rand((n,), dtype=torch.float32, device="cuda", generator=g)
             idx = torch.randint(0, 50, (n,), dtype=torch.int64, device="cuda", generator=g)
             c2 = dic[idx]
             del idx
             t = ctx.wrap([(M.INTEGER, 4), (M.REAL, 4), (M.STRING, 16)], [c0.data_ptr(), c1.data_ptr(), c2.data_ptr()],
-                         n)
+                         n, row_offset=s)
             cnf = [[(M.LT, ("sym", 1), ("int", 1 << 19))], [(M.GE, ("sym", 2), ("real", 0.25))],
                    [(M.GE, ("sym", 3), ("str", "M"))]]
             plan = ctx.compile(t, cnf)
-            aggbuf = torch.zeros(6, dtype=torch.int64, device="cuda")
-            ms = timed(ctx, ext, lambda: ctx.scan_aggregate_async(plan, 1, aggbuf.data_ptr()), 10, 2)
-            res = ctx.scan_aggregate(plan, 1)
-            first = c2[:, 0]
-            sel = (c0 < (1 << 19)) & (c1 >= 0.25) & (first >= ord("M"))
+            steps, warmup = max(10, args.steps // 5), 2
+            W = D.AGG_WORDS
+            recs = torch.zeros(steps + warmup, W, dtype=torch.int64, device="cuda")
+            gathered = torch.zeros(steps + warmup, world * W, dtype=torch.int64, device="cuda")
+
+            def query(k):
+                ctx.scan_aggregate_async(plan, 1, recs[k].data_ptr())
+                exchange(k, recs[k], gathered)
+
+            ms = wall_ms(query, steps, warmup)
+            scan_ms = kernel_ms(lambda: ctx.scan_aggregate_async(plan, 1, recs[0].data_ptr()), steps, warmup)
+            # check: this rank's record vs torch, the folded global vs torch combined
+            sel = (c0 < (1 << 19)) & (c1 >= 0.25) & (c2[:, 0] >= ord("M"))
             want = int(sel.sum().item())
-            assert res["count"] == want, (res["count"], want)
+            mine = D.fold_aggregates(recs[-1].cpu().numpy())
+            assert mine["count"] == want, (mine["count"], want)
             ref_sum = float(c1[sel].double().sum().item())
-            assert abs(res["sum"] - ref_sum) <= 1e-6 * abs(ref_sum)
-            byts = n * (4 + 4 + 16)
-            print(json.dumps({"config": "C5", "rows": n, "selected": want, "ms_per_query": ms,
-                              "rows_per_s": n / ms * 1e3, "algorithmic_gbs": byts / ms / 1e6,
-                              "sum": res["sum"], "min": res["min"], "max": res["max"], "gpus": 1}), flush=True)
-            del c0, c1, c2, t, plan, sel, first
+            assert abs(mine["sum"] - ref_sum) <= 1e-6 * abs(ref_sum)
+            vals = c1[sel]
+            ref = dict(count=want, sum=ref_sum, min=float(vals.min().item()) if want else float("inf"),
+                       max=float(vals.max().item()) if want else float("-inf"))
+            assert mine["min"] == ref["min"] and mine["max"] == ref["max"]
+            if world > 1:
+                glob = D.fold_aggregates(gathered[-1].cpu().numpy())
+                gref = D.combine_aggregate(ref, device="cuda" if backend == "nccl" else None)
+                assert glob["count"] == gref["count"] and glob["min"] == gref["min"] and glob["max"] == gref["max"]
+                assert abs(glob["sum"] - gref["sum"]) <= 1e-6 * abs(gref["sum"])
+            else:
+                glob = mine
+            byts = N * (4 + 4 + 16)
+            emit({"config": "C5", "rows": N, "gpus": world, "rows_per_gpu": n, "selected": glob["count"],
+                  "ms_per_query": ms, "rows_per_s": N / ms * 1e3, "algorithmic_gbs": byts / ms / 1e6,
+                  "phases_ms": {"scan_aggregate": scan_ms},
+                  "scan_gbs_per_gpu": n * 24 / scan_ms / 1e6,
+                  "sum": glob["sum"], "min": glob["min"], "max": glob["max"],
+                  "exchange": "none" if world == 1 else "one all_gather of the 48-byte aggregate records (side stream)",
+                  "backend": backend if world > 1 else None})
+            del c0, c1, c2, t, plan, sel, vals
             torch.cuda.empty_cache()
     ctx.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

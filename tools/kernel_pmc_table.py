@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Per-kernel table from rocprofv3 CSV output: dispatches, average / median
+duration (kernel trace), median HBM read / write bytes per dispatch (PMC
+FETCH_SIZE x 2 x 1024 -- the gfx950 correction, MI355X_MICROARCH.md -- and
+WRITE_SIZE x 1024).  usage: kernel_pmc_table.py DIR [DIR...]"""
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+
+def rows_of(dirs, suffix):
+    out = []
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True):
+            with open(f) as fh:
+                out += list(csv.DictReader(fh))
+    return out
+
+
+def short(name):
+    n = name.split("(")[0]
+    return n.replace("void ", "").replace("mbx::", "")[:110]
+
+
+def main():
+    dirs = sys.argv[1:]
+    dur = collections.defaultdict(list)
+    for r in rows_of(dirs, "kernel_trace.csv"):
+        dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    ctr = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in rows_of(dirs, "counter_collection.csv"):
+        ctr[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    for k in sorted(set(dur) | set(ctr), key=lambda k: -sum(dur.get(k, [0]))):
+        if not k.startswith(("k_", "k_scan")) and "mbx" not in k and not k.startswith("k"):
+            continue
+        d = dur.get(k, [])
+        c = ctr.get(k, {})
+        line = {"kernel": k, "dispatches": len(d)}
+        if d:
+            line["avg_us"] = round(sum(d) / len(d) / 1e3, 2)
+            line["median_us"] = round(statistics.median(d) / 1e3, 2)
+        if "FETCH_SIZE" in c:
+            line["read_MB"] = round(2 * statistics.median(c["FETCH_SIZE"]) * 1024 / 1e6, 3)
+        if "WRITE_SIZE" in c:
+            line["write_MB"] = round(statistics.median(c["WRITE_SIZE"]) * 1024 / 1e6, 3)
+        for name, vals in c.items():
+            if name not in ("FETCH_SIZE", "WRITE_SIZE"):
+                line[name] = statistics.median(vals)
+        print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()
