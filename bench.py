@@ -11,8 +11,10 @@ own HIP stream and scratch); the default 1 runs one pass at a time.
 
 Multi-GPU (weak scaling): each rank owns its own 100M-row
 shard (rows [rank*N, (rank+1)*N) of one logical table); per step the ranks'
-counts are combined by one RCCL all_reduce on a side stream that overlaps the
-next step's scan.  value = total rows scanned by all ranks / max-over-ranks time.
+counts are combined by one RCCL all_reduce (async, ordered after that step's
+scan, overlapping the next step's scan).  value = total rows scanned by all
+ranks / max-over-ranks time.  MBX_BENCH_FORCE_EXCHANGE=1 keeps the exchange at
+N=1 (a one-rank RCCL group).  stdout carries only the JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R]
 """
@@ -107,6 +109,17 @@ def read_probe(ctx, table, ext, torch, reps=30):
     return {"best_gbs": res[best], "best": best, "gbs": res}
 
 
+def quiet_stdout():
+    """The one JSON line is the only thing on stdout: fd 1 is pointed at
+    stderr for the libraries (RCCL prints a version banner when it creates
+    its first communicator) and the result goes to a duplicate of the
+    original fd 1."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return fd
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +133,7 @@ def main():
                          "measured on MI355X the two concurrent passes then share fetches through the 256 MB "
                          "Infinity Cache (6.8 TB/s apparent), so the headline keeps 1: one pass at a time")
     args = ap.parse_args()
+    out_fd = quiet_stdout()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -135,7 +149,16 @@ def main():
     backend = os.environ.get("MBX_BENCH_BACKEND", "nccl")
     device = 0 if os.environ.get("MBX_BENCH_SAME_DEVICE") == "1" else local_rank
     torch.cuda.set_device(device)
-    if world > 1:
+    # MBX_BENCH_FORCE_EXCHANGE=1 keeps the per-step RCCL exchange at N=1 (a
+    # one-rank process group): the N>1 step, host enqueue cost included, on
+    # one GPU
+    exchange = world > 1 or os.environ.get("MBX_BENCH_FORCE_EXCHANGE") == "1"
+    if exchange and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if exchange:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
@@ -169,20 +192,32 @@ def main():
     counts = torch.zeros(steps + warmup, dtype=torch.int64, device="cuda")
     exts = [torch.cuda.ExternalStream(c.stream) for c in ctxs]
     ext = exts[0]
-    xs = torch.cuda.Stream() if world > 1 else None
+    if len(exts) == 1:
+        torch.cuda.set_stream(ext)  # collectives are ordered after the library stream's scans
     base = counts.data_ptr()
+
+    works = []
 
     def step(k):
         j = k % len(ctxs)
         ctxs[j].scan_count_async(plans[j], base + 8 * k)
-        if world > 1:  # the one exchange step: combine COUNT over ranks
-            ev = torch.cuda.Event()
-            ev.record(exts[j])
-            xs.wait_event(ev)
-            with torch.cuda.stream(xs):
-                dist.all_reduce(counts[k:k + 1])
+        if exchange:
+            # the one exchange step: combine this step's COUNT over ranks.  The
+            # collective's stream waits for the scan just enqueued on the
+            # library stream (the current stream); async_op=True keeps the
+            # library stream from waiting on the collective, so the next
+            # step's scan overlaps it.  Completion is waited for before the
+            # clock stops.
+            if len(exts) > 1:
+                with torch.cuda.stream(exts[j]):
+                    works.append(dist.all_reduce(counts[k:k + 1], async_op=True))
+            else:
+                works.append(dist.all_reduce(counts[k:k + 1], async_op=True))
 
     def sync_all():
+        for w in works:
+            w.wait()
+        works.clear()
         for c in ctxs:
             c.sync()
 
@@ -251,7 +286,7 @@ def main():
                 "rows_per_gpu": n,
                 "global_rows": n * world,
                 "parallelism": f"row-range shards x{world}" + (
-                    f", {'RCCL' if backend == 'nccl' else backend} all_reduce of COUNT per step" if world > 1 else ""),
+                    f", {'RCCL' if backend == 'nccl' else backend} all_reduce of COUNT per step" if exchange else ""),
                 "streams": len(ctxs),
             },
             "hbm_gbs": algo_bytes * world / (t_max / steps) / 1e9,
@@ -276,13 +311,13 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
 
     for t in tables:
         t.close()
     for c in ctxs:
         c.close()
-    if world > 1:
+    if exchange:
         dist.destroy_process_group()
 
 

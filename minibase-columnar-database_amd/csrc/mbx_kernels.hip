@@ -1124,6 +1124,7 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
                                                        int64_t* __restrict__ total) {
   __shared__ int64_t wcount[kWaves];
   __shared__ int64_t wpre[kWaves];
+  __shared__ uint16_t stage[kWaves][32 * 64];
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
   const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
@@ -1184,14 +1185,21 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
     for (int m = 32; m >= 1; m >>= 1) maxpc = max(maxpc, (uint32_t)__shfl_xor(maxpc, m));
     if (2 * maxpc <= (uint32_t)__popcll(nz)) {
       // sparse step: lane = word, each lane peels its own bits (max-popcount
-      // iterations instead of one per non-zero word)
+      // iterations instead of one per non-zero word) into the wave's LDS
+      // stage (12-bit offsets within the step; maxpc <= 32 here, so at most
+      // 2048 of them), then the wave copies them out with coalesced stores
+      // -- written straight from the peel loop, one store instruction spread
+      // over ~26 cache lines
+      uint16_t* st = stage[wave];
       uint64_t m = mw;
-      int64_t o = off + excl;
-      const int64_t rbase = row_offset + (base + lane) * 64;
+      uint32_t o = excl;
       while (m) {
-        ids[o++] = rbase + __builtin_ctzll(m);
+        st[o++] = (uint16_t)(lane * 64 + __builtin_ctzll(m));
         m &= m - 1ull;
       }
+      __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+      const int64_t rbase = row_offset + base * 64;
+      for (uint32_t i = lane; i < total; i += 64) ids[off + i] = rbase + st[i];
       nz = 0;
     }
     while (nz) {

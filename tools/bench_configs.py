@@ -44,8 +44,12 @@ def main():
     ap.add_argument("--c4-rows", type=int, default=100_000_000, help="global rows")
     ap.add_argument("--c5-rows", default="125000000,1000000000", help="global rows, comma separated")
     args = ap.parse_args()
+    # JSON lines only on stdout: libraries (RCCL's version banner) write to fd 1
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world =int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -136,7 +140,7 @@ def main():
 
     def emit(d):
         if rank == 0:
-            print(json.dumps(d), flush=True)
+            os.write(out_fd, (json.dumps(d) + "\n").encode())
 
     if "C2" in args.configs and world == 1:
         n = 10_000_000
