@@ -51,6 +51,21 @@ static int64_t tiles_per_block_for(int64_t nrows) {
   return choose_tiles_per_block(nrows);
 }
 
+// COUNT / aggregate scans choose their own grid (BitSet scans follow the
+// output bitmap's segments).  Plans with 16-byte string slots do more work per
+// byte and run best with ~4096 blocks (C5, 125M rows: 483 -> 470 us; 1B rows:
+// 3908 -> 3729 us, profiles/r01/round_e); 4-byte-only plans with ~1024.
+static int64_t scan_tiles_per_block(int64_t nrows, const PlanVariant& v) {
+  const char* e = getenv("MBX_TILES_PER_BLOCK");
+  if (e && atoll(e) > 0) return atoll(e);
+  if (v.fast_ks > 0) {
+    const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+    const int64_t tpb = (ntiles + 4095) / 4096;
+    return tpb < 4 ? 4 : tpb;
+  }
+  return choose_tiles_per_block(nrows);
+}
+
 static int ensure_partials(mbx_ctx* c, int64_t n) {
   if (n <= c->partials_cap) return MBX_OK;
   if (c->partials) HIPCHK(hipFree(c->partials));
@@ -734,7 +749,7 @@ static int scan_to_count(mbx_ctx* c, mbx_plan* p, int64_t* dev_count, int32_t* d
   PlanVariant* v = nullptr;
   int rc = plan_variant(p, -1, &v);
   if (rc) return rc;
-  const int64_t tpb = tiles_per_block_for(p->t->nrows);
+  const int64_t tpb = scan_tiles_per_block(p->t->nrows, *v);
   const int64_t nb = grid_blocks(p->t->nrows, tpb);
   if ((rc = ensure_partials(c, nb))) return rc;
   return enqueue_scan(c, p, *v, kModeCount, nullptr, c->partials, tpb, dev_count, nullptr, dev_nan);
@@ -840,7 +855,7 @@ static int scan_agg(mbx_ctx* c, mbx_plan* p, int32_t agg_col, AggOut* dev_out, i
   PlanVariant* v = nullptr;
   int rc = plan_variant(p, agg_col, &v);
   if (rc) return rc;
-  const int64_t tpb = tiles_per_block_for(p->t->nrows);
+  const int64_t tpb = scan_tiles_per_block(p->t->nrows, *v);
   const int64_t nb = grid_blocks(p->t->nrows, tpb);
   if ((rc = ensure_partials(c, nb))) return rc;
   return enqueue_scan(c, p, *v, kModeAgg, nullptr, c->partials, tpb, nullptr, dev_out, dev_nan);
