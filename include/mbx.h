@@ -182,6 +182,15 @@ int mbx_scan_count_async(mbx_ctx *ctx, const mbx_plan *p, int64_t *dev_count);
 /* the selection as a device BitSet (the get_next_tid() stream as positions) */
 int mbx_scan_bitmap(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap **out, int64_t *count);
 int mbx_scan_bitmap_async(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap *out);
+/* the get_next_tid() stream as ascending positions (TID.position, global:
+ * row_offset added): BitSet + positions in ONE kernel launch for fast-kernel
+ * plans (SURVEY 8(b) mbx_scan_select); host_ids holds up to cap positions */
+int mbx_scan_select(mbx_ctx *ctx, const mbx_plan *p, int64_t *host_ids, int64_t cap, int64_t *n);
+/* enqueue only: BitSet into `out` (nbits = the table's rows), positions into
+ * dev_ids (capacity: the selected rows, at most the table's rows), the count
+ * into *dev_count (device memory) */
+int mbx_scan_select_async(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap *out, int64_t *dev_ids,
+                          int64_t *dev_count);
 /* COUNT/SUM/MIN/MAX of column `agg_col` (0-based) over the selection */
 int mbx_scan_aggregate(mbx_ctx *ctx, const mbx_plan *p, int32_t agg_col, mbx_agg *out);
 int mbx_scan_aggregate_async(mbx_ctx *ctx, const mbx_plan *p, int32_t agg_col, mbx_agg *dev_out);

@@ -331,6 +331,55 @@ __device__ __forceinline__ uint64_t pack_word16(uint32_t nib, int lane) {
   return (lane & 8) ? (((uint64_t)v32 << 32) | o) : ((uint64_t)v32 | ((uint64_t)o << 32));
 }
 
+// Positions of one step of 64 consecutive BitSet words (lane = word `base +
+// lane`, mw = its bits) to ids[off ...]; off advances by the step's count.
+// Sparse steps (2 * max popcount <= non-zero words): each lane peels its own
+// bits into the wave's LDS stage `st` (12-bit offsets within the step; at
+// most 2048 of them), then the wave copies them out with coalesced stores --
+// stored straight from the peel loop, one store instruction spreads over ~26
+// cache lines.  Dense steps: lane = bit, one coalesced store per non-zero
+// word.
+__device__ __forceinline__ void emit_step(int64_t base, uint64_t mw, int64_t& off, int64_t row_offset,
+                                          int64_t* __restrict__ ids, uint16_t* st, int lane) {
+  const uint32_t pc = (uint32_t)__popcll(mw);
+  uint32_t incl = pc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d);
+    if (lane >= d) incl += y;
+  }
+  const uint32_t excl = incl - pc;
+  const uint32_t total = __shfl(incl, 63);
+  uint64_t nz = __ballot(mw != 0ull);
+  uint32_t maxpc = pc;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) maxpc = max(maxpc, (uint32_t)__shfl_xor(maxpc, m));
+  if (2 * maxpc <= (uint32_t)__popcll(nz)) {
+    uint64_t m = mw;
+    uint32_t o = excl;
+    while (m) {
+      st[o++] = (uint16_t)(lane * 64 + __builtin_ctzll(m));
+      m &= m - 1ull;
+    }
+    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+    const int64_t rbase = row_offset + base * 64;
+    for (uint32_t i = lane; i < total; i += 64) ids[off + i] = rbase + st[i];
+    __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next step
+    nz = 0;
+  }
+  while (nz) {
+    const int j = __builtin_ctzll(nz);
+    nz &= nz - 1ull;
+    const uint64_t m = __shfl(mw, j);
+    const uint32_t slot = __shfl(excl, j);
+    if ((m >> lane) & 1ull) {
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      ids[off + slot + below] = row_offset + (base + j) * 64 + lane;
+    }
+  }
+  off += total;
+}
+
 // ------------------------------------------------------------- fast scan
 //
 // K 4-byte columns in plan slots 0..K-1, every term `slot OP literal`.
@@ -1135,6 +1184,19 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   // a wave range of <= 64 * kSelRegs words is loaded once, all loads in
   // flight together, and kept in registers for the write pass
   const bool cached = a1 - a0 <= 64 * kSelRegs;
+  // this block's output offset: the segment counts before it, 4 loads in
+  // flight per thread, issued before the word loads so both latencies overlap
+  int64_t pre = 0;
+  for (int64_t i0 = 0; i0 < (int64_t)blockIdx.x; i0 += 4 * kBlock) {
+    int64_t v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = i0 + k * kBlock + threadIdx.x;
+      v[k] = i < (int64_t)blockIdx.x ? seg_parts[i].count : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pre += v[k];
+  }
   uint64_t wr[kSelRegs];
   int64_t c = 0;
   if (cached) {
@@ -1148,8 +1210,6 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   } else {
     for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(words[w]);
   }
-  int64_t pre = 0;
-  for (int64_t i = threadIdx.x; i < (int64_t)blockIdx.x; i += kBlock) pre += seg_parts[i].count;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
     c += __shfl_xor(c, m);
@@ -1169,52 +1229,7 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   }
   for (int k = 0; k < wave; ++k) off += wcount[k];
   // one step = 64 consecutive words, lane = word
-  auto step = [&](int64_t base, uint64_t mw) {
-    const uint32_t pc = (uint32_t)__popcll(mw);
-    uint32_t incl = pc;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
-    }
-    const uint32_t excl = incl - pc;
-    const uint32_t total = __shfl(incl, 63);
-    uint64_t nz = __ballot(mw != 0ull);
-    uint32_t maxpc = pc;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) maxpc = max(maxpc, (uint32_t)__shfl_xor(maxpc, m));
-    if (2 * maxpc <= (uint32_t)__popcll(nz)) {
-      // sparse step: lane = word, each lane peels its own bits (max-popcount
-      // iterations instead of one per non-zero word) into the wave's LDS
-      // stage (12-bit offsets within the step; maxpc <= 32 here, so at most
-      // 2048 of them), then the wave copies them out with coalesced stores
-      // -- written straight from the peel loop, one store instruction spread
-      // over ~26 cache lines
-      uint16_t* st = stage[wave];
-      uint64_t m = mw;
-      uint32_t o = excl;
-      while (m) {
-        st[o++] = (uint16_t)(lane * 64 + __builtin_ctzll(m));
-        m &= m - 1ull;
-      }
-      __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
-      const int64_t rbase = row_offset + base * 64;
-      for (uint32_t i = lane; i < total; i += 64) ids[off + i] = rbase + st[i];
-      nz = 0;
-    }
-    while (nz) {
-      const int j = __builtin_ctzll(nz);
-      nz &= nz - 1ull;
-      const uint64_t m = __shfl(mw, j);
-      const uint32_t slot = __shfl(excl, j);
-      if ((m >> lane) & 1ull) {
-        const uint32_t below =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        ids[off + slot + below] = row_offset + (base + j) * 64 + lane;
-      }
-    }
-    off += total;
-  };
+  auto step = [&](int64_t base, uint64_t mw) { emit_step(base, mw, off, row_offset, ids, stage[wave], lane); };
   if (cached) {
 #pragma unroll
     for (int r = 0; r < kSelRegs; ++r) {

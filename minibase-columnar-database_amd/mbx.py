@@ -81,7 +81,8 @@ def java_mutf8(s):
 EXPORTS = [
     "mbx_abi_version", "mbx_last_error", "mbx_device_count", "mbx_init", "mbx_free", "mbx_sync", "mbx_stream",
     "mbx_table_stage", "mbx_table_wrap", "mbx_table_free", "mbx_table_info", "mbx_plan_compile", "mbx_plan_free",
-    "mbx_scan_count", "mbx_scan_count_async", "mbx_scan_bitmap", "mbx_scan_bitmap_async", "mbx_scan_aggregate",
+    "mbx_scan_count", "mbx_scan_count_async", "mbx_scan_bitmap", "mbx_scan_bitmap_async", "mbx_scan_select",
+    "mbx_scan_select_async", "mbx_scan_aggregate",
     "mbx_scan_aggregate_async", "mbx_bitmap_alloc", "mbx_bitmap_upload", "mbx_bitmap_download", "mbx_bitmap_info",
     "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_bitmap_index_build",
     "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
@@ -138,6 +139,8 @@ def lib():
         "mbx_scan_count_async": ([V, V, V], ctypes.c_int),
         "mbx_scan_bitmap": ([V, V, P(V), P(I64)], ctypes.c_int),
         "mbx_scan_bitmap_async": ([V, V, V], ctypes.c_int),
+        "mbx_scan_select": ([V, V, V, I64, P(I64)], ctypes.c_int),
+        "mbx_scan_select_async": ([V, V, V, V, V], ctypes.c_int),
         "mbx_scan_aggregate": ([V, V, I32, P(Agg)], ctypes.c_int),
         "mbx_scan_aggregate_async": ([V, V, I32, V], ctypes.c_int),
         "mbx_bitmap_alloc": ([V, I64, P(V)], ctypes.c_int),
@@ -415,6 +418,17 @@ class Context:
     def scan_bitmap_async(self, plan, bitmap):
         _chk(lib().mbx_scan_bitmap_async(self.h, plan.h, bitmap.h))
 
+    def scan_select(self, plan, cap=None):
+        """Ascending global positions of the rows the plan selects (one launch)."""
+        cap = plan.table.nrows if cap is None else cap
+        ids = np.zeros(max(1, cap), dtype=np.int64)
+        n = ctypes.c_int64()
+        _chk(lib().mbx_scan_select(self.h, plan.h, ids.ctypes.data, cap, ctypes.byref(n)))
+        return ids[:n.value]
+
+    def scan_select_async(self, plan, bitmap, dev_ids, dev_count):
+        _chk(lib().mbx_scan_select_async(self.h, plan.h, bitmap.h, dev_ids, dev_count))
+
     def scan_aggregate(self, plan, col):
         a = Agg()
         _chk(lib().mbx_scan_aggregate(self.h, plan.h, col, ctypes.byref(a)))
@@ -480,7 +494,8 @@ class Context:
 
     def select(self, bitmap, row_offset=0):
         n = ctypes.c_int64()
-        cap = max(1, bitmap.count)
+        known = bitmap.count  # -1 after an async producer: the library counts first
+        cap = max(1, known if known >= 0 else bitmap.nbits)
         ids = np.zeros(cap, dtype=np.int64)
         _chk(lib().mbx_bitmap_select(self.h, bitmap.h, row_offset, ids.ctypes.data, cap, ctypes.byref(n)))
         return ids[:n.value]

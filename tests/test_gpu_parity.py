@@ -222,6 +222,60 @@ def test_bitset_segments_and_tile_layouts(ctx, tpb, ri, deleted, monkeypatch):
     assert np.array_equal(ids, np.nonzero(np.unpackbits(want.view(np.uint8), bitorder="little"))[0][:bm.count])
 
 
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 255, 256, 257, 4099, 70001, 1_000_003])
+def test_scan_select_positions(ctx, n):
+    """mbx_scan_select gives the oracle's get_next_tid positions (global:
+    the shard's row_offset added), launch after launch."""
+    cols, dele = int_table(n, hi=100, deleted_frac=0.05)
+    ot, t = oracle.Table(cols, dele), ctx.stage(cols, dele, row_offset=640)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", 50))], [(oracle.GE, ("sym", 2), ("int", 10)),
+                                                      (oracle.EQ, ("sym", 3), ("int", 7))]]
+    n_o, w_o, ids_o = oracle.filescan(ot, cnf)
+    plan = ctx.compile(t, cnf)
+    for _ in range(3):
+        assert np.array_equal(ctx.scan_select(plan), ids_o + 640)
+
+
+@pytest.mark.parametrize("tpb", [4, 37, 200, 512, 513, 1000])
+def test_scan_select_segment_sizes(ctx, tpb, monkeypatch):
+    """Segments of 16..4000 words; positions and the BitSet left in the
+    bitmap both exact, also through the async entry point."""
+    monkeypatch.setenv("MBX_TILES_PER_BLOCK", str(tpb))
+    n = 3_000_017
+    cols, _ = int_table(n, hi=1000)
+    t = ctx.stage(cols)
+    plan = ctx.compile(t, [[(oracle.LT, ("sym", 1), ("int", 300))]])
+    mask = cols[0][2] < 300
+    ids = ctx.scan_select(plan)
+    assert np.array_equal(ids, np.nonzero(mask)[0])
+    import torch
+    bm = ctx.bitmap_alloc(n)
+    dev_ids = torch.zeros(n, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.scan_select_async(plan, bm, dev_ids.data_ptr(), cnt.data_ptr())
+    ctx.sync()
+    k = int(cnt.item())
+    assert k == int(mask.sum())
+    assert np.array_equal(dev_ids[:k].cpu().numpy(), ids)
+    assert np.array_equal(bm.download(), _np_words(mask))
+    assert bm.count == -1  # unknown after an async call until something needs it
+    assert np.array_equal(ctx.select(bm), ids)  # via the segment counts the scan left
+    assert bm.count == k
+
+
+@pytest.mark.parametrize("generic", [False, True])
+def test_scan_select_strings_and_floats(ctx, generic, monkeypatch):
+    """String-slot (KS > 0) and float plans, fast and generic kernels."""
+    if generic:
+        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+    cols, _ = mixed_table(200_003, seed=11)
+    ot, t = oracle.Table(cols), ctx.stage(cols)
+    cnf = [[(oracle.GE, ("sym", 3), ("str", "M"))], [(oracle.LT, ("sym", 2), ("real", 0.5)),
+                                                      (oracle.LT, ("sym", 1), ("int", 1000))]]
+    n_o, w_o, ids_o = oracle.filescan(ot, cnf)
+    assert np.array_equal(ctx.scan_select(ctx.compile(t, cnf)), ids_o)
+
+
 @pytest.mark.parametrize("op", [oracle.EQ, oracle.LT, oracle.GT, oracle.NE, oracle.LE, oracle.GE, oracle.NOT,
                                 oracle.NOP, oracle.RANGE])
 @pytest.mark.parametrize("lit_left", [False, True])

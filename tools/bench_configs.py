@@ -49,7 +49,7 @@ def main():
     out_fd = os.dup(1)
     os.dup2(2, 1)
 
-    world =int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -151,9 +151,8 @@ def main():
         ids = torch.zeros(n, dtype=torch.int64, device="cuda")
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
 
-        def step(k=0):
-            ctx.scan_bitmap_async(plan, bm)
-            M._chk(L.mbx_materialize_async(ctx.h, t.h, bm.h, None, 0, ids.data_ptr(), None, cnt.data_ptr()))
+        def step(k=0):  # BitSet + positions + COUNT: one launch (mbx_scan_select_async)
+            M._chk(L.mbx_scan_select_async(ctx.h, plan.h, bm.h, ids.data_ptr(), cnt.data_ptr()))
 
         ms = kernel_ms(step, args.steps, args.warmup)
         want = int((cols[0] < 104858).sum().item())

@@ -7,6 +7,7 @@ own bitmaps.  Per setting, HIP-event times on the library stream of
   scan_count   (c0 < 104858)                      k_scan_fast<1, COUNT>
   scan_bitmap  (c0 < 104858) -> BitSet            k_scan_fast<1, BITMAP>
   select       BitSet -> positions                k_select_ids
+  scan_select  BitSet + positions, one launch     k_scan_fast<1, SELECT> (mbx_scan_select_async)
   and          bm_a AND bm_b (random 10 % / 10 %) k_bitmap_cnf
   and_sel_g    AND + positions + gather c0, c1    (C4 query)
 Interleaved rounds, median of rounds.  One JSON line per (rows, tpb).
@@ -28,7 +29,7 @@ def main():
     ap.add_argument("--tpb", default="0,2,4,8,12,16,24")
     ap.add_argument("--launches", type=int, default=30)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--ops", default="scan_count,scan_bitmap,select,and,and_sel_g")
+    ap.add_argument("--ops", default="scan_count,scan_bitmap,select,scan_select,and,and_sel_g")
     args = ap.parse_args()
 
     import numpy as np
@@ -95,6 +96,12 @@ def main():
                                                                                 ids.data_ptr(), None,
                                                                                 cnt.data_ptr() + 8)))
                     assert int(cnt[1].item()) == want
+                if "scan_select" in ops:  # BitSet + positions in one launch (C2's query)
+                    r["scan_select"] = timed(lambda: M._chk(L.mbx_scan_select_async(ctx.h, plan.h, bm.h, ids.data_ptr(),
+                                                                                    cnt.data_ptr() + 24)))
+                    if not os.environ.get("SWEEP_NOCHECK"):  # A/B knobs that drop work
+                        assert int(cnt[3].item()) == want
+                        assert bool((ids[:want] == torch.nonzero(cols[0] < 104858).flatten()).all())
                 # ctypes arguments built once: the launch itself is what is timed
                 bms = (ctypes.c_void_p * 2)(ba.h.value, bb.h.value)
                 offs = (ctypes.c_int32 * 3)(0, 1, 2)
@@ -115,7 +122,7 @@ def main():
         os.environ.pop("MBX_TILES_PER_BLOCK", None)
         for tp in tpbs:
             line = {"rows": n, "tpb": tp or "default"}
-            for k in ["scan_count", "scan_bitmap", "select", "and", "and_sel_g"]:
+            for k in ["scan_count", "scan_bitmap", "select", "scan_select", "and", "and_sel_g"]:
                 if (tp, k) in res:
                     line[k + "_us"] = round(statistics.median(res[(tp, k)]), 2)
             print(json.dumps(line), flush=True)
