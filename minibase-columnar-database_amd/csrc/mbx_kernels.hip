@@ -191,8 +191,22 @@ __device__ __forceinline__ void finalize_block(const Partial* parts, int64_t n, 
   __shared__ Acc fsh[kWaves];
   Acc a;
   acc_init(a);
-  for (int64_t i = threadIdx.x; i < n; i += kBlock)
-    acc_merge(a, LITE ? load_count_sc1(parts + i) : from_partial(SC1 ? load_partial_sc1(parts + i) : parts[i]));
+  // 4 partials' loads in flight per thread, then folded in the same order
+  // (i, i + 256, ...) -- one at a time, each sc1 load's trip to memory was
+  // paid serially (4 per thread at 1024 blocks)
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += 4 * kBlock) {
+    Acc b[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = i0 + (int64_t)k * kBlock;
+      if (i < n)
+        b[k] = LITE ? load_count_sc1(parts + i) : from_partial(SC1 ? load_partial_sc1(parts + i) : parts[i]);
+      else
+        acc_init(b[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc_merge(a, b[k]);
+  }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
     Acc b = shfl_xor_acc(a, m);
