@@ -46,3 +46,23 @@ def test_two_rank_gloo_combine_gpu_shards():
 
 def test_three_rank_gloo_combine_cpu():
     _spawn("oracle", world=3)
+
+
+def test_fold_aggregates_rank_order_and_empty_shards():
+    """The one-collective combine's fold (dist.fold_aggregates): int64 sums
+    exact, the double SUM added in rank order, MIN/MAX with empty shards
+    carrying the identities (INT32_MAX / INT32_MIN, +inf / -inf)."""
+    import numpy as np
+    D = mbx_pkg.load().dist
+    ints = [dict(count=3, sum=10, min=-4, max=9), dict(count=0, sum=0, min=2**31 - 1, max=-2**31),
+            dict(count=2, sum=-7, min=-8, max=1)]
+    recs = np.concatenate([D.pack_aggregate(a, True) for a in ints])
+    assert D.fold_aggregates(recs) == dict(count=5, sum=3, min=-8, max=9)
+    fl = [dict(count=1, sum=1e16, min=0.5, max=0.5), dict(count=0, sum=0.0, min=float("inf"), max=float("-inf")),
+          dict(count=2, sum=1.0, min=0.25, max=0.75), dict(count=1, sum=-1e16, min=0.125, max=0.125)]
+    recs = np.concatenate([D.pack_aggregate(a, False) for a in fl])
+    got = D.fold_aggregates(recs)
+    want = ((1e16 + 0.0) + 1.0) + -1e16  # rank order, as a sequential double sum
+    assert got == dict(count=4, sum=want, min=0.125, max=0.75)
+    # the record layout is the C-ABI's mbx_agg (48 bytes)
+    assert D.AGG_RECORD.itemsize == 48 and D.AGG_WORDS == 6
