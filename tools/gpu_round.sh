@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-round}
 mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; exit 1; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo SMOKE_FAIL; exit 1; }
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo BENCH_FAIL; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o c3 --output-format csv -- python3 bench.py --steps 100 --warmup 10 --no-cpu-baseline > $OUT/kt.log 2>&1 || { echo KT_FAIL; exit 1; }
