@@ -100,3 +100,17 @@ def random_deleted(n, frac, seed=7):
     idx = np.nonzero(bits)[0]
     np.bitwise_or.at(words, idx // 64, (np.uint64(1) << (idx % 64).astype(np.uint64)))
     return words
+
+
+def device_dictionary_column(dic, idx, chunk=1 << 23):
+    """dic[idx] for a device dictionary `dic` (V, w) and device codes `idx`
+    (n,), built chunk by chunk.  One torch advanced-index launch with a large
+    output returns wrong rows on this ROCm image (measured: dic.view(int64)[idx]
+    over 200M rows left 2^27 rows zero and 67 % of sampled rows wrong), so each
+    launch writes at most `chunk` rows and the caller checks the result."""
+    import torch
+    n = idx.shape[0]
+    out = torch.empty((n,) + tuple(dic.shape[1:]), dtype=dic.dtype, device=dic.device)
+    for s in range(0, n, chunk):
+        out[s:s + chunk].copy_(dic[idx[s:s + chunk].long()])
+    return out
