@@ -14,6 +14,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -698,6 +699,13 @@ extern "C" int mbx_plan_free(mbx_plan* p) {
 
 // ------------------------------------------------------------------- scans
 
+// kFinPackedCount's 64-bit ticket words hold < 4096 arrivals and NaN blocks
+// per word and a 40-bit count (mbx_kernels.hip, packed_count_finalize).
+static bool packed_count_fits(int64_t nrows, int64_t nb, int32_t groups) {
+  const int64_t per_word = (groups > 1 && nb > groups) ? std::max<int64_t>((nb + groups - 1) / groups, groups) : nb;
+  return per_word < 4096 && nrows < (int64_t(1) << 40);
+}
+
 // One launch per scan: the kernel's last block finalizes (count / aggregate /
 // NaN flag) through the context's ticket.
 static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int32_t mode, uint64_t* out_words,
@@ -733,12 +741,15 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
     const int pol = ri ? atoi(ri) : 1;
     L.ri = pol == 2 || (pol == 1 && mode == kModeBitmap);
   }
-  const char* fm = getenv("MBX_FIN_MODE");
-  L.fin_mode = fm ? atoi(fm) : kFinWriteThrough;
-  if (L.fin_mode == kFinSeparate) L.ticket = nullptr;
   const char* tg = getenv("MBX_TICKET_GROUPS");
   L.ticket_groups = tg ? atoi(tg) : kDefaultTicketGroups;
   if (L.ticket_groups < 0 || L.ticket_groups > kMaxTicketGroups) L.ticket_groups = kDefaultTicketGroups;
+  const char* fm = getenv("MBX_FIN_MODE");
+  L.fin_mode = fm ? atoi(fm) : (mode == kModeCount ? kFinPackedCount : kFinWriteThrough);
+  if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))
+    L.fin_mode = kFinWriteThrough;
+  if (L.fin_mode == kFinPackedCount && mode != kModeCount) L.fin_mode = kFinWriteThrough;
+  if (L.fin_mode == kFinSeparate) L.ticket = nullptr;
   HIPCHK(launch_scan(L, c->stream));
   if (L.fin_mode == kFinSeparate)
     HIPCHK(launch_finalize(parts, grid_blocks(L.nrows, tpb), L.agg_kind, agg_out, count_out, nan_out, c->stream));

@@ -137,6 +137,9 @@ enum FinMode : int32_t {
   kFinWriteThrough = 0,  // sc1 partial stores + ticket, sc1 loads by the last block
   kFinFences = 1,        // plain stores + agent release / acquire fences
   kFinSeparate = 2,      // no ticket: a separate k_finalize launch
+  kFinPackedCount = 3,   // COUNT: each block adds (count, nan, 1) packed in one
+                         // 64-bit word to its group's ticket; the last arriver
+                         // of the top ticket holds the total -- no partials
 };
 
 struct ProjCol {

@@ -259,6 +259,50 @@ __device__ __forceinline__ bool arrive(uint32_t* ticket, int groups) {
   return true;
 }
 
+// COUNT finalize without partials (kFinPackedCount).  One 64-bit atomic word
+// per ticket: bits 0..11 arrivals, 12..23 blocks that saw a NaN, 24..63 the
+// row count.  Integer addition is order-free, so the total is exact and the
+// same for every arrival order.  The last arriver of a group adds the group's
+// sum to the top word; the last arriver of the top word holds the launch's
+// total, writes it, and (like every last arriver) resets its word for the
+// next launch on the stream.  One dependent atomic round trip per level, no
+// partial stores or loads (the sc1 path pays store, ticket and load trips).
+constexpr int kPackArrBits = 12, kPackNanBits = 12;
+constexpr uint64_t kPackArrMask = (1ull << kPackArrBits) - 1;
+constexpr uint64_t kPackNanMask = (1ull << kPackNanBits) - 1;
+
+__device__ __forceinline__ uint64_t pack_count(int64_t count, uint32_t nan_blocks) {
+  return ((uint64_t)count << (kPackArrBits + kPackNanBits)) | ((uint64_t)nan_blocks << kPackArrBits) | 1ull;
+}
+
+// true for the last arriver; *sum = the word's total including this add
+__device__ __forceinline__ bool packed_arrive(uint64_t* w, uint64_t add, uint32_t members, uint64_t* sum) {
+  const uint64_t prev = __hip_atomic_fetch_add(w, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((prev & kPackArrMask) != members - 1) return false;
+  __hip_atomic_store(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *sum = prev + add;
+  return true;
+}
+
+__device__ __forceinline__ void packed_count_finalize(uint32_t* ticket, int groups, int64_t count, int nan,
+                                                      int64_t* count_out, int32_t* nan_out) {
+  const uint32_t nb = gridDim.x;
+  uint64_t add = pack_count(count, nan ? 1u : 0u), sum;
+  if (groups > 1 && nb > (uint32_t)groups) {
+    const uint32_t G = (uint32_t)groups;
+    const uint32_t g = blockIdx.x % G;
+    const uint32_t members = (nb - g + G - 1) / G;
+    if (!packed_arrive(reinterpret_cast<uint64_t*>(ticket + (1 + g) * kTicketStride), add, members, &sum)) return;
+    const uint64_t nan_g = (sum >> kPackArrBits) & kPackNanMask;
+    add = pack_count((int64_t)(sum >> (kPackArrBits + kPackNanBits)), nan_g ? 1u : 0u);
+    if (!packed_arrive(reinterpret_cast<uint64_t*>(ticket), add, G, &sum)) return;
+  } else if (!packed_arrive(reinterpret_cast<uint64_t*>(ticket), add, nb, &sum)) {
+    return;
+  }
+  if (count_out) *count_out = (int64_t)(sum >> (kPackArrBits + kPackNanBits));
+  if (nan_out) *nan_out = ((sum >> kPackArrBits) & kPackNanMask) ? 1 : 0;
+}
+
 // Block-wide fixed-order reduction of per-thread accumulators into this
 // block's Partial; with a ticket, the last block to arrive then finalizes all
 // partials inside the same launch.  Hand-off (MI355X: per-XCD L2s are not
@@ -285,6 +329,15 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
   }
   if (lane == 0) sh[wave] = a;
   __syncthreads();
+  if (!FULL && L.ticket && L.fin_mode == kFinPackedCount) {
+    if (threadIdx.x == 0) {
+      Acc r = sh[0];
+#pragma unroll
+      for (int w = 1; w < kWaves; ++w) acc_merge(r, sh[w]);
+      packed_count_finalize(L.ticket, L.ticket_groups, r.count, r.nan, L.count_out, L.nan_out);
+    }
+    return;
+  }
   if (threadIdx.x == 0) {
     Acc r = sh[0];
 #pragma unroll
