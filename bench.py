@@ -233,11 +233,14 @@ def main():
     t0 = time.perf_counter()
     for k in range(steps):
         step(warmup + k)
+    t_enq = time.perf_counter() - t0  # host enqueue time of the steps (diagnostic, stderr)
     sync_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    print(f"rank {rank}: host enqueue {t_enq * 1e6 / steps:.1f} us/step, wall {wall * 1e6 / steps:.1f} us/step",
+          file=sys.stderr)
     c = counts[warmup:].cpu()
 
     # kernel duration: the same launches again, each bracketed by HIP events

@@ -1,7 +1,10 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/exp10; mkdir -p $OUT
-for r in 10000000 100000000; do
-timeout -k 10 200 python -u tools/ab_tmp.py $r >> $OUT/ab.jsonl 2> $OUT/ab.err || { tail $OUT/ab.err; exit 1; }
+OUT=gpurun_out/exp14; mkdir -p $OUT
+for mode in none marker exchange; do
+env_args=""
+[ $mode = marker ] && export MARKER_ONLY=1 || unset MARKER_ONLY
+[ $mode = exchange ] && export MBX_BENCH_FORCE_EXCHANGE=1 || unset MBX_BENCH_FORCE_EXCHANGE
+timeout -k 10 200 python -u tools/bench_marker_tmp.py --steps 200 --warmup 20 --no-cpu-baseline > $OUT/b_$mode.json 2> $OUT/b_$mode.err || { tail $OUT/b_$mode.err; exit 1; }
+echo $mode; grep 'host enqueue' $OUT/b_$mode.err
 done
-cat $OUT/ab.jsonl
