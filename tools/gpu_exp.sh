@@ -1,10 +1,9 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/exp14; mkdir -p $OUT
-for mode in none marker exchange; do
-env_args=""
-[ $mode = marker ] && export MARKER_ONLY=1 || unset MARKER_ONLY
-[ $mode = exchange ] && export MBX_BENCH_FORCE_EXCHANGE=1 || unset MBX_BENCH_FORCE_EXCHANGE
-timeout -k 10 200 python -u tools/bench_marker_tmp.py --steps 200 --warmup 20 --no-cpu-baseline > $OUT/b_$mode.json 2> $OUT/b_$mode.err || { tail $OUT/b_$mode.err; exit 1; }
-echo $mode; grep 'host enqueue' $OUT/b_$mode.err
+OUT=gpurun_out/exp15; mkdir -p $OUT
+for rep in 1 2; do
+for v in 0 21; do
+MBX_SCAN_VARIANT=$v timeout -k 10 200 python -u tools/small_sweep.py --rows 10000000,12500000,100000000 --tpb 0 --ops scan_count,scan_bitmap,select,scan_select --rounds 3 > $OUT/v$v.$rep.jsonl 2> $OUT/v$v.err || { tail $OUT/v$v.err; exit 1; }
+echo "variant $v rep $rep"; cat $OUT/v$v.$rep.jsonl
+done
 done
