@@ -745,10 +745,10 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.ticket_groups = tg ? atoi(tg) : kDefaultTicketGroups;
   if (L.ticket_groups < 0 || L.ticket_groups > kMaxTicketGroups) L.ticket_groups = kDefaultTicketGroups;
   const char* fm = getenv("MBX_FIN_MODE");
-  L.fin_mode = fm ? atoi(fm) : (mode == kModeCount ? kFinPackedCount : kFinWriteThrough);
+  L.fin_mode = fm ? atoi(fm) : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
   if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))
     L.fin_mode = kFinWriteThrough;
-  if (L.fin_mode == kFinPackedCount && mode != kModeCount) L.fin_mode = kFinWriteThrough;
+  if (L.fin_mode == kFinPackedCount && mode == kModeAgg) L.fin_mode = kFinWriteThrough;
   if (L.fin_mode == kFinSeparate) L.ticket = nullptr;
   HIPCHK(launch_scan(L, c->stream));
   if (L.fin_mode == kFinSeparate)

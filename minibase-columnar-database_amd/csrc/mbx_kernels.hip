@@ -334,6 +334,15 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
       Acc r = sh[0];
 #pragma unroll
       for (int w = 1; w < kWaves; ++w) acc_merge(r, sh[w]);
+      if (L.mode == kModeBitmap) {
+        // the segment count for the compaction launch that follows: only a
+        // later launch reads it, so the store is not waited for here
+        Partial p;
+        p.count = r.count;
+        p.nan_seen = r.nan;
+        p.pad_ = 0;
+        store_count_sc1(L.partials + blockIdx.x, p);
+      }
       packed_count_finalize(L.ticket, L.ticket_groups, r.count, r.nan, L.count_out, L.nan_out);
     }
     return;
