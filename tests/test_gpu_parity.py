@@ -639,3 +639,37 @@ def test_c5_full_table_1b_rows(ctx, m):
     t.close()
     del c0, c1, c2, idx
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("groups,tpb,fin", [
+    ("32", "0", None),     # default: 32 group words + the top word
+    ("1", "0", None),      # one flat packed word (~1000 arrivals)
+    ("1", "4", None),      # flat, > 4095 arrivals: falls back to the write-through partials
+    ("64", "4", None),     # 64 groups x ~77 arrivals
+    ("5", "7", None),      # groups that do not divide the grid
+    ("32", "0", "0"),      # write-through partials (MBX_FIN_MODE=0)
+    ("32", "0", "2"),      # separate finalize launch
+])
+def test_count_and_bitset_finalize_forms(ctx, groups, tpb, fin, monkeypatch):
+    """COUNT and BitSet scans end in the packed 64-bit ticket words (count |
+    NaN blocks | arrivals); every grouping, the > 4095-arrival fallback and
+    the other finalize forms give the same count, BitSet and positions
+    (numpy check), and back-to-back launches see the words reset."""
+    monkeypatch.setenv("MBX_TICKET_GROUPS", groups)
+    if tpb != "0":
+        monkeypatch.setenv("MBX_TILES_PER_BLOCK", tpb)
+    if fin is not None:
+        monkeypatch.setenv("MBX_FIN_MODE", fin)
+    n = 5_000_017
+    cols, _ = int_table(n, hi=1000)
+    t = ctx.stage(cols)
+    c0, c1 = cols[0][2], cols[1][2]
+    for lim in (700, 3, 1000):  # a different count each launch: a stale ticket word would show
+        cnf = [[(oracle.LT, ("sym", 1), ("int", lim))], [(oracle.GE, ("sym", 2), ("int", 100))]]
+        mask = (c0 < lim) & (c1 >= 100)
+        plan = ctx.compile(t, cnf)
+        assert ctx.scan_count(plan) == int(mask.sum())
+        bm = ctx.scan_bitmap(plan)
+        assert bm.count == int(mask.sum())
+        assert np.array_equal(bm.download(), _np_words(mask))
+        assert np.array_equal(ctx.select(bm), np.nonzero(mask)[0])
