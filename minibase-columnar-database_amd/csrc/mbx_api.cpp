@@ -741,6 +741,19 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
     const int pol = ri ? atoi(ri) : 1;
     L.ri = pol == 2 || (pol == 1 && mode == kModeBitmap);
   }
+  {
+    // BitSet words staged in LDS per block when the segment fits
+    // (MBX_SINK_LDS=0: stored as produced, A/B tuning); the fast kernel's RI
+    // BitSet form only
+    const char* sl = getenv("MBX_SINK_LDS");
+    // measured: 100 M rows (382 tiles per block) 79.1 -> 77.6 us; 10 M / 12.5 M
+    // rows (<= 48 tiles per block) +0.2 us, so small segments keep the
+    // direct stores (profiles/r01/round_i/sink_lds)
+    L.sink_lds = mode == kModeBitmap && L.ri && v.fast_k + v.fast_ks > 0 && !(sl && sl[0] == '0') &&
+                 tpb >= 128 && tpb * kWordsPerTile * (int64_t)sizeof(uint64_t) <= kSinkLdsMaxBytes;
+    if (sl && sl[0] == '2') L.sink_lds = L.ri && mode == kModeBitmap && v.fast_k + v.fast_ks > 0 &&
+                                         tpb * kWordsPerTile * (int64_t)sizeof(uint64_t) <= kSinkLdsMaxBytes;
+  }
   const char* tg = getenv("MBX_TICKET_GROUPS");
   L.ticket_groups = tg ? atoi(tg) : kDefaultTicketGroups;
   if (L.ticket_groups < 0 || L.ticket_groups > kMaxTicketGroups) L.ticket_groups = kDefaultTicketGroups;

@@ -119,7 +119,13 @@ struct ScanLaunch {
   int32_t diag_terms;         // term i compares slot i, for every term
   int32_t fin_mode;           // FinMode (MBX_FIN_MODE): how the last block sees the partials
   int32_t ri;                 // 1: row-interleaved tile layout (register j of lane l = row 64j + l)
+  int32_t sink_lds;           // 1: BitSet words of the block's full tiles staged in dynamic LDS
+                              //    (tiles_per_block x 32 B) and stored in one burst at the block's end
 };
+
+// dynamic LDS per block for the staged BitSet (4 blocks per CU: <= 128 KB of
+// the CU's 160 KB)
+constexpr int64_t kSinkLdsMaxBytes = 32 * 1024;
 
 // Arrival tickets of the in-launch finalize.  Blocks arrive on the ticket of
 // their group (blockIdx % G, so a group lives on one XCD -- blocks are dealt

@@ -197,7 +197,8 @@ def _np_words(mask):
 @pytest.mark.parametrize("tpb", [0, 4, 63, 64, 65, 200, 1000])
 @pytest.mark.parametrize("ri", ["0", "1"])
 @pytest.mark.parametrize("deleted", [False, True])
-def test_bitset_segments_and_tile_layouts(ctx, tpb, ri, deleted, monkeypatch):
+@pytest.mark.parametrize("sink_lds", ["1", "2"])  # LDS-staged BitSet: default rule / whenever it fits
+def test_bitset_segments_and_tile_layouts(ctx, tpb, ri, deleted, sink_lds, monkeypatch):
     """BitSet output over segment sizes that give each wave 1..250 tiles (the
     RI layout buffers 16 tiles' words per store) and a ragged tail, both tile
     layouts (MBX_SCAN_RI), with and without deleted rows; numpy is the check
@@ -205,6 +206,7 @@ def test_bitset_segments_and_tile_layouts(ctx, tpb, ri, deleted, monkeypatch):
     if tpb:
         monkeypatch.setenv("MBX_TILES_PER_BLOCK", str(tpb))
     monkeypatch.setenv("MBX_SCAN_RI", ri)
+    monkeypatch.setenv("MBX_SINK_LDS", sink_lds)
     n = 2_000_003
     cols, dele = int_table(n, hi=1000, deleted_frac=0.05 if deleted else None)
     t = ctx.stage(cols, dele)
