@@ -17,7 +17,9 @@
  *     R/global/SystemDefs.java:6-9).  Multi-GPU = one process (or one
  *     context) per GPU, rows sharded by range.
  *   - Synchronous calls return with their results on the host.  *_async calls
- *     only enqueue on the context stream; mbx_sync() waits.
+ *     only enqueue on the context stream; mbx_sync() waits and returns
+ *     MBX_E_TYPE if a scan enqueued since the previous mbx_sync reached a
+ *     float compare on a NaN (the exception PredEval would have thrown).
  *   - Positions: a table holds rows [row_offset, row_offset + nrows) of a
  *     Columnarfile in position order (position == row index of a dense file,
  *     R/heap/Heapfile.java:262-289).  row_offset must be a multiple of 64 so
@@ -258,6 +260,12 @@ int mbx_cursor_close(mbx_cursor *c);   /* Iterator.close(), idempotent via free 
  * grid-stride over `grid` blocks instead of segments. */
 int mbx_probe_read(mbx_ctx *ctx, const mbx_table *t, const int32_t *cols, int32_t ncols,
                    int64_t tiles_per_block, int32_t interleave, int64_t grid);
+/* A/B tuning knobs of this context, no reference
+ * counterpart.  mbx_init reads their MBX_* environment defaults once; no
+ * launch reads the environment.  knob: "tiles_per_block", "force_generic",
+ * "scan_hoist", "scan_ri", "sink_lds", "ticket_groups", "fin_mode",
+ * "join_plain", "distinct_lds_probes"; "reset" restores the defaults. */
+int mbx_set_tuning(mbx_ctx *ctx, const char *knob, int64_t value);
 
 #ifdef __cplusplus
 }

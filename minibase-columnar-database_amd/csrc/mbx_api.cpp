@@ -46,9 +46,8 @@ int mbx::fail(int code, const char* fmt, ...) {
 
 // ----------------------------------------------------------------- helpers
 
-static int64_t tiles_per_block_for(int64_t nrows) {
-  const char* e = getenv("MBX_TILES_PER_BLOCK");
-  if (e && atoll(e) > 0) return atoll(e);
+static int64_t tiles_per_block_for(const mbx_ctx* c, int64_t nrows) {
+  if (c->tune.tiles_per_block > 0) return c->tune.tiles_per_block;
   return choose_tiles_per_block(nrows);
 }
 
@@ -56,15 +55,33 @@ static int64_t tiles_per_block_for(int64_t nrows) {
 // output bitmap's segments).  Plans with 16-byte string slots do more work per
 // byte and run best with ~4096 blocks (C5, 125M rows: 483 -> 470 us; 1B rows:
 // 3908 -> 3729 us, profiles/r01/round_e); 4-byte-only plans with ~1024.
-static int64_t scan_tiles_per_block(int64_t nrows, const PlanVariant& v) {
-  const char* e = getenv("MBX_TILES_PER_BLOCK");
-  if (e && atoll(e) > 0) return atoll(e);
+static int64_t scan_tiles_per_block(const mbx_ctx* c, int64_t nrows, const PlanVariant& v) {
+  if (c->tune.tiles_per_block > 0) return c->tune.tiles_per_block;
   if (v.fast_ks > 0) {
     const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
     const int64_t tpb = (ntiles + 4095) / 4096;
     return tpb < 4 ? 4 : tpb;
   }
   return choose_tiles_per_block(nrows);
+}
+
+static int64_t env_knob(const char* name, int64_t dflt) {
+  const char* e = getenv(name);
+  return e && *e ? atoll(e) : dflt;
+}
+
+// the MBX_* A/B knobs, read once per context (mbx_init)
+static void tuning_from_env(MbxTuning& t) {
+  t = MbxTuning();
+  t.tiles_per_block = env_knob("MBX_TILES_PER_BLOCK", -1);
+  t.force_generic = (int32_t)env_knob("MBX_FORCE_GENERIC", 0);
+  t.scan_hoist = (int32_t)env_knob("MBX_SCAN_HOIST", 1);
+  t.scan_ri = (int32_t)env_knob("MBX_SCAN_RI", 1);
+  t.sink_lds = (int32_t)env_knob("MBX_SINK_LDS", 1);
+  t.ticket_groups = (int32_t)env_knob("MBX_TICKET_GROUPS", -1);
+  t.fin_mode = (int32_t)env_knob("MBX_FIN_MODE", -1);
+  t.join_plain = (int32_t)env_knob("MBX_JOIN_PLAIN", 0);
+  t.distinct_lds_probes = (int32_t)env_knob("MBX_DISTINCT_LDS_PROBES", -1);
 }
 
 static int ensure_partials(mbx_ctx* c, int64_t n) {
@@ -124,7 +141,7 @@ int mbx::bitmap_new(mbx_ctx* c, int64_t nbits, mbx_bitmap** out) {
   b->ctx = c;
   b->nbits = nbits;
   b->nwords = words_for(nbits);
-  b->wpb = tiles_per_block_for(nbits) * kWordsPerTile;
+  b->wpb = tiles_per_block_for(c, nbits) * kWordsPerTile;
   b->nseg = b->nwords == 0 ? 1 : (b->nwords + b->wpb - 1) / b->wpb;
   hipError_t e = hipMalloc(&b->words, sizeof(uint64_t) * (size_t)(b->nwords > 0 ? b->nwords : 1));
   if (e == hipSuccess) e = hipMalloc(&b->segs, sizeof(Partial) * (size_t)b->nseg);
@@ -167,13 +184,15 @@ extern "C" int mbx_init(int32_t device, mbx_ctx** out) {
   mbx_ctx* c = new (std::nothrow) mbx_ctx();
   if (!c) return fail(MBX_E_NOMEM, "mbx_init: host allocation");
   c->device = device;
+  tuning_from_env(c->tune);
   int rc = MBX_OK;
   do {
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->dagg, sizeof(AggOut));
     if (e == hipSuccess) e = hipMalloc(&c->dcount, sizeof(int64_t) * 2);
-    if (e == hipSuccess) e = hipMalloc(&c->dnan, sizeof(int32_t) * 2);
+    if (e == hipSuccess) e = hipMalloc(&c->dnan, sizeof(int32_t) * 4);
+    if (e == hipSuccess) e = hipMemset(c->dnan, 0, sizeof(int32_t) * 4);
     if (e == hipSuccess) e = hipMalloc(&c->ticket, sizeof(uint32_t) * kTicketWords);
     if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(uint32_t) * kTicketWords);
     if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 256, hipHostMallocDefault);
@@ -207,9 +226,44 @@ extern "C" int mbx_free(mbx_ctx* c) {
   return MBX_OK;
 }
 
+// Waits for the context stream and reports what the *_async scans enqueued
+// since the last mbx_sync raised: a NaN reached by a float compare sets the
+// sticky word dnan[1] (the kernels' last block), read and cleared here.
 extern "C" int mbx_sync(mbx_ctx* c) {
   NOTNULL(c);
+  HIPCHK(hipSetDevice(c->device));
+  int32_t* h = (int32_t*)c->pinned + 24;
+  HIPCHK(hipMemcpyAsync(h, c->dnan + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (*h) {
+    HIPCHK(hipMemsetAsync(c->dnan + 1, 0, sizeof(int32_t), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return fail(MBX_E_TYPE,
+                "NaN in a float comparison in an asynchronous scan (TupleUtils falls through to the string compare "
+                "and raises)");
+  }
+  return MBX_OK;
+}
+
+extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
+  NOTNULL(c);
+  NOTNULL(knob);
+  MbxTuning& t = c->tune;
+  if (!strcmp(knob, "reset")) {
+    tuning_from_env(t);
+    return MBX_OK;
+  }
+  const int32_t v = (int32_t)value;
+  if (!strcmp(knob, "tiles_per_block")) t.tiles_per_block = value;
+  else if (!strcmp(knob, "force_generic")) t.force_generic = v;
+  else if (!strcmp(knob, "scan_hoist")) t.scan_hoist = v;
+  else if (!strcmp(knob, "scan_ri")) t.scan_ri = v;
+  else if (!strcmp(knob, "sink_lds")) t.sink_lds = v;
+  else if (!strcmp(knob, "ticket_groups")) t.ticket_groups = v;
+  else if (!strcmp(knob, "fin_mode")) t.fin_mode = v;
+  else if (!strcmp(knob, "join_plain")) t.join_plain = v;
+  else if (!strcmp(knob, "distinct_lds_probes")) t.distinct_lds_probes = v;
+  else return fail(MBX_E_INVALID, "mbx_set_tuning: unknown knob `%s`", knob);
   return MBX_OK;
 }
 
@@ -230,7 +284,7 @@ extern "C" int mbx_probe_read(mbx_ctx* c, const mbx_table* t, const int32_t* col
   A.ncols = ncols;
   A.interleave = interleave ? 1 : 0;
   A.nrows = t->nrows;
-  A.tiles_per_block = tiles_per_block > 0 ? tiles_per_block : tiles_per_block_for(t->nrows);
+  A.tiles_per_block = tiles_per_block > 0 ? tiles_per_block : tiles_per_block_for(c, t->nrows);
   const int64_t ntiles = t->nrows / kTileRows;
   A.grid = interleave ? (grid > 0 ? grid : 1024) : (ntiles + A.tiles_per_block - 1) / A.tiles_per_block;
   if (A.grid < 1) A.grid = 1;
@@ -497,6 +551,8 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
   for (int32_t ci = 0; ci < nconj; ci++) {
     const int32_t k0 = cnf->conj_offsets[ci], k1 = cnf->conj_offsets[ci + 1];
     if (k0 < 0 || k1 < k0) return fail(MBX_E_INVALID, "plan: conj_offsets not ascending at %d", ci);
+    // always_true: a literal-vs-literal term that holds ends the conjunct's OR
+    // list (PredEval.java:164-166); later terms are never evaluated
     bool always_true = false;
     const int32_t first_term = nterms;
     for (int32_t k = k0; k < k1; k++) {
@@ -528,22 +584,41 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
       if (t2 != ctype)
         return fail(MBX_E_TYPE, "plan: term %d compares AttrType %d with %d (reference misreads the field)", k,
                     ctype, t2);
+      if (always_true) continue;  // never reached; still type-checked above
+      const bool real = ctype == MBX_ATTR_REAL;
+      const bool never = e.op == MBX_OP_NOP || e.op == MBX_OP_RANGE;  // no case in the op switch: false
       const mbx_operand* lit = o2.type == MBX_ATTR_SYMBOL ? (o1.type == MBX_ATTR_SYMBOL ? nullptr : &o1) : &o2;
-      if (lit && lit->type == MBX_ATTR_REAL && std::isnan(lit->real))
-        return fail(MBX_E_TYPE, "plan: NaN literal (TupleUtils falls through to the string compare and raises)");
-      if (e.op == MBX_OP_NOP || e.op == MBX_OP_RANGE) continue;  // never true
-      if (o1.type != MBX_ATTR_SYMBOL && o2.type != MBX_ATTR_SYMBOL) {
-        // two literals share PredEval's `value` tuple: operand 2 vs itself
-        if (op_on(e.op, 0)) always_true = true;
-        continue;
-      }
-      if (nterms >= kMaxTerms) return fail(MBX_E_UNSUPPORTED, "plan: more than %d terms", kMaxTerms);
+      // TupleUtils compares first and maps the operator after
+      // (PredEval.java:131-162): a float compare with a NaN operand raises
+      // whenever it is reached, whatever the operator.
+      const bool nan_lit = lit && real && std::isnan(lit->real);
       KTerm kt;
       memset(&kt, 0, sizeof(kt));
-      kt.kind = col_kind(ctype);
       kt.conj_bit = 1u << ci;
       kt.rhs = -1;
-      int32_t op = cmp_op_of(e.op);
+      if (o1.type != MBX_ATTR_SYMBOL && o2.type != MBX_ATTR_SYMBOL) {
+        // two literals share PredEval's `value` tuple: operand 2 vs itself
+        if (real && std::isnan(o2.real)) {
+          // raises wherever reached: a never-true float term that reads no
+          // column (its slot is any one the plan streams anyway)
+          const int s0 = p->slot_col.empty() ? slot_for(p, 0) : 0;
+          if (s0 < 0) return fail(MBX_E_UNSUPPORTED, "plan: more than %d distinct columns", kMaxCols);
+          if (nterms >= kMaxTerms) return fail(MBX_E_UNSUPPORTED, "plan: more than %d terms", kMaxTerms);
+          kt.kind = kReal;
+          kt.op = kNever;
+          kt.lhs = s0;
+          kt.nan_lit = 1;
+          p->host.has_real = 1;
+          p->host.terms[nterms++] = kt;
+        } else if (!never && op_on(e.op, 0)) {
+          always_true = true;
+        }
+        continue;
+      }
+      if (never && !real) continue;  // never true and cannot raise: dropped
+      if (nterms >= kMaxTerms) return fail(MBX_E_UNSUPPORTED, "plan: more than %d terms", kMaxTerms);
+      kt.kind = col_kind(ctype);
+      int32_t op = never ? kNever : cmp_op_of(e.op);
       const mbx_operand* coln;
       if (o1.type == MBX_ATTR_SYMBOL) {
         coln = &o1;
@@ -561,24 +636,30 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
       if (s1 < 0) return fail(MBX_E_UNSUPPORTED, "plan: more than %d distinct columns", kMaxCols);
       kt.lhs = s1;
       kt.op = op;
+      kt.nan_lit = nan_lit ? 1 : 0;
       if (kt.rhs < 0) {
         if (ctype == MBX_ATTR_INTEGER) kt.ilit = lit->integer;
-        else if (ctype == MBX_ATTR_REAL) kt.flit = lit->real;
+        else if (real) kt.flit = lit->real;
         else {
           int rc = add_pool_string(p, *lit, pool_used, kt);
           if (rc) return rc;
         }
       }
       if (ctype == MBX_ATTR_STRING && kt.rhs < 0 && kt.swords > 4) p->str_lit_fits16 = false;
-      if (ctype == MBX_ATTR_REAL) p->host.has_real = 1;
+      if (real) p->host.has_real = 1;
       p->host.terms[nterms++] = kt;
     }
     if (always_true) {
-      nterms = first_term;  // the conjunct holds for every row: drop it
+      // the conjunct holds for every row: it is not required, but the float
+      // compares before the folding term still run for their NaN reach
+      bool can_raise = false;
+      for (int32_t i = first_term; i < nterms; i++) can_raise = can_raise || p->host.terms[i].kind == kReal;
+      if (!can_raise) nterms = first_term;
       continue;
     }
     all |= 1u << ci;  // an empty conjunct stays required and is never satisfied
   }
+  for (int32_t i = 0; i < nterms; i++) p->host.terms[i].req_below = all & (p->host.terms[i].conj_bit - 1u);
   p->host.nterms = nterms;
   p->host.all_conj = all;
   return MBX_OK;
@@ -617,9 +698,7 @@ static int plan_variant(mbx_plan* p, int32_t agg_col, PlanVariant** out) {
   // Fast kernel eligibility: every term `column OP literal`, 16-byte aligned
   // columns, <= 4 four-byte slots and <= 2 char(13..16) slots whose literals
   // fit 16 bytes.  Slots are renumbered 4-byte first, strings after.
-  bool fast = p->all_literal && p->str_lit_fits16 && p->t->aligned16;
-  const char* force = getenv("MBX_FORCE_GENERIC");
-  if (force && force[0] == '1') fast = false;
+  bool fast = p->all_literal && p->str_lit_fits16 && p->t->aligned16 && !p->ctx->tune.force_generic;
   std::vector<int> four, wide;
   for (size_t i = 0; i < slots.size(); i++) {
     const TCol& tc = p->t->cols[slots[i]];
@@ -725,40 +804,21 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.count_out = count_out;
   L.agg_out = agg_out;
   L.nan_out = nan_out;
-  const char* var = getenv("MBX_SCAN_VARIANT");
-  L.variant = var ? atoi(var) : 0;
+  const MbxTuning& tu = c->tune;
   L.nterms_host = p->host.nterms;
-  {
-    const char* mf = getenv("MBX_SCAN_HOIST");  // 0: terms read from the plan per tile (A/B tuning)
-    L.hoist_terms = p->host.nterms >= 1 && p->host.nterms <= kHoistTerms && !(mf && mf[0] == '0');
-    L.diag_terms = L.hoist_terms && v.fast_ks == 0 && p->host.nterms == v.fast_k;
-    for (int i = 0; i < p->host.nterms && L.diag_terms; ++i) L.diag_terms = p->host.terms[i].lhs == i;
-  }
-  {
-    // tile layout: row-interleaved for BitSet output (the ballots are the
-    // words); MBX_SCAN_RI=0 never, 1 BitSet output only, 2 always (A/B tuning)
-    const char* ri = getenv("MBX_SCAN_RI");
-    const int pol = ri ? atoi(ri) : 1;
-    L.ri = pol == 2 || (pol == 1 && mode == kModeBitmap);
-  }
-  {
-    // BitSet words staged in LDS per block when the segment fits
-    // (MBX_SINK_LDS=0: stored as produced, A/B tuning); the fast kernel's RI
-    // BitSet form only
-    const char* sl = getenv("MBX_SINK_LDS");
-    // measured: 100 M rows (382 tiles per block) 79.1 -> 77.6 us; 10 M / 12.5 M
-    // rows (<= 48 tiles per block) +0.2 us, so small segments keep the
-    // direct stores (profiles/r01/round_i/sink_lds)
-    L.sink_lds = mode == kModeBitmap && L.ri && v.fast_k + v.fast_ks > 0 && !(sl && sl[0] == '0') &&
-                 tpb >= 128 && tpb * kWordsPerTile * (int64_t)sizeof(uint64_t) <= kSinkLdsMaxBytes;
-    if (sl && sl[0] == '2') L.sink_lds = L.ri && mode == kModeBitmap && v.fast_k + v.fast_ks > 0 &&
-                                         tpb * kWordsPerTile * (int64_t)sizeof(uint64_t) <= kSinkLdsMaxBytes;
-  }
-  const char* tg = getenv("MBX_TICKET_GROUPS");
-  L.ticket_groups = tg ? atoi(tg) : kDefaultTicketGroups;
-  if (L.ticket_groups < 0 || L.ticket_groups > kMaxTicketGroups) L.ticket_groups = kDefaultTicketGroups;
-  const char* fm = getenv("MBX_FIN_MODE");
-  L.fin_mode = fm ? atoi(fm) : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
+  L.hoist_terms = p->host.nterms >= 1 && p->host.nterms <= kHoistTerms && tu.scan_hoist != 0;
+  // tile layout: row-interleaved for BitSet output (the ballots are the words)
+  L.ri = tu.scan_ri == 2 || (tu.scan_ri == 1 && mode == kModeBitmap);
+  // BitSet words staged in LDS per block when the segment fits; the fast
+  // kernel's RI BitSet form only.  Measured: 100 M rows (382 tiles per block)
+  // 79.1 -> 77.6 us; 10 M / 12.5 M rows (<= 48 tiles per block) +0.2 us, so
+  // small segments keep the direct stores (profiles/r01/round_i/sink_lds)
+  const bool sink_fits = mode == kModeBitmap && L.ri && v.fast_k + v.fast_ks > 0 &&
+                         tpb * kWordsPerTile * (int64_t)sizeof(uint64_t) <= kSinkLdsMaxBytes;
+  L.sink_lds = sink_fits && (tu.sink_lds == 2 || (tu.sink_lds == 1 && tpb >= 128));
+  L.ticket_groups = tu.ticket_groups >= 0 ? tu.ticket_groups : kDefaultTicketGroups;
+  if (L.ticket_groups > kMaxTicketGroups) L.ticket_groups = kDefaultTicketGroups;
+  L.fin_mode = tu.fin_mode >= 0 ? tu.fin_mode : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
   if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))
     L.fin_mode = kFinWriteThrough;
   if (L.fin_mode == kFinPackedCount && mode == kModeAgg) L.fin_mode = kFinWriteThrough;
@@ -773,11 +833,16 @@ static int scan_to_count(mbx_ctx* c, mbx_plan* p, int64_t* dev_count, int32_t* d
   PlanVariant* v = nullptr;
   int rc = plan_variant(p, -1, &v);
   if (rc) return rc;
-  const int64_t tpb = scan_tiles_per_block(p->t->nrows, *v);
+  const int64_t tpb = scan_tiles_per_block(c, p->t->nrows, *v);
   const int64_t nb = grid_blocks(p->t->nrows, tpb);
   if ((rc = ensure_partials(c, nb))) return rc;
   return enqueue_scan(c, p, *v, kModeCount, nullptr, c->partials, tpb, dev_count, nullptr, dev_nan);
 }
+
+// NaN words: the *_async entry points report through dnan[0..1] ([1] sticky
+// until mbx_sync); the synchronous ones read their own flag, dnan[2], so a
+// NaN they already raised is not reported again by mbx_sync
+static int32_t* nan_sync(mbx_ctx* c) { return c->dnan + 2; }
 
 static int check_nan(mbx_ctx* c) {
   const int32_t* h = (const int32_t*)c->pinned;
@@ -792,10 +857,10 @@ extern "C" int mbx_scan_count(mbx_ctx* c, const mbx_plan* pc, int64_t* count) {
   mbx_plan* p = const_cast<mbx_plan*>(pc);
   int rc = set_device(c);
   if (rc) return rc;
-  if ((rc = scan_to_count(c, p, c->dcount, c->dnan))) return rc;
+  if ((rc = scan_to_count(c, p, c->dcount, nan_sync(c)))) return rc;
   int64_t* h = (int64_t*)c->pinned;
   HIPCHK(hipMemcpyAsync(h, c->dcount, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, c->dnan, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, nan_sync(c), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   *count = h[0];
   return check_nan(c);
@@ -808,7 +873,7 @@ extern "C" int mbx_scan_count_async(mbx_ctx* c, const mbx_plan* pc, int64_t* dev
   return scan_to_count(c, const_cast<mbx_plan*>(pc), dev_count, c->dnan);
 }
 
-static int scan_bitmap_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b) {
+static int scan_bitmap_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int32_t* dev_nan) {
   if (b->nbits != p->t->nrows)
     return fail(MBX_E_INVALID, "scan_bitmap: bitmap has %lld bits, table %lld rows", (long long)b->nbits,
                 (long long)p->t->nrows);
@@ -817,14 +882,14 @@ static int scan_bitmap_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b) {
   if (rc) return rc;
   const int64_t tpb = b->wpb / kWordsPerTile;
   if (grid_blocks(p->t->nrows, tpb) != b->nseg) return fail(MBX_E_INVALID, "scan_bitmap: segment mismatch");
-  return enqueue_scan(c, p, *v, kModeBitmap, b->words, b->segs, tpb, c->dcount, nullptr, c->dnan);
+  return enqueue_scan(c, p, *v, kModeBitmap, b->words, b->segs, tpb, c->dcount, nullptr, dev_nan);
 }
 
 // read back the count + NaN flag the last scan's final block wrote
 static int scan_result_sync(mbx_ctx* c, int64_t* count) {
   int64_t* h = (int64_t*)c->pinned;
   HIPCHK(hipMemcpyAsync(h, c->dcount, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, c->dnan, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, nan_sync(c), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   *count = h[0];
   return MBX_OK;
@@ -835,7 +900,7 @@ extern "C" int mbx_scan_bitmap_async(mbx_ctx* c, const mbx_plan* pc, mbx_bitmap*
   NOTNULL(pc);
   NOTNULL(out);
   out->count = -1;
-  return scan_bitmap_into(c, const_cast<mbx_plan*>(pc), out);
+  return scan_bitmap_into(c, const_cast<mbx_plan*>(pc), out, c->dnan);
 }
 
 static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel, const int32_t* proj,
@@ -848,8 +913,9 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
 // writing its positions from LDS) measured the same -- C2 10M rows 22.9 vs
 // 24.0 us, 100M rows 102 vs 101.5 us: the tail's dependent global round trips
 // cost what the launch boundary costs -- and was not kept.
-static int scan_select_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int64_t* dev_ids, int64_t* dev_count) {
-  int rc = scan_bitmap_into(c, p, b);
+static int scan_select_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int64_t* dev_ids, int64_t* dev_count,
+                            int32_t* dev_nan) {
+  int rc = scan_bitmap_into(c, p, b, dev_nan);
   if (rc) return rc;
   return materialize_dev(c, p->t, b, nullptr, 0, p->t->row_offset, dev_ids, nullptr, dev_count);
 }
@@ -864,7 +930,7 @@ extern "C" int mbx_scan_select_async(mbx_ctx* c, const mbx_plan* pc, mbx_bitmap*
   int rc = set_device(c);
   if (rc) return rc;
   out->count = -1;
-  return scan_select_into(c, const_cast<mbx_plan*>(pc), out, dev_ids, dev_count);
+  return scan_select_into(c, const_cast<mbx_plan*>(pc), out, dev_ids, dev_count, c->dnan);
 }
 
 extern "C" int mbx_scan_select(mbx_ctx* c, const mbx_plan* pc, int64_t* host_ids, int64_t cap, int64_t* n) {
@@ -886,7 +952,7 @@ extern "C" int mbx_scan_select(mbx_ctx* c, const mbx_plan* pc, int64_t* host_ids
   mbx_bitmap* b = nullptr;
   if ((rc = bitmap_new(c, nrows, &b))) return rc;
   int64_t count = 0;
-  if (!(rc = scan_select_into(c, p, b, c->ids_scratch, c->dcount)) && !(rc = scan_result_sync(c, &count)))
+  if (!(rc = scan_select_into(c, p, b, c->ids_scratch, c->dcount, nan_sync(c))) && !(rc = scan_result_sync(c, &count)))
     rc = check_nan(c);
   if (!rc && count > cap)
     rc = fail(MBX_E_INVALID, "scan_select: %lld positions, capacity %lld", (long long)count, (long long)cap);
@@ -906,10 +972,10 @@ extern "C" int mbx_scan_select(mbx_ctx* c, const mbx_plan* pc, int64_t* host_ids
 }
 
 static int bitmap_count_sync(mbx_ctx* c, mbx_bitmap* b, bool with_nan) {
-  HIPCHK(launch_finalize(b->segs, b->nseg, kInt, nullptr, c->dcount, c->dnan, c->stream));
+  HIPCHK(launch_finalize(b->segs, b->nseg, kInt, nullptr, c->dcount, nan_sync(c), c->stream));
   int64_t* h = (int64_t*)c->pinned;
   HIPCHK(hipMemcpyAsync(h, c->dcount, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, c->dnan, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, nan_sync(c), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   b->count = h[0];
   return with_nan ? check_nan(c) : MBX_OK;
@@ -930,7 +996,7 @@ extern "C" int mbx_scan_bitmap(mbx_ctx* c, const mbx_plan* pc, mbx_bitmap** out,
   if (rc) return rc;
   mbx_bitmap* b = nullptr;
   if ((rc = bitmap_new(c, p->t->nrows, &b))) return rc;
-  if (!(rc = scan_bitmap_into(c, p, b)) && !(rc = scan_result_sync(c, &b->count))) rc = check_nan(c);
+  if (!(rc = scan_bitmap_into(c, p, b, nan_sync(c))) && !(rc = scan_result_sync(c, &b->count))) rc = check_nan(c);
   if (rc) {
     mbx_bitmap_free(b);
     return rc;
@@ -946,7 +1012,7 @@ static int scan_agg(mbx_ctx* c, mbx_plan* p, int32_t agg_col, AggOut* dev_out, i
   PlanVariant* v = nullptr;
   int rc = plan_variant(p, agg_col, &v);
   if (rc) return rc;
-  const int64_t tpb = scan_tiles_per_block(p->t->nrows, *v);
+  const int64_t tpb = scan_tiles_per_block(c, p->t->nrows, *v);
   const int64_t nb = grid_blocks(p->t->nrows, tpb);
   if ((rc = ensure_partials(c, nb))) return rc;
   return enqueue_scan(c, p, *v, kModeAgg, nullptr, c->partials, tpb, nullptr, dev_out, dev_nan);
@@ -959,9 +1025,9 @@ extern "C" int mbx_scan_aggregate(mbx_ctx* c, const mbx_plan* pc, int32_t agg_co
   static_assert(sizeof(mbx_agg) == sizeof(AggOut), "mbx_agg layout");
   int rc = set_device(c);
   if (rc) return rc;
-  if ((rc = scan_agg(c, const_cast<mbx_plan*>(pc), agg_col, c->dagg, c->dnan))) return rc;
+  if ((rc = scan_agg(c, const_cast<mbx_plan*>(pc), agg_col, c->dagg, nan_sync(c)))) return rc;
   HIPCHK(hipMemcpyAsync(c->pinned, c->dagg, sizeof(AggOut), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 16, c->dnan, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 16, nan_sync(c), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   memcpy(out, c->pinned, sizeof(mbx_agg));
   if (((const int32_t*)c->pinned)[16])

@@ -1144,8 +1144,8 @@ extern "C" int mbx_db_create_bitmap_index(mbx_ctx* c, mbx_db* db, const char* na
     A.minpos = minpos;
     A.cap = cap;
     A.overflow = dflag;
-    const char* lp = getenv("MBX_DISTINCT_LDS_PROBES");  // test knob: 0 sends every row to the global table
-    A.lds_probes = lp ? atoi(lp) : kLdsProbes;
+    // test knob (mbx_set_tuning "distinct_lds_probes"): 0 sends every row to the global table
+    A.lds_probes = c->tune.distinct_lds_probes >= 0 ? c->tune.distinct_lds_probes : kLdsProbes;
     e = launch_distinct(A, s);
   }
   std::vector<unsigned long long> hmin((size_t)cap);

@@ -34,7 +34,9 @@ enum ColKind : int32_t { kInt = 0, kReal = 1, kStr = 2 };
 
 // normalized comparison: the kernel evaluates `lhs_col OP rhs` where rhs is a
 // literal or another column; literal-on-left terms are flipped on the host.
-enum CmpOp : int32_t { kLT = 0, kLE = 1, kGT = 2, kGE = 3, kEQ = 4, kNE = 5 };
+// kNever: aopNOP / opRANGE, never true (PredEval.java:137-162 has no case for
+// them) -- kept as a term only where reaching it can raise (a float compare).
+enum CmpOp : int32_t { kLT = 0, kLE = 1, kGT = 2, kGE = 3, kEQ = 4, kNE = 5, kNever = 6 };
 
 struct KCol {
   const void* base;
@@ -52,6 +54,13 @@ struct KTerm {
   float flit;
   int32_t soff;      // string literal: word offset in the pool
   int32_t swords;    // string literal: words
+  // PredEval's evaluation order (R/iterator/PredEval.java:164-175): this term
+  // is evaluated for a row only if every required conjunct before it held
+  // ((cb & req_below) == req_below) and no earlier term of its own conjunct
+  // held (!(cb & conj_bit)).  A float compare reached with a NaN operand
+  // raises (TupleUtils.java:61-69 falls through to the string branch).
+  uint32_t req_below;  // all_conj & (conj_bit - 1)
+  int32_t nan_lit;     // the literal is NaN (or a literal-vs-literal NaN term): raises whenever reached
 };
 
 // The compiled predicate (PredEval over one CNF) + optional aggregate column.
@@ -113,10 +122,8 @@ struct ScanLaunch {
   int64_t* count_out;         // device or null
   AggOut* agg_out;            // device or null
   int32_t* nan_out;           // device or null
-  int32_t variant;            // 0: default kernel; >0: tuning variant (MBX_SCAN_VARIANT)
   int32_t nterms_host;        // the plan's term count, for launch-time kernel choice
   int32_t hoist_terms;        // 1..kHoistTerms literal terms: hoisted into registers
-  int32_t diag_terms;         // term i compares slot i, for every term
   int32_t fin_mode;           // FinMode (MBX_FIN_MODE): how the last block sees the partials
   int32_t ri;                 // 1: row-interleaved tile layout (register j of lane l = row 64j + l)
   int32_t sink_lds;           // 1: BitSet words of the block's full tiles staged in dynamic LDS
@@ -213,7 +220,7 @@ struct JoinTerm {
   const void* icol;    // inner column
   int32_t ostride_w, istride_w;
   uint32_t conj_bit;
-  int32_t pad_;
+  uint32_t req_below;  // all_conj & (conj_bit - 1): PredEval's reach rule (KTerm.req_below)
 };
 
 struct JoinArgs {
@@ -231,6 +238,8 @@ struct JoinArgs {
   int64_t words_per_row;
   uint64_t* out;                // nrows * words_per_row words
   int32_t* nan;
+  int32_t plain;                // 1: k_join_matrix even where the fast form applies (A/B)
+  int32_t pad2_;
 };
 
 struct JoinDecode {

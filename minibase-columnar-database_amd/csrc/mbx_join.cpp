@@ -141,7 +141,9 @@ extern "C" int mbx_join(mbx_ctx* c, const mbx_table* outer, const mbx_bitmap* ou
       T.conj_bit = 1u << k;
     }
   }
+  for (int32_t t = 0; t < nterms; ++t) A.terms[t].req_below = A.all_conj & (A.terms[t].conj_bit - 1u);
   A.nterms = nterms;
+  A.plain = c->tune.join_plain;
   int rc = set_device(c);
   if (rc) return rc;
   hipStream_t s = c->stream;

@@ -59,7 +59,9 @@ __device__ __forceinline__ uint32_t eval_pair(const JoinArgs& A, int64_t orow, i
       c = a < b ? -1 : (a > b ? 1 : 0);
     } else {
       const float a = ((const float*)T.ocol)[orow], b = ((const float*)T.icol)[irow];
-      nan |= (a != a) || (b != b);
+      // raises only where PredEval evaluates this compare (R/iterator/PredEval.java:164-175)
+      const bool reach = ((cb & T.req_below) == T.req_below) && !(cb & T.conj_bit);
+      nan |= reach && ((a != a) || (b != b));
       c = a < b ? -1 : (a > b ? 1 : 0);
     }
     cb |= jop(T.op, c) ? T.conj_bit : 0u;
@@ -121,6 +123,7 @@ struct FastJoin {
   int32_t is_real[kFastJoinTerms];
   uint32_t mask[kFastJoinTerms];   // bit0: x<y, bit1: x==y, bit2: x>y
   uint32_t bit[kFastJoinTerms];
+  uint32_t below[kFastJoinTerms];  // JoinTerm.req_below
 };
 
 __device__ __forceinline__ void lane_values(const JoinArgs& A, const FastJoin& F, int64_t pos, int32_t* lv) {
@@ -193,7 +196,8 @@ __global__ __launch_bounds__(kBlock) void k_join_matrix_fast(JoinArgs A, FastJoi
               const float xf = __int_as_float(lv[t]), yf = __int_as_float(y);
               lt = xf < yf;
               gt = xf > yf;
-              nan |= (lane_pos >= 0) && ((xf != xf) || (yf != yf));
+              const bool reach = ((cb & F.below[t]) == F.below[t]) && !(cb & F.bit[t]);
+              nan |= (lane_pos >= 0) && reach && ((xf != xf) || (yf != yf));
             } else {
               lt = lv[t] < y;
               gt = lv[t] > y;
@@ -255,7 +259,7 @@ static int64_t grid_for(int64_t work, int64_t per_block, int64_t cap) {
 
 hipError_t launch_join_matrix(const JoinArgs& A, hipStream_t s) {
   if (A.nrows <= 0 || A.words_per_row <= 0) return hipSuccess;
-  bool fast = A.nterms <= kFastJoinTerms && !getenv("MBX_JOIN_PLAIN");
+  bool fast = A.nterms <= kFastJoinTerms && !A.plain;
   uint32_t covered = 0;  // an empty conjunct is never true: leave it to the plain kernel
   for (int t = 0; t < A.nterms; ++t) {
     fast = fast && A.terms[t].kind != kStr;
@@ -286,6 +290,7 @@ hipError_t launch_join_matrix(const JoinArgs& A, hipStream_t s) {
       if (A.mode == 0) m = (m & 2u) | ((m & 1u) << 2) | ((m & 4u) >> 2);
       F.mask[t] = m;
       F.bit[t] = T.conj_bit;
+      F.below[t] = T.req_below;
     }
     const int64_t nchunks = (A.nrows + 63) / 64;
     const int64_t want = std::max<int64_t>(1, 8192 / gy);

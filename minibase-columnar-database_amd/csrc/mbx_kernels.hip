@@ -35,7 +35,8 @@ __device__ __forceinline__ bool cmp1(int op, T a, T b) {
     case kGT: return a > b;
     case kGE: return a >= b;
     case kEQ: return a == b;
-    default: return a != b;
+    case kNE: return a != b;
+    default: return false;  // kNever
   }
 }
 
@@ -63,9 +64,13 @@ __device__ __forceinline__ void cmp4(int op, const T (&a)[4], T b, bool (&r)[4])
 #pragma unroll
       for (int j = 0; j < 4; ++j) r[j] = a[j] == b;
       break;
-    default:
+    case kNE:
 #pragma unroll
       for (int j = 0; j < 4; ++j) r[j] = a[j] != b;
+      break;
+    default:  // kNever
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = false;
       break;
   }
 }
@@ -231,7 +236,10 @@ __device__ __forceinline__ void finalize_block(const Partial* parts, int64_t n, 
       *out = o;
     }
     if (count_out) *count_out = r.count;
-    if (nan_flag) *nan_flag = r.nan;
+    if (nan_flag) {  // [0] this launch, [1] sticky until mbx_sync reads it
+      nan_flag[0] = r.nan;
+      if (r.nan) nan_flag[1] = 1;
+    }
   }
 }
 
@@ -300,7 +308,11 @@ __device__ __forceinline__ void packed_count_finalize(uint32_t* ticket, int grou
     return;
   }
   if (count_out) *count_out = (int64_t)(sum >> (kPackArrBits + kPackNanBits));
-  if (nan_out) *nan_out = ((sum >> kPackArrBits) & kPackNanMask) ? 1 : 0;
+  if (nan_out) {  // [0] this launch, [1] sticky until mbx_sync reads it
+    const int32_t nan_any = ((sum >> kPackArrBits) & kPackNanMask) ? 1 : 0;
+    nan_out[0] = nan_any;
+    if (nan_any) nan_out[1] = 1;
+  }
 }
 
 // Block-wide fixed-order reduction of per-thread accumulators into this
@@ -498,7 +510,11 @@ __device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const u
 // the tile instead of row 4l + j, so the wave ballot of row group j *is*
 // BitSet word j of the tile -- no cross-lane packing for BitSet output, the
 // deleted words apply as they are, string compares need no re-layout.
-template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool DG = false, bool RI = false>
+// NaN: a row raises only where PredEval would evaluate the float compare --
+// the row is live (TupleScan skips deleted rows, R/columnar/TupleScan.java:80-87),
+// every required conjunct before the term held and no earlier term of its
+// own conjunct did (R/iterator/PredEval.java:164-175); KTerm.req_below.
+template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool RI = false>
 __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, KS>& D,
                                           int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
                                           Acc& acc, uint64_t& wave_count, const KTerm* th = nullptr,
@@ -508,6 +524,7 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
   const int64_t row0 = t * kTileRows + lane * (RI ? 1 : 4);
   constexpr int kRowStep = RI ? 64 : 1;  // row of register j = row0 + j * kRowStep
   uint32_t cb[4] = {0u, 0u, 0u, 0u};
+  bool nanr[4] = {false, false, false, false};  // reached a float compare on a NaN
 #pragma unroll
   for (int ti = 0; ti < (TQ > 0 ? TQ : nterms); ++ti) {
     if (TQ > 0 && ti > 0 && ti >= nterms) break;  // TQ > 0 implies nterms >= 1
@@ -531,37 +548,33 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
 #pragma unroll
         for (int j = 0; j < 4; ++j) r[j] = rs[j];
       } else {
-      const uint64_t w0 = __ballot(rs[0]), w1 = __ballot(rs[1]), w2 = __ballot(rs[2]), w3 = __ballot(rs[3]);
-      const int q = lane >> 4;
-      const uint64_t w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
-      const uint32_t nib = (uint32_t)(w >> ((lane & 15) * 4));
+        const uint64_t w0 = __ballot(rs[0]), w1 = __ballot(rs[1]), w2 = __ballot(rs[2]), w3 = __ballot(rs[3]);
+        const int q = lane >> 4;
+        const uint64_t w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
+        const uint32_t nib = (uint32_t)(w >> ((lane & 15) * 4));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) r[j] = (nib >> j) & 1u;
+        for (int j = 0; j < 4; ++j) r[j] = (nib >> j) & 1u;
       }
     } else {
       int32_t a[4];
-      if (DG) {  // term ti reads slot ti (host-checked): a compile-time register choice
-        constexpr int kLast = K > 0 ? K - 1 : 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = D.v[ti < kLast ? ti : kLast][j];
-      } else {
+      for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
+      for (int s = 1; s < K; ++s)
+        if (lhs == s) {
 #pragma unroll
-        for (int s = 1; s < K; ++s)
-          if (lhs == s) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
-          }
-      }
+          for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
+        }
       if (T.kind == kInt) {
         cmp4<int32_t>(T.op, a, T.ilit, r);
       } else {
         float f[4];
+        const uint32_t below = T.req_below, own = T.conj_bit;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           f[j] = __int_as_float(a[j]);
-          acc.nan |= (f[j] != f[j]) && (row0 + j * kRowStep < nrows);
+          const bool reach = ((cb[j] & below) == below) && !(cb[j] & own);
+          nanr[j] = nanr[j] || (reach && (T.nan_lit || f[j] != f[j]));
         }
         cmp4<float>(T.op, f, T.flit, r);
       }
@@ -571,21 +584,29 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
     for (int j = 0; j < 4; ++j) cb[j] |= r[j] ? bit : 0u;
   }
 
-  bool p[4];
+  bool live[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) p[j] = (cb[j] == all) && (row0 + j * kRowStep < nrows);
+  for (int j = 0; j < 4; ++j) live[j] = row0 + j * kRowStep < nrows;
   const int64_t word = t * kWordsPerTile + (RI ? 0 : (lane >> 4));
   if (DEL && RI) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint64_t dw = word + j < nwords ? L.deleted[word + j] : 0ull;  // uniform: one scalar load
-      p[j] = p[j] && !((dw >> lane) & 1ull);
+      live[j] = live[j] && !((dw >> lane) & 1ull);
     }
   } else if (DEL) {
     const uint64_t dw = word < nwords ? L.deleted[word] : 0ull;
     const uint32_t dn = (uint32_t)(dw >> ((lane & 15) * 4)) & 0xFu;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) p[j] = p[j] && !((dn >> j) & 1u);
+    for (int j = 0; j < 4; ++j) live[j] = live[j] && !((dn >> j) & 1u);
+  }
+  bool p[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    // a conjunct folded to `true` on the host may keep terms for their NaN
+    // reach, so its bit can be set without being required
+    p[j] = ((cb[j] & all) == all) && live[j];
+    acc.nan |= nanr[j] && live[j];
   }
   if (MODE == kModeBitmap && RI) {
     const uint64_t w0 = __ballot(p[0]), w1 = __ballot(p[1]), w2 = __ballot(p[2]), w3 = __ballot(p[3]);
@@ -629,141 +650,6 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
         acc.isum += p[j] ? (int64_t)g[j] : 0;
         acc.imin = p[j] && g[j] < acc.imin ? g[j] : acc.imin;
         acc.imax = p[j] && g[j] > acc.imax ? g[j] : acc.imax;
-      }
-    }
-  }
-}
-
-// Hoisted literal-term program for the mask form of the tile body: per term
-// the slot, the literal, the outcome mask {a<lit, a==lit, a>lit} of its
-// operator and whether it opens a conjunct (terms come conjunct by conjunct
-// from the plan compiler).
-struct TermProg {
-  int32_t lhs;
-  int32_t is_real;
-  int32_t ilit;
-  float flit;
-  uint64_t m_lt, m_eq, m_gt;  // all-ones / zero lane masks
-  int32_t first;
-};
-
-__device__ __forceinline__ uint32_t outcome_mask(int op) {
-  switch (op) {
-    case kLT: return 1u;
-    case kLE: return 3u;
-    case kGT: return 4u;
-    case kGE: return 6u;
-    case kEQ: return 2u;
-    case kNE: return 5u;
-    default: return 0u;
-  }
-}
-
-// Mask form (KS == 0, <= TQ hoisted literal terms): every compare's wave
-// ballot is a lane mask in SGPRs (bit l = row 4l + j of the tile); operator,
-// OR within a conjunct and AND across conjuncts run on the scalar unit, so a
-// term costs 2 v_cmp per row group and no branches on the operator.
-template <int K, int MODE, bool DEL, int TQ>
-__device__ __forceinline__ void mask_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, 0>& D,
-                                          int64_t t, int lane, int nterms, bool cnf_live, bool partial, bool tile_valid,
-                                          const TermProg (&tp)[TQ], int agg_slot, bool agg_real, Acc& acc,
-                                          uint64_t& wave_count) {
-  const int64_t nrows = L.nrows;
-  const int64_t nwords = (nrows + 63) >> 6;
-  const int64_t row0 = t * kTileRows + lane * 4;
-  uint64_t word[4], cur[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    word[j] = cnf_live && tile_valid ? ~0ull : 0ull;
-    cur[j] = 0ull;
-  }
-#pragma unroll
-  for (int ti = 0; ti < TQ; ++ti) {
-    if (ti > 0 && ti >= nterms) break;  // nterms >= 1: term 0 always runs (keeps the loads unsunk)
-    const TermProg& T = tp[ti];
-    int32_t a[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
-#pragma unroll
-    for (int s = 1; s < K; ++s)
-      if (T.lhs == s) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
-      }
-    if (T.first && ti > 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        word[j] &= cur[j];
-        cur[j] = 0ull;
-      }
-    }
-    uint64_t lt[4], gt[4];
-    if (T.is_real) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float f = __int_as_float(a[j]);
-        lt[j] = __ballot(f < T.flit);
-        gt[j] = __ballot(f > T.flit);
-        acc.nan |= (f != f) && tile_valid && (!partial || row0 + j < nrows);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        lt[j] = __ballot(a[j] < T.ilit);
-        gt[j] = __ballot(a[j] > T.ilit);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cur[j] |= (lt[j] & T.m_lt) | (~(lt[j] | gt[j]) & T.m_eq) | (gt[j] & T.m_gt);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) word[j] &= cur[j];
-  if (partial) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) word[j] &= __ballot(row0 + j < nrows);
-  }
-  const int64_t wd = t * kWordsPerTile + (lane >> 4);
-  if (DEL) {
-    const uint64_t dw = wd < nwords ? L.deleted[wd] : 0ull;
-    const uint32_t dn = (uint32_t)(dw >> ((lane & 15) * 4)) & 0xFu;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) word[j] &= ~__ballot((dn >> j) & 1u);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) wave_count += __popcll(word[j]);
-  if (MODE == kModeBitmap || MODE == kModeAgg) {
-    bool p[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) p[j] = (word[j] >> lane) & 1ull;
-    if (MODE == kModeBitmap) {
-      const uint32_t nib = (uint32_t)p[0] | ((uint32_t)p[1] << 1) | ((uint32_t)p[2] << 2) | ((uint32_t)p[3] << 3);
-      const uint64_t w = pack_word16(nib, lane);
-      if (tile_valid && (lane & 15) == 0 && wd < nwords) L.out_words[wd] = w;
-    } else if (K > 0) {
-      int32_t g[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) g[j] = D.v[0][j];
-#pragma unroll
-      for (int s = 1; s < K; ++s)
-        if (agg_slot == s) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) g[j] = D.v[s][j];
-        }
-      if (agg_real) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float f = __int_as_float(g[j]);
-          acc.fsum += p[j] ? (double)f : 0.0;
-          acc.fmin = p[j] && f < acc.fmin ? f : acc.fmin;
-          acc.fmax = p[j] && f > acc.fmax ? f : acc.fmax;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc.isum += p[j] ? (int64_t)g[j] : 0;
-          acc.imin = p[j] && g[j] < acc.imin ? g[j] : acc.imin;
-          acc.imax = p[j] && g[j] > acc.imax ? g[j] : acc.imax;
-        }
       }
     }
   }
@@ -886,25 +772,21 @@ __device__ __forceinline__ void load_partial(TileRegs<K, KS>& D, int64_t t, int6
 }
 
 // U tiles per wave iteration: all loads of the U tiles are issued before the
-// first compare (U x (K + 4 KS) x 1 KiB in flight per wave).
-// IL = false: a block owns a contiguous segment of tiles, dealt round-robin
-//   to its 4 waves (per-segment counts feed compaction).
-// IL = true:  grid-stride interleave -- at any moment the whole grid reads one
-//   contiguous window of each column; partial counts are then per block, not
-//   per segment (COUNT / aggregate only).  Measured equal on MI355X.
-// TQ > 0: the mask form (mask_tile) over <= TQ hoisted literal terms.
-template <int K, int KS, int MODE, bool DEL, int U, bool NT, bool IL = false, int TQ = 0, bool MB = true, bool DG = false,
-          bool RI = false>
+// first compare (U x (K + 4 KS) x 1 KiB in flight per wave).  A block owns a
+// contiguous segment of tiles, dealt round-robin to its 4 waves (per-segment
+// counts feed compaction).  A grid-stride interleave measured equal on MI355X
+// (DESIGN.md section 5).
+// TQ > 0: <= TQ literal terms hoisted into registers, term loop unrolled.
+template <int K, int KS, int MODE, bool DEL, int U, bool NT, int TQ = 0, bool RI = false>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
-  static_assert(!(RI && TQ > 0 && KS == 0 && MB), "the mask form keeps the 4-rows-per-lane layout");
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
   const int64_t nrows = L.nrows;
   const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
-  const int64_t t0 = IL ? (int64_t)blockIdx.x * kWaves : (int64_t)blockIdx.x * L.tiles_per_block;
-  const int64_t t1 = IL ? ntiles : min(t0 + L.tiles_per_block, ntiles);
-  const int64_t ustep = IL ? (int64_t)gridDim.x * kWaves : kWaves;  // between the U tiles of one wave
+  const int64_t t0 = (int64_t)blockIdx.x * L.tiles_per_block;
+  const int64_t t1 = min(t0 + L.tiles_per_block, ntiles);
+  constexpr int64_t ustep = kWaves;  // between the U tiles of one wave
   const int nterms = P->nterms;
   const uint32_t all = P->all_conj;
   const int agg_slot = MODE == kModeAgg ? P->agg_slot : 0;
@@ -924,30 +806,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
 #pragma unroll
   for (int ti = 0; ti < TQ; ++ti)
     if (ti < nterms) th[ti] = P->terms[ti];
-  constexpr bool kMask = TQ > 0 && KS == 0 && MB;
-  TermProg tprog[TQ > 0 ? TQ : 1];
-  bool cnf_live = true;
-  if (kMask) {
-    uint32_t covered = 0, prev = 0;
-#pragma unroll
-    for (int ti = 0; ti < TQ; ++ti) {
-      if (ti < nterms) {
-        const KTerm& T = th[ti];
-        const uint32_t m = outcome_mask(T.op);
-        tprog[ti].lhs = T.lhs;
-        tprog[ti].is_real = T.kind == kReal;
-        tprog[ti].ilit = T.ilit;
-        tprog[ti].flit = T.flit;
-        tprog[ti].m_lt = (m & 1u) ? ~0ull : 0ull;
-        tprog[ti].m_eq = (m & 2u) ? ~0ull : 0ull;
-        tprog[ti].m_gt = (m & 4u) ? ~0ull : 0ull;
-        tprog[ti].first = T.conj_bit != prev;
-        prev = T.conj_bit;
-        covered |= T.conj_bit;
-      }
-    }
-    cnf_live = covered == all;  // a conjunct without a live term is never true
-  }
 
   // full tiles in the main loop; the partial last tile (if any) after it
   const int64_t tf = min(t1, nrows / kTileRows);
@@ -984,40 +842,31 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t t = base + (int64_t)u * ustep;
-      if constexpr (kMask) {
-        // unconditional: a clamped (duplicate) tile is evaluated with an empty
-        // result and writes nothing, so no branch separates the loads from
-        // their compares
-        const bool valid = t < tf;
-        mask_tile<K, MODE, DEL, (TQ > 0 ? TQ : 1)>(L, P, D[u], valid ? t : tf - 1, lane, nterms, cnf_live, false,
-                                                   valid, tprog, agg_slot, agg_real, acc, wave_count);
-      } else if (t < tf) {
+      if (t < tf) {
         if constexpr (kSink) {
           uint64_t w[4];
-          fast_tile<K, KS, MODE, DEL, TQ, DG, RI>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc,
-                                                  wave_count, th, w);
+          fast_tile<K, KS, MODE, DEL, TQ, RI>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
+                                              th, w);
           if ((lane >> 2) == sink_n) {
             const int j = lane & 3;
             sink = j == 0 ? w[0] : (j == 1 ? w[1] : (j == 2 ? w[2] : w[3]));
           }
           if (++sink_n == 16) sink_flush();
         } else {
-          fast_tile<K, KS, MODE, DEL, TQ, DG, RI>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc,
-                                                  wave_count, th);
+          fast_tile<K, KS, MODE, DEL, TQ, RI>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
+                                              th);
         }
       }
     }
   };
   const int64_t step = ustep * U;
-  {
-    for (int64_t base = t0 + wave; base < tf; base += step) {
-      TileRegs<K, KS> D[U];
-      if (TQ > 0)  // every path issues all U loads: exact vmcnt waits
-        load_tiles_clamped<K, KS, U, NT, RI>(D, base, ustep, tf, colp, strp, lane);
-      else
-        load_tiles<K, KS, U, NT, RI>(D, base, ustep, tf, colp, strp, lane);
-      compute(D, base);
-    }
+  for (int64_t base = t0 + wave; base < tf; base += step) {
+    TileRegs<K, KS> D[U];
+    if (TQ > 0)  // every path issues all U loads: exact vmcnt waits
+      load_tiles_clamped<K, KS, U, NT, RI>(D, base, ustep, tf, colp, strp, lane);
+    else
+      load_tiles<K, KS, U, NT, RI>(D, base, ustep, tf, colp, strp, lane);
+    compute(D, base);
   }
   if constexpr (kSink) {
     sink_flush();
@@ -1032,11 +881,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   if ((nrows % kTileRows) != 0 && tp >= t0 + wave && tp < t1 && (tp - t0 - wave) % ustep == 0) {
     TileRegs<K, KS> D;
     load_partial<K, KS, RI>(D, tp, nrows, colp, strp, lane);
-    if constexpr (kMask)
-      mask_tile<K, MODE, DEL, (TQ > 0 ? TQ : 1)>(L, P, D, tp, lane, nterms, cnf_live, true, true, tprog, agg_slot,
-                                                 agg_real, acc, wave_count);
-    else
-      fast_tile<K, KS, MODE, DEL, TQ, DG, RI>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+    fast_tile<K, KS, MODE, DEL, TQ, RI>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
   }
   acc.count = lane == 0 ? (int64_t)wave_count : 0;
   block_reduce_store<MODE == kModeAgg>(acc, L);
@@ -1067,6 +912,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_generic(ScanLaunch L) {
     const int64_t row = w * 64 + lane;
     const bool valid = row < nrows;
     uint32_t cb = 0;
+    bool nanr = false;  // reached a float compare on a NaN (fast_tile's rule)
     for (int ti = 0; ti < nterms; ++ti) {
       const KTerm& T = P->terms[ti];
       bool r = false;
@@ -1089,14 +935,17 @@ __global__ __launch_bounds__(kBlock) void k_scan_generic(ScanLaunch L) {
         } else {
           const float a = ((const float*)A.base)[row];
           const float b = T.rhs >= 0 ? ((const float*)P->cols[T.rhs].base)[row] : T.flit;
-          acc.nan |= (a != a) || (b != b);
+          const bool reach = ((cb & T.req_below) == T.req_below) && !(cb & T.conj_bit);
+          nanr = nanr || (reach && (T.nan_lit || a != a || b != b));
           r = cmp1<float>(T.op, a, b);
         }
       }
       cb |= r ? T.conj_bit : 0u;
     }
-    bool p = valid && cb == all;
-    if (DEL) p = p && !((L.deleted[w] >> lane) & 1ull);
+    bool live = valid;
+    if (DEL) live = live && !((L.deleted[w] >> lane) & 1ull);
+    const bool p = live && (cb & all) == all;
+    acc.nan |= nanr && live;
     const uint64_t m = __ballot(p);
     if (MODE == kModeBitmap && lane == 0) L.out_words[w] = m;
     wave_count += __popcll(m);
@@ -1584,63 +1433,30 @@ static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   // 4-byte slots only and 1..kHoistTerms literal terms (L.hoist_terms): the terms
   // are hoisted into registers (TQ) and the per-row tile body is unrolled over
   // them -- measured 2.5 % faster than reading them from the plan per tile
-  // and than the SGPR-mask body (variant 16), profiles/r01/an3
+  // and than an SGPR-lane-mask body, profiles/r01/an3
   constexpr int TQ = KS == 0 ? kHoistTerms : 0;
   // one 4-byte column: 4 tiles in flight per wave (the same bytes in flight as
   // two columns at U=2); 100M rows: COUNT 69.7 -> 67.3 us, BitSet 87.5 -> 81.0 us
   constexpr int kU = K == 1 && KS == 0 ? 4 : kDefaultU;
   const unsigned lds = L.sink_lds ? (unsigned)(L.tiles_per_block * kWordsPerTile * sizeof(uint64_t)) : 0u;
   if (KS == 0 && L.hoist_terms)
-    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, false, TQ, false, false, RI>), grid,
-                       dim3(kBlock), lds, s, L);
+    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, TQ, RI>), grid, dim3(kBlock), lds, s, L);
   else
-    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, false, 0, false, false, RI>), grid,
-                       dim3(kBlock), lds, s, L);
+    hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, 0, RI>), grid, dim3(kBlock), lds, s, L);
 }
 
 template <int K, int KS, int MODE>
 static void fast_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
-  constexpr int TQ = KS == 0 ? kHoistTerms : 0;
-  const bool hoist = KS == 0 && L.hoist_terms;
   if (L.deleted) {
     if (L.ri)
       prod_launch<K, KS, MODE, true, true>(L, grid, s);
     else
       prod_launch<K, KS, MODE, true, false>(L, grid, s);
-    return;
-  }
-  if (L.ri) {
+  } else if (L.ri) {
     prod_launch<K, KS, MODE, false, true>(L, grid, s);
-    return;
+  } else {
+    prod_launch<K, KS, MODE, false, false>(L, grid, s);
   }
-  if constexpr (K == 2 && KS == 0 && MODE == kModeCount) {  // tuning variants of the C3 kernel
-    switch (L.variant) {
-      case 1: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 1, false>), grid, dim3(kBlock), 0, s, L); return;
-      case 4: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 1, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 6: hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 4, true>), grid, dim3(kBlock), 0, s, L); return;
-      case 11:  // per-row form, grid-stride interleave
-        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, true>), grid, dim3(kBlock), 0, s, L);
-        return;
-      case 12:  // per-row form, U=2 (the round-B kernel)
-        hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true>), grid, dim3(kBlock), 0, s, L);
-        return;
-      case 19:  // hoisted terms, term i on slot i (compile-time register choice)
-        if (hoist && L.diag_terms) {
-          hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, TQ, false, true>), grid, dim3(kBlock), 0,
-                             s, L);
-          return;
-        }
-        break;
-      case 16:  // mask form (mask_tile): CNF on SGPR lane masks
-        if (hoist) {
-          hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, false, 2, true, false, TQ, true>), grid, dim3(kBlock), 0, s, L);
-          return;
-        }
-        break;
-      default: break;
-    }
-  }
-  prod_launch<K, KS, MODE, false, false>(L, grid, s);
 }
 
 // fast_k = number of 4-byte slots, fast_ks = number of 16-byte string slots;

@@ -38,14 +38,30 @@ using mbx::AggOut;
 using mbx::KPlan;
 using mbx::Partial;
 
+// A/B tuning knobs of the scan path.  Read from the
+// MBX_* environment once in mbx_init and changed only by mbx_set_tuning, so
+// no launch reads the environment.  -1 = the built-in default.
+struct MbxTuning {
+  int64_t tiles_per_block = -1;   // MBX_TILES_PER_BLOCK: segment size of every scan / BitSet
+  int32_t force_generic = 0;      // MBX_FORCE_GENERIC: plans compiled after this use k_scan_generic
+  int32_t scan_hoist = 1;         // MBX_SCAN_HOIST: 0 reads terms from the plan per tile
+  int32_t scan_ri = 1;            // MBX_SCAN_RI: 0 never, 1 BitSet output only, 2 always
+  int32_t sink_lds = 1;           // MBX_SINK_LDS: 0 never, 1 segments >= 128 tiles, 2 whenever it fits
+  int32_t ticket_groups = -1;     // MBX_TICKET_GROUPS
+  int32_t fin_mode = -1;          // MBX_FIN_MODE (FinMode)
+  int32_t join_plain = 0;         // MBX_JOIN_PLAIN: k_join_matrix instead of the fast form
+  int32_t distinct_lds_probes = -1;  // MBX_DISTINCT_LDS_PROBES
+};
+
 struct mbx_ctx {
   int32_t device = 0;
+  MbxTuning tune;
   hipStream_t stream = nullptr;
   Partial* partials = nullptr;  // scratch, one per block of the largest scan so far
   int64_t partials_cap = 0;
   AggOut* dagg = nullptr;
   int64_t* dcount = nullptr;
-  int32_t* dnan = nullptr;
+  int32_t* dnan = nullptr;       // async scans: [0] last, [1] sticky until mbx_sync; sync scans: [2]
   uint32_t* ticket = nullptr;   // in-launch finalize ticket (always 0 between launches)
   int64_t* ids_scratch = nullptr;  // positions for a gather whose caller wants no positions
   int64_t ids_cap = 0;

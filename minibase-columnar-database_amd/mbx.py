@@ -86,7 +86,7 @@ EXPORTS = [
     "mbx_scan_aggregate_async", "mbx_bitmap_alloc", "mbx_bitmap_upload", "mbx_bitmap_download", "mbx_bitmap_info",
     "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_bitmap_index_build",
     "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
-    "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close", "mbx_probe_read",
+    "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close", "mbx_probe_read", "mbx_set_tuning",
     # include/mbx_db.h
     "mbx_db_create", "mbx_db_open", "mbx_db_close", "mbx_db_info", "mbx_db_file_entry", "mbx_db_columnar_create",
     "mbx_db_columnar_insert", "mbx_db_columnar_info", "mbx_db_mark_deleted", "mbx_db_bitmap_write",
@@ -161,6 +161,7 @@ def lib():
         "mbx_cursor_restart": ([V], ctypes.c_int),
         "mbx_cursor_close": ([V], ctypes.c_int),
         "mbx_probe_read": ([V, V, P(I32), I32, I64, I32, I64], ctypes.c_int),
+        "mbx_set_tuning": ([V, ctypes.c_char_p, I64], ctypes.c_int),
         "mbx_db_create": ([ctypes.c_char_p, I32, P(V)], ctypes.c_int),
         "mbx_db_open": ([ctypes.c_char_p, P(V)], ctypes.c_int),
         "mbx_db_close": ([V], ctypes.c_int),
@@ -297,6 +298,11 @@ class Context:
 
     def sync(self):
         _chk(lib().mbx_sync(self.h))
+
+    def set_tuning(self, knob, value=0):
+        """mbx_set_tuning: one A/B knob of this context ("reset" restores the
+        MBX_* environment defaults read at mbx_init)."""
+        _chk(lib().mbx_set_tuning(self.h, knob.encode(), int(value)))
 
     def probe_read(self, table, cols, tiles_per_block=0, interleave=False, grid=0):
         """Enqueue the read-bandwidth probe (mbx_probe_read) on self.stream."""

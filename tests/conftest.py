@@ -27,3 +27,11 @@ def minidata():
     import oracle
     rows = helpers.load_minidata()
     return rows, oracle.Table(helpers.minidata_columns(rows))
+
+
+@pytest.fixture
+def tune(ctx):
+    """ctx.set_tuning for one test (the A/B knobs mbx_init otherwise reads
+    once from MBX_*), restored to the defaults afterwards."""
+    yield ctx.set_tuning
+    ctx.set_tuning("reset")

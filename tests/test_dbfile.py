@@ -369,7 +369,7 @@ def test_bitmap_index_large_and_deleted(m, ctx, tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("lds_probes", [None, "0", "1"])
-def test_bitmap_index_many_values(m, ctx, tmp_path, monkeypatch, lds_probes):
+def test_bitmap_index_many_values(m, ctx, tmp_path, tune, lds_probes):
     """k_distinct with thousands of distinct values: blocks whose LDS table
     overflows (and, with MBX_DISTINCT_LDS_PROBES=0 / 1, rows sent to the global
     table directly or after one LDS probe) still give every live value once, in
@@ -378,7 +378,7 @@ def test_bitmap_index_many_values(m, ctx, tmp_path, monkeypatch, lds_probes):
     equal-sized and Heapfile's first-fit insert keeps them in insertion order
     (with mixed widths a shorter later record can fill an earlier page)."""
     if lds_probes is not None:
-        monkeypatch.setenv("MBX_DISTINCT_LDS_PROBES", lds_probes)
+        tune("distinct_lds_probes", int(lds_probes))
     path = str(tmp_path / "db")
     n = 40_000
     rng = np.random.Generator(np.random.PCG64(31))

@@ -124,9 +124,9 @@ def int_table(n, seed=42, hi=1 << 20, ncols=4, deleted_frac=None):
 
 @pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 255, 256, 257, 1000, 4099, 70001])
 @pytest.mark.parametrize("generic", [False, True])
-def test_ragged_sizes(ctx, n, generic, monkeypatch):
+def test_ragged_sizes(ctx, n, generic, tune):
     if generic:
-        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+        tune("force_generic", 1)
     cols, _ = int_table(n, hi=100)
     ot = oracle.Table(cols)
     t = ctx.stage(cols)
@@ -141,10 +141,10 @@ def test_ragged_sizes(ctx, n, generic, monkeypatch):
 
 
 @pytest.mark.parametrize("generic", [False, True])
-def test_c2_range_filter_full_size(ctx, generic, monkeypatch):
+def test_c2_range_filter_full_size(ctx, generic, tune):
     """C2: 10M rows x 4 int32, `c0 < 104858` -> BitSet + positions + COUNT, bit-exact."""
     if generic:
-        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+        tune("force_generic", 1)
     n = 10_000_000
     cols, _ = int_table(n)
     ot = oracle.Table(cols)
@@ -173,9 +173,9 @@ def test_c3_conjunction_count_full_size(ctx):
 
 
 @pytest.mark.parametrize("generic", [False, True])
-def test_deleted_rows(ctx, generic, monkeypatch):
+def test_deleted_rows(ctx, generic, tune):
     if generic:
-        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+        tune("force_generic", 1)
     n = 1_000_003
     cols, dele = int_table(n, hi=1000, deleted_frac=0.1)
     ot = oracle.Table(cols, dele)
@@ -198,15 +198,15 @@ def _np_words(mask):
 @pytest.mark.parametrize("ri", ["0", "1"])
 @pytest.mark.parametrize("deleted", [False, True])
 @pytest.mark.parametrize("sink_lds", ["1", "2"])  # LDS-staged BitSet: default rule / whenever it fits
-def test_bitset_segments_and_tile_layouts(ctx, tpb, ri, deleted, sink_lds, monkeypatch):
+def test_bitset_segments_and_tile_layouts(ctx, tpb, ri, deleted, sink_lds, tune):
     """BitSet output over segment sizes that give each wave 1..250 tiles (the
     RI layout buffers 16 tiles' words per store) and a ragged tail, both tile
     layouts (MBX_SCAN_RI), with and without deleted rows; numpy is the check
     (the same predicate, bit for bit)."""
     if tpb:
-        monkeypatch.setenv("MBX_TILES_PER_BLOCK", str(tpb))
-    monkeypatch.setenv("MBX_SCAN_RI", ri)
-    monkeypatch.setenv("MBX_SINK_LDS", sink_lds)
+        tune("tiles_per_block", tpb)
+    tune("scan_ri", int(ri))
+    tune("sink_lds", int(sink_lds))
     n = 2_000_003
     cols, dele = int_table(n, hi=1000, deleted_frac=0.05 if deleted else None)
     t = ctx.stage(cols, dele)
@@ -239,10 +239,10 @@ def test_scan_select_positions(ctx, n):
 
 
 @pytest.mark.parametrize("tpb", [4, 37, 200, 512, 513, 1000])
-def test_scan_select_segment_sizes(ctx, tpb, monkeypatch):
+def test_scan_select_segment_sizes(ctx, tpb, tune):
     """Segments of 16..4000 words; positions and the BitSet left in the
     bitmap both exact, also through the async entry point."""
-    monkeypatch.setenv("MBX_TILES_PER_BLOCK", str(tpb))
+    tune("tiles_per_block", tpb)
     n = 3_000_017
     cols, _ = int_table(n, hi=1000)
     t = ctx.stage(cols)
@@ -266,10 +266,10 @@ def test_scan_select_segment_sizes(ctx, tpb, monkeypatch):
 
 
 @pytest.mark.parametrize("generic", [False, True])
-def test_scan_select_strings_and_floats(ctx, generic, monkeypatch):
+def test_scan_select_strings_and_floats(ctx, generic, tune):
     """String-slot (KS > 0) and float plans, fast and generic kernels."""
     if generic:
-        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+        tune("force_generic", 1)
     cols, _ = mixed_table(200_003, seed=11)
     ot, t = oracle.Table(cols), ctx.stage(cols)
     cnf = [[(oracle.GE, ("sym", 3), ("str", "M"))], [(oracle.LT, ("sym", 2), ("real", 0.5)),
@@ -333,11 +333,11 @@ C5_CNF = [[(oracle.LT, ("sym", 1), ("int", 1 << 19))], [(oracle.GE, ("sym", 2), 
 
 @pytest.mark.parametrize("generic", [False, True])
 @pytest.mark.parametrize("deleted", [False, True])
-def test_c5_mixed_filter_and_aggregates(ctx, generic, deleted, monkeypatch):
+def test_c5_mixed_filter_and_aggregates(ctx, generic, deleted, tune):
     """C5 shape: int32 + float32 + char(16) (16-byte string slot of the fast
     kernel, or the generic kernel), 3 conjuncts + SUM/MIN/MAX."""
     if generic:
-        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+        tune("force_generic", 1)
     n = 2_000_003
     cols, _ = mixed_table(n)
     dele = helpers.random_deleted(n, 0.07) if deleted else None
@@ -356,9 +356,9 @@ def test_c5_mixed_filter_and_aggregates(ctx, generic, deleted, monkeypatch):
 
 
 @pytest.mark.parametrize("generic", [False, True])
-def test_fast_path_aggregates(ctx, generic, monkeypatch):
+def test_fast_path_aggregates(ctx, generic, tune):
     if generic:
-        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+        tune("force_generic", 1)
     n = 3_000_017
     rng = np.random.Generator(np.random.PCG64(11))
     cols = [(oracle.INTEGER, 4, rng.integers(-1000, 1000, n, dtype=np.int32)),
@@ -384,9 +384,9 @@ def test_nan_raises_like_the_reference(ctx, m):
 
 
 @pytest.mark.parametrize("generic", [False, True])
-def test_strings_java_order(ctx, generic, monkeypatch):
+def test_strings_java_order(ctx, generic, tune):
     if generic:
-        monkeypatch.setenv("MBX_FORCE_GENERIC", "1")
+        tune("force_generic", 1)
     vals = ["", "a", "ab", "b", "South_Dakota", "South", "é", "€", "\U0001F600", "a\u0000b", "a\u0000",
             "zzzzzzzzzzzzzzzz"]
     arr = helpers.encode_strings(vals, 16)
@@ -652,16 +652,16 @@ def test_c5_full_table_1b_rows(ctx, m):
     ("32", "0", "0"),      # write-through partials (MBX_FIN_MODE=0)
     ("32", "0", "2"),      # separate finalize launch
 ])
-def test_count_and_bitset_finalize_forms(ctx, groups, tpb, fin, monkeypatch):
+def test_count_and_bitset_finalize_forms(ctx, groups, tpb, fin, tune):
     """COUNT and BitSet scans end in the packed 64-bit ticket words (count |
     NaN blocks | arrivals); every grouping, the > 4095-arrival fallback and
     the other finalize forms give the same count, BitSet and positions
     (numpy check), and back-to-back launches see the words reset."""
-    monkeypatch.setenv("MBX_TICKET_GROUPS", groups)
+    tune("ticket_groups", int(groups))
     if tpb != "0":
-        monkeypatch.setenv("MBX_TILES_PER_BLOCK", tpb)
+        tune("tiles_per_block", int(tpb))
     if fin is not None:
-        monkeypatch.setenv("MBX_FIN_MODE", fin)
+        tune("fin_mode", int(fin))
     n = 5_000_017
     cols, _ = int_table(n, hi=1000)
     t = ctx.stage(cols)

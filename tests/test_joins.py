@@ -193,7 +193,7 @@ def test_gpu_join_edges(m, ctx):
 @pytest.mark.parametrize("order", ["bmj", "nlj"])
 @pytest.mark.parametrize("jc", ["{(x,<=,x)}^{(f,>,f)|(y,=,y)}", "{(x,!=,y)}^{(f,>=,f)}^{(y,<,x)|(x,=,y)}", "{(x,=,x)}",
                                 "{(x,!=,y)}^{(f,>=,f)}^{(y,<,x)|(x,=,y)}^{(f,<,f)|(x,>,x)}"])
-def test_gpu_join_numeric_fast_path(m, ctx, order, jc, monkeypatch):
+def test_gpu_join_numeric_fast_path(m, ctx, order, jc, tune):
     """CNFs of <= 4 int / float terms take k_join_matrix_fast (row side swept
     by v_readlane; the 6-term CNF stays on the plain kernel).  Ragged selections (not multiples of 64) and an NLJ block
     whose passes start inside a 64-row chunk; pairs == oracle pairs and ==
@@ -225,18 +225,18 @@ def test_gpu_join_numeric_fast_path(m, ctx, order, jc, monkeypatch):
     op_, ip_, ps, _ = ctx.join(to, so, ti, si, join_cnf(O, I, jc), kind, block)
     got = list(zip(op_.tolist(), ip_.tolist(), ps.tolist()))
     assert got == want
-    monkeypatch.setenv("MBX_JOIN_PLAIN", "1")
+    tune("join_plain", 1)
     op_, ip_, ps, _ = ctx.join(to, so, ti, si, join_cnf(O, I, jc), kind, block)
     assert list(zip(op_.tolist(), ip_.tolist(), ps.tolist())) == got
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("plain", [False, True])
-def test_gpu_join_float_nan_raises(m, ctx, monkeypatch, plain):
+def test_gpu_join_float_nan_raises(m, ctx, tune, plain):
     """A NaN reaching a float join compare is an error (TupleUtils' float
     branch falls through), in both kernels; NaN outside the selections is not."""
     if plain:
-        monkeypatch.setenv("MBX_JOIN_PLAIN", "1")
+        tune("join_plain", 1)
     f = np.arange(100, dtype=np.float32)
     f[70] = np.nan
     t = ctx.stage([(oracle.REAL, 4, f)])
