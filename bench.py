@@ -1,22 +1,31 @@
 #!/usr/bin/env python3
 """bench.py -- BASELINE.json headline: scanned rows/s + HBM GB/s on the C3
-workload (100M-row 4 x int32 Columnarfile, 2-predicate conjunction + COUNT).
+workload (100M-row 4 x int32 Columnarfile, 2-predicate conjunction + COUNT),
+at 1 / 2 / 4 / 8 GPUs.
 
 One "step" = one ColumnarFileScan COUNT pass over the resident table:
 `query ... {(c0 < 2^19)} ^ {(c1 >= 2^19)} FILESCAN` -> Total Results Count,
-executed as ONE kernel launch (k_scan_fast<2, COUNT>; its last block folds the
-per-block partials).  Inputs are resident in HBM before the timed region.
-With --streams > 1 consecutive steps alternate over library contexts (each its
-own HIP stream and scratch); the default 1 runs one pass at a time.
+executed as ONE kernel launch per GPU (k_scan_fast<2, COUNT>; its last block
+folds the per-block counts), plus -- on N > 1 GPUs -- the path's one exchange
+step: an in-place RCCL all-reduce of the step's COUNT over xGMI, issued by
+libmbx (mbx_comm_allreduce_count_async) on the communicator's exchange
+stream, so the next step's scan overlaps it.  Inputs are resident in HBM
+before the timed region.
 
-Multi-GPU (weak scaling): each rank owns its own 100M-row
-shard (rows [rank*N, (rank+1)*N) of one logical table); per step the ranks'
-counts are combined by one RCCL all_reduce (async, ordered after that step's
-scan, overlapping the next step's scan).  value = total rows scanned by all
-ranks / max-over-ranks time.  MBX_BENCH_FORCE_EXCHANGE=1 keeps the exchange at
-N=1 (a one-rank RCCL group).  stdout carries only the JSON line.
+Scaling:
+  --scaling strong (default): the metric's config -- ONE 100M-row table, split
+      into N 64-aligned row-range shards (mbx_shard_bounds); every GPU holds
+      the same global table's columns for its shard (generated full-size with
+      the same seeds, then sliced), so the global COUNT is the same for every
+      N and is checked against a torch reduction of the whole table.
+  --scaling weak: every rank owns its own --rows-row table.
+The timed steps replay HIP graphs (mbx_graph_*) of --graph-steps captured
+steps (scan + exchange each): launch-bound small shards (12.5M rows/GPU at
+N=8, ~18 us per scan) would otherwise wait on the host.  value = global rows
+scanned by all ranks / max-over-ranks wall time.  stdout carries only the
+JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
 """
 import argparse
 import json
@@ -120,18 +129,46 @@ def quiet_stdout():
     return fd
 
 
+def make_columns(torch, n_global, s, e, seed_base):
+    """Columns c0..c3 of rows [s, e) of one logical table: each column is
+    generated whole on this GPU from its own seed (torch Philox), so every
+    shard count N slices the same table, then the shard is copied out."""
+    cols = []
+    for j in range(4):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(seed_base + j)
+        full = torch.randint(0, 1 << 20, (n_global,), dtype=torch.int32, device="cuda", generator=g)
+        cols.append(full[s:e].clone())
+        del full
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return cols
+
+
+def full_count(torch, n_global, seed_base):
+    """The global C3 COUNT of the whole table (torch reduction, chunk-free)."""
+    out = []
+    for j in range(2):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(seed_base + j)
+        out.append(torch.randint(0, 1 << 20, (n_global,), dtype=torch.int32, device="cuda", generator=g))
+    c = int(((out[0] < THRESH) & (out[1] >= THRESH)).sum().item())
+    del out
+    torch.cuda.empty_cache()
+    return c
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--rows", type=int, default=100_000_000, help="rows per GPU")
+    ap.add_argument("--rows", type=int, default=100_000_000,
+                    help="global rows (strong scaling) or rows per GPU (weak)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured HIP graph (0: eager launches)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="contexts (HIP streams) the steps alternate over.  >1 overlaps consecutive passes; "
-                         "measured on MI355X the two concurrent passes then share fetches through the 256 MB "
-                         "Infinity Cache (6.8 TB/s apparent), so the headline keeps 1: one pass at a time")
     args = ap.parse_args()
     out_fd = quiet_stdout()
 
@@ -144,86 +181,99 @@ def main():
 
     import mbx_pkg
 
-    # rehearsal knobs (never set by the driver): MBX_BENCH_BACKEND=gloo and
-    # MBX_BENCH_SAME_DEVICE=1 run N ranks on one GPU to exercise the N>1 flow
-    backend = os.environ.get("MBX_BENCH_BACKEND", "nccl")
-    device = 0 if os.environ.get("MBX_BENCH_SAME_DEVICE") == "1" else local_rank
+    # rehearsal knob (never set by the driver): MBX_BENCH_SAME_DEVICE=1 runs N
+    # ranks on one GPU (RCCL refuses two ranks on one device, so the exchange
+    # then goes over gloo on the host)
+    same_device = os.environ.get("MBX_BENCH_SAME_DEVICE") == "1"
+    device = 0 if same_device else local_rank
     torch.cuda.set_device(device)
-    # MBX_BENCH_FORCE_EXCHANGE=1 keeps the per-step RCCL exchange at N=1 (a
-    # one-rank process group): the N>1 step, host enqueue cost included, on
-    # one GPU
+    # MBX_BENCH_FORCE_EXCHANGE=1 keeps the per-step exchange at N=1 (a one-rank
+    # RCCL clique): the N>1 step on one GPU
     exchange = world > 1 or os.environ.get("MBX_BENCH_FORCE_EXCHANGE") == "1"
-    if exchange and world == 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29561")
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
-    if exchange:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group(backend)
+    if world > 1:
+        # host-side bootstrap, barriers and the max-over-ranks clock only: the
+        # data-path exchange is libmbx's own RCCL communicator
+        dist.init_process_group("gloo")
     m = mbx_pkg.load()
-    ctxs = [m.Context(device) for _ in range(max(1, args.streams))]
-    ctx = ctxs[0]
-    n = args.rows
+    ctx = m.Context(device)
+
+    n_global = args.rows if args.scaling == "strong" else args.rows * world
+    if args.scaling == "strong":
+        s, e = m.mbx.shard_bounds(args.rows, world, rank)
+        seed_base = 42
+    else:
+        s, e = rank * args.rows, (rank + 1) * args.rows
+        seed_base = 42 + 1000 * rank
+    n = e - s
 
     # synthetic C3 shard, generated in HBM: 4 x int32 uniform [0, 2^20)
-    cols = []
-    for j in range(4):
-        g = torch.Generator(device="cuda")
-        g.manual_seed(42 + j + 1000 * rank)
-        cols.append(torch.randint(0, 1 << 20, (n,), dtype=torch.int32, device="cuda", generator=g))
-    torch.cuda.synchronize()
-    # one zero-copy table view + compiled plan per context (same HBM columns)
-    tables = [c.wrap([(m.mbx.INTEGER, 4)] * 4, [col.data_ptr() for col in cols], n, None, row_offset=rank * n)
-              for c in ctxs]
+    if args.scaling == "strong":
+        cols = make_columns(torch, args.rows, s, e, seed_base)
+    else:
+        cols = make_columns(torch, n, 0, n, seed_base)
+    table = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [col.data_ptr() for col in cols], n, None, row_offset=s)
     cnf = [[(m.mbx.LT, ("sym", 1), ("int", THRESH))], [(m.mbx.GE, ("sym", 2), ("int", THRESH))]]
-    plans = [c.compile(t, cnf) for c, t in zip(ctxs, tables)]
-    table, plan = tables[0], plans[0]
+    plan = ctx.compile(table, cnf)
+
+    comm = None
+    if exchange and not same_device:
+        uid = m.mbx.comm_unique_id() if rank == 0 else None
+        if world > 1:
+            box = [uid]
+            dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+        comm = ctx.comm_init_rank(world, rank, uid)
 
     # correctness gate before timing: the kernel's count vs a torch reduction
-    # of the same device columns (the oracle cross-check lives in tests/)
+    # of the same device columns; with the exchange, the global count vs the
+    # whole table (strong) (the oracle cross-check lives in tests/)
     got = ctx.scan_count(plan)
     want = int(((cols[0] < THRESH) & (cols[1] >= THRESH)).sum().item())
     assert got == want, f"rank {rank}: scan count {got} != reference {want}"
 
     steps, warmup = args.steps, args.warmup
     counts = torch.zeros(steps + warmup, dtype=torch.int64, device="cuda")
-    exts = [torch.cuda.ExternalStream(c.stream) for c in ctxs]
-    ext = exts[0]
-    if len(exts) == 1:
-        torch.cuda.set_stream(ext)  # collectives are ordered after the library stream's scans
+    ext = torch.cuda.ExternalStream(ctx.stream)
+    torch.cuda.set_stream(ext)
     base = counts.data_ptr()
-
-    works = []
+    gloo_works = []
 
     def step(k):
-        j = k % len(ctxs)
-        ctxs[j].scan_count_async(plans[j], base + 8 * k)
-        if exchange:
-            # the one exchange step: combine this step's COUNT over ranks.  The
-            # collective's stream waits for the scan just enqueued on the
-            # library stream (the current stream); async_op=True keeps the
-            # library stream from waiting on the collective, so the next
-            # step's scan overlaps it.  Completion is waited for before the
-            # clock stops.
-            if len(exts) > 1:
-                with torch.cuda.stream(exts[j]):
-                    works.append(dist.all_reduce(counts[k:k + 1], async_op=True))
-            else:
-                works.append(dist.all_reduce(counts[k:k + 1], async_op=True))
+        ctx.scan_count_async(plan, base + 8 * k)
+        if comm is not None:
+            comm.allreduce_count_async(base + 8 * k, 1)
+        elif exchange:  # same-device rehearsal: gloo over host copies
+            gloo_works.append(k)
 
-    def sync_all():
-        for w in works:
-            w.wait()
-        works.clear()
-        for c in ctxs:
-            c.sync()
+    def drain():
+        ctx.sync()
+        if gloo_works:
+            h = counts[gloo_works].cpu()
+            dist.all_reduce(h)
+            counts[gloo_works] = h.cuda()
+            gloo_works.clear()
 
     for k in range(warmup):
         step(k)
-    sync_all()
+    drain()
+
+    # HIP graphs of G steps each (the timed region replays them); captured
+    # after the warm-up, which sized every scratch buffer
+    G = args.graph_steps if (args.graph_steps > 0 and not gloo_works and not (exchange and comm is None)) else 0
+    graphs = []
+    if G:
+        k0 = warmup
+        while k0 < warmup + steps:
+            g = min(G, warmup + steps - k0)
+            ctx.graph_begin()
+            for k in range(k0, k0 + g):
+                step(k)
+            graphs.append(ctx.graph_end())
+            k0 += g
+        for gr in graphs:  # one untimed replay
+            gr.launch()
+        drain()
+    counts.zero_()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -231,19 +281,21 @@ def main():
 
     # timed region: exactly `steps` steps, barrier + synchronize on both sides
     t0 = time.perf_counter()
-    for k in range(steps):
-        step(warmup + k)
+    if G:
+        for gr in graphs:
+            gr.launch()
+    else:
+        for k in range(steps):
+            step(warmup + k)
     t_enq = time.perf_counter() - t0  # host enqueue time of the steps (diagnostic, stderr)
-    sync_all()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    print(f"rank {rank}: host enqueue {t_enq * 1e6 / steps:.1f} us/step, wall {wall * 1e6 / steps:.1f} us/step",
-          file=sys.stderr)
     c = counts[warmup:].cpu()
 
-    # kernel duration: the same launches again, each bracketed by HIP events
+    # kernel duration: the scans alone again, each bracketed by HIP events
     # recorded on the stream the kernel runs on (the library's stream)
     ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
@@ -253,23 +305,32 @@ def main():
         ev_e[k].record(ext)
     ctx.sync()
     kern_ms = sum(a.elapsed_time(b) for a, b in zip(ev_s, ev_e)) / steps
-    probe = read_probe(ctx, table, ext, torch)
-    if world > 1:
-        assert bool((c == c[0]).all()), "per-step global counts differ"
+    print(f"rank {rank}: rows [{s}, {e}), host enqueue {t_enq * 1e6 / steps:.1f} us/step, "
+          f"wall {wall * 1e6 / steps:.1f} us/step, scan kernel {kern_ms * 1e3:.1f} us", file=sys.stderr)
+    probe = read_probe(ctx, table, ext, torch) if rank == 0 else None
+
+    if exchange:
+        glob = full_count(torch, n_global, seed_base) if args.scaling == "strong" else None
+        if glob is not None:
+            assert bool((c == glob).all()), f"rank {rank}: per-step global counts {c[:4].tolist()} != {glob}"
+        else:
+            assert bool((c == c[0]).all()), "per-step global counts differ"
     else:
         assert bool((c == got).all()), "per-step counts differ"
 
-    t_max = wall
+    t_max, kern_max = wall, kern_ms
     if world > 1:
-        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([wall, kern_ms], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max, kern_ms = float(tt[0]), float(tt[1])
+        t_max, kern_max = float(tt[0]), float(tt[1])
 
     if rank == 0:
-        total_rows = n * world * steps
+        total_rows = n_global * steps
         ms_per_step = t_max * 1e3 / steps
-        algo_bytes = 2 * 4 * n  # c0 + c1 read once per launch
+        algo_bytes = 2 * 4 * n  # c0 + c1 read once per launch (rank 0's shard)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+        xchg = "RCCL all-reduce of the step's COUNT (libmbx mbx_comm, exchange stream)" if comm is not None else (
+            "gloo all-reduce (same-device rehearsal)" if exchange else "none")
         out = {
             "metric": METRIC,
             "value": total_rows / t_max,
@@ -279,20 +340,29 @@ def main():
             "warmup": warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic: 4 x int32 uniform [0, 2^20) per row, generated in HBM (torch Philox, seed 42+col+1000*rank)",
+            "data": "synthetic: 4 x int32 uniform [0, 2^20) per row, generated in HBM (torch Philox, seed 42+col"
+                    + (", one global table sliced into row-range shards)" if args.scaling == "strong"
+                       else "+1000*rank, one table per rank)"),
             "config": {
                 "workload": "C3: 100M-row 4xint32 Columnarfile, {(c0 < 2^19)} ^ {(c1 >= 2^19)} + COUNT "
-                            "(ColumnarFileScan / PredEval), 1 kernel launch per step",
+                            "(ColumnarFileScan / PredEval), 1 scan launch per GPU per step"
+                            + (" + 1 exchange" if exchange else ""),
+                "global_rows": n_global,
                 "rows_per_gpu": n,
-                "global_rows": n * world,
-                "parallelism": f"row-range shards x{world}" + (
-                    f", {'RCCL' if backend == 'nccl' else backend} all_reduce of COUNT per step" if exchange else ""),
-                "streams": len(ctxs),
+                "parallelism": f"row-range shards x{world}",
+                "exchange": xchg,
+                "graph_steps": G,
             },
-            "hbm_gbs": algo_bytes * world / (t_max / steps) / 1e9,
+            "phases_us": {
+                "step_wall": ms_per_step * 1e3,
+                "scan_kernel_max_over_ranks": kern_max * 1e3,
+                "host_enqueue_rank0": t_enq * 1e6 / steps,
+                "exchange_and_overlap": max(0.0, ms_per_step * 1e3 - kern_max * 1e3),
+            },
+            "hbm_gbs": 2 * 4 * n_global / (t_max / steps) / 1e9,
             "roofline": {
                 "bound": "hbm",
                 "kernel": "mbx::k_scan_fast<2, COUNT, no-deleted>",
@@ -316,11 +386,11 @@ def main():
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
         os.write(out_fd, (json.dumps(out) + "\n").encode())
 
-    for t in tables:
-        t.close()
-    for c in ctxs:
-        c.close()
-    if exchange:
+    for gr in graphs:
+        gr.close()
+    ctx.close()
+    if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

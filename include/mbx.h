@@ -252,6 +252,60 @@ int mbx_cursor_next(mbx_cursor *c, int64_t max_rows, int64_t *host_ids, void *co
 int mbx_cursor_restart(mbx_cursor *c); /* Iterator.restart() */
 int mbx_cursor_close(mbx_cursor *c);   /* Iterator.close(), idempotent via free */
 
+/* ---- multi-GPU: row-range shards + one RCCL combine over xGMI ------------
+ * SURVEY.md 8(e), DESIGN.md section 6.  The reference engine is one process
+ * (R/global/SystemDefs.java:6-9); a drop-in caller either drives every GPU
+ * of the node from that process (mbx_comm_init_all: one context per GPU, one
+ * RCCL clique, the *_all collectives in one RCCL group) or runs one process
+ * per GPU (mbx_comm_init_rank with an id from mbx_comm_unique_id, shared by
+ * the launcher).  Rows are independent, so scans never communicate; a
+ * shard's table is staged with row_offset = its first position, and the one
+ * exchange step combines per-shard results:
+ *   COUNT             -> in-place int64 all-reduce (SUM), exact in any order
+ *   COUNT/SUM/MIN/MAX -> all-gather of every rank's 48-byte mbx_agg, folded
+ *                        in rank order on the device (int64 sums exact, the
+ *                        double SUM of the per-rank partials in rank order,
+ *                        MIN/MAX over the per-rank values)
+ *   positions         -> all-gather of the per-rank counts (the concatenation
+ *                        offsets; shard order = ascending global positions)
+ * Stream order: a collective runs on the communicator's exchange stream after
+ * everything already enqueued on the context stream; the context stream does
+ * not wait for it (the next scans overlap).  mbx_sync waits for both;
+ * mbx_comm_wait makes later context work (device side) wait for it. */
+typedef struct mbx_comm mbx_comm;
+#define MBX_COMM_ID_BYTES 128
+
+/* [begin, end) of shard `shard` of `nshards` over nrows positions: begins are
+ * multiples of 64 (BitSet words never straddle shards); non-empty ranges tile
+ * [0, nrows) in shard order */
+int mbx_shard_bounds(int64_t nrows, int32_t nshards, int32_t shard, int64_t *begin, int64_t *end);
+int mbx_comm_unique_id(void *id /* MBX_COMM_ID_BYTES */);
+int mbx_comm_init_rank(mbx_ctx *ctx, int32_t nranks, int32_t rank, const void *id, mbx_comm **out);
+/* one process: ctxs[i] (distinct devices) becomes rank i of one clique */
+int mbx_comm_init_all(mbx_ctx *const *ctxs, int32_t n, mbx_comm **outs);
+int mbx_comm_free(mbx_comm *comm);
+int mbx_comm_info(const mbx_comm *comm, int32_t *nranks, int32_t *rank);
+/* the context stream waits (on the device) for the collectives enqueued so far */
+int mbx_comm_wait(mbx_comm *comm);
+int mbx_comm_allreduce_count_async(mbx_comm *comm, int64_t *dev_counts, int64_t n);
+int mbx_comm_allreduce_agg_async(mbx_comm *comm, mbx_agg *dev_rec);
+/* dev_all[r] = rank r's *dev_count (device memory, nranks entries) */
+int mbx_comm_allgather_count_async(mbx_comm *comm, const int64_t *dev_count, int64_t *dev_all);
+/* one process, n communicators of one mbx_comm_init_all clique (rank order) */
+int mbx_comm_allreduce_count_all(mbx_comm *const *comms, int32_t n, int64_t *const *dev_counts, int64_t count);
+int mbx_comm_allreduce_agg_all(mbx_comm *const *comms, int32_t n, mbx_agg *const *dev_recs);
+
+/* ---- HIP graphs: a repeated query (scan + exchange) captured once and
+ * replayed with one launch.  Between begin and end the context's *_async
+ * calls and its communicator's collectives are recorded, not run; scratch
+ * must already be sized by one uncaptured call of the same query (a capture
+ * allocates nothing).  Replays run on the context stream. */
+typedef struct mbx_graph mbx_graph;
+int mbx_graph_begin(mbx_ctx *ctx);
+int mbx_graph_end(mbx_ctx *ctx, mbx_graph **out);
+int mbx_graph_launch(mbx_graph *g);
+int mbx_graph_free(mbx_graph *g);
+
 /* ---- diagnostics (no reference counterpart): the scan's load pattern with
  * the predicate removed, over the 4-byte columns cols[0..ncols) (ncols <= 4)
  * of t's full 256-row tiles, enqueued on mbx_stream(ctx).  Timed by the

@@ -214,6 +214,7 @@ extern "C" int mbx_free(mbx_ctx* c) {
   if (!c) return MBX_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  comm_release_of(c);
   hipFree(c->partials);
   hipFree(c->dagg);
   hipFree(c->dcount);
@@ -231,7 +232,9 @@ extern "C" int mbx_free(mbx_ctx* c) {
 // sticky word dnan[1] (the kernels' last block), read and cleared here.
 extern "C" int mbx_sync(mbx_ctx* c) {
   NOTNULL(c);
+  if (c->capturing) return fail(MBX_E_INVALID, "mbx_sync inside a graph capture");
   HIPCHK(hipSetDevice(c->device));
+  if (int rc = comm_sync(c)) return rc;
   int32_t* h = (int32_t*)c->pinned + 24;
   HIPCHK(hipMemcpyAsync(h, c->dnan + 1, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));

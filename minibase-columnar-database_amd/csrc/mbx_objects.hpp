@@ -66,6 +66,8 @@ struct mbx_ctx {
   int64_t* ids_scratch = nullptr;  // positions for a gather whose caller wants no positions
   int64_t ids_cap = 0;
   void* pinned = nullptr;       // 256 bytes of pinned host scratch
+  mbx_comm* comm = nullptr;     // multi-GPU exchange (mbx_comm.cpp), owned
+  bool capturing = false;       // mbx_graph_begin .. mbx_graph_end
 };
 
 struct TCol {
@@ -150,5 +152,8 @@ int ensure_count(mbx_ctx* c, mbx_bitmap* b);
 // recount per-segment popcounts of a bitmap written on the device, sync, and
 // set b->count
 int bitmap_recount(mbx_ctx* c, mbx_bitmap* b);
+// mbx_comm.cpp: mbx_sync / mbx_free of a context with a communicator
+int comm_sync(mbx_ctx* c);
+void comm_release_of(mbx_ctx* c);
 
 }  // namespace mbx

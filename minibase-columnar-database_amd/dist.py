@@ -16,8 +16,13 @@ collective combines the per-rank results:
   positions / rows  -> all_gather, concatenated in rank order (= ascending
                        global position order, the reference's nextSetBit order)
 
-Backend-agnostic torch.distributed: "nccl" (RCCL over xGMI) with one process
-per MI355X, "gloo" for the CPU tests.
+Two transports for the same combine:
+  * libmbx's own RCCL communicator (include/mbx.h mbx_comm_*, RcclExchange
+    below): the product path -- the collective runs on the communicator's
+    exchange stream over xGMI, the fold of an aggregate is a one-wave kernel
+    in rank order (identical to fold_aggregates), no host round trip.
+    torch.distributed (any backend) only carries the 128-byte RCCL id.
+  * torch.distributed ("gloo") for the CPU tests: the host-side restatement.
 """
 import numpy as np
 
@@ -135,3 +140,32 @@ def gather_positions(ids, device=None, group=None):
     outs = [torch.zeros(max(cap, 1), dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(outs, buf, group=group)
     return np.concatenate([o[:int(k.item())].cpu().numpy() for o, k in zip(outs, ns)])
+
+
+class RcclExchange:
+    """The exchange step of one rank through libmbx (mbx_comm_init_rank):
+    rank 0's RCCL id is broadcast over the torch.distributed group (gloo is
+    enough: 128 bytes, once), then every collective is libmbx's, enqueued
+    after the context's scans on its exchange stream."""
+
+    def __init__(self, ctx, group=None):
+        import torch.distributed as dist
+        from . import mbx
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        box = [mbx.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0, group=group)
+        self.ctx, self.world, self.rank = ctx, world, rank
+        self.comm = ctx.comm_init_rank(world, rank, box[0])
+
+    def count_async(self, dev_ptr, n=1):
+        """in place: dev_ptr[0..n) = the sum over ranks (int64)"""
+        self.comm.allreduce_count_async(dev_ptr, n)
+
+    def aggregate_async(self, dev_rec_ptr):
+        """in place: the 48-byte mbx_agg record becomes the rank-ordered fold"""
+        self.comm.allreduce_agg_async(dev_rec_ptr)
+
+    def counts_async(self, dev_count_ptr, dev_all_ptr):
+        """dev_all[r] = rank r's count (the concatenation offsets of the
+        per-rank positions / rows, shard order)"""
+        self.comm.allgather_count_async(dev_count_ptr, dev_all_ptr)

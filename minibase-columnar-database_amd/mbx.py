@@ -87,6 +87,10 @@ EXPORTS = [
     "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_bitmap_index_build",
     "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
     "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close", "mbx_probe_read", "mbx_set_tuning",
+    "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
+    "mbx_comm_info", "mbx_comm_wait", "mbx_comm_allreduce_count_async", "mbx_comm_allreduce_agg_async",
+    "mbx_comm_allgather_count_async", "mbx_comm_allreduce_count_all", "mbx_comm_allreduce_agg_all",
+    "mbx_graph_begin", "mbx_graph_end", "mbx_graph_launch", "mbx_graph_free",
     # include/mbx_db.h
     "mbx_db_create", "mbx_db_open", "mbx_db_close", "mbx_db_info", "mbx_db_file_entry", "mbx_db_columnar_create",
     "mbx_db_columnar_insert", "mbx_db_columnar_info", "mbx_db_mark_deleted", "mbx_db_bitmap_write",
@@ -162,6 +166,22 @@ def lib():
         "mbx_cursor_close": ([V], ctypes.c_int),
         "mbx_probe_read": ([V, V, P(I32), I32, I64, I32, I64], ctypes.c_int),
         "mbx_set_tuning": ([V, ctypes.c_char_p, I64], ctypes.c_int),
+        "mbx_shard_bounds": ([I64, I32, I32, P(I64), P(I64)], ctypes.c_int),
+        "mbx_comm_unique_id": ([V], ctypes.c_int),
+        "mbx_comm_init_rank": ([V, I32, I32, V, P(V)], ctypes.c_int),
+        "mbx_comm_init_all": ([P(V), I32, P(V)], ctypes.c_int),
+        "mbx_comm_free": ([V], ctypes.c_int),
+        "mbx_comm_info": ([V, P(I32), P(I32)], ctypes.c_int),
+        "mbx_comm_wait": ([V], ctypes.c_int),
+        "mbx_comm_allreduce_count_async": ([V, V, I64], ctypes.c_int),
+        "mbx_comm_allreduce_agg_async": ([V, V], ctypes.c_int),
+        "mbx_comm_allgather_count_async": ([V, V, V], ctypes.c_int),
+        "mbx_comm_allreduce_count_all": ([P(V), I32, P(V), I64], ctypes.c_int),
+        "mbx_comm_allreduce_agg_all": ([P(V), I32, P(V)], ctypes.c_int),
+        "mbx_graph_begin": ([V], ctypes.c_int),
+        "mbx_graph_end": ([V, P(V)], ctypes.c_int),
+        "mbx_graph_launch": ([V], ctypes.c_int),
+        "mbx_graph_free": ([V], ctypes.c_int),
         "mbx_db_create": ([ctypes.c_char_p, I32, P(V)], ctypes.c_int),
         "mbx_db_open": ([ctypes.c_char_p, P(V)], ctypes.c_int),
         "mbx_db_close": ([V], ctypes.c_int),
@@ -280,7 +300,8 @@ class Context:
     def close(self):
         if self.h:
             # cursors and bitmaps first, then plans, then tables
-            order = {"mbx_cursor_close": 0, "mbx_bitmap_free": 1, "mbx_plan_free": 2, "mbx_table_free": 3}
+            order = {"mbx_graph_free": -2, "mbx_comm_free": -1, "mbx_cursor_close": 0, "mbx_bitmap_free": 1,
+                     "mbx_plan_free": 2, "mbx_table_free": 3}
             for ch in sorted(list(self._children), key=lambda o: order.get(o._free, 9)):
                 ch.close()
             lib().mbx_free(self.h)
@@ -524,6 +545,23 @@ class Context:
         _chk(lib().mbx_cursor_open(self.h, table.h, bitmap.h, pj, len(proj), ctypes.byref(h)))
         return Cursor(self, h, table, list(proj))
 
+    # -- multi-GPU exchange (RCCL) and graphs ------------------------------
+    def comm_init_rank(self, nranks, rank, uid):
+        """mbx_comm_init_rank: this context becomes `rank` of an RCCL clique
+        (one process per GPU; every rank passes rank 0's comm_unique_id())."""
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        _chk(lib().mbx_comm_init_rank(self.h, nranks, rank, buf, ctypes.byref(h)))
+        return Comm(self, h, nranks, rank)
+
+    def graph_begin(self):
+        _chk(lib().mbx_graph_begin(self.h))
+
+    def graph_end(self):
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_graph_end(self.h, ctypes.byref(h)))
+        return Graph(self, h)
+
 
 class _Handle:
     _free = None
@@ -538,6 +576,88 @@ class _Handle:
             self.close()
         except Exception:
             pass
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id():
+    """mbx_comm_unique_id: rank 0 creates it, the launcher shares it."""
+    buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+    _chk(lib().mbx_comm_unique_id(buf))
+    return buf.raw
+
+
+def shard_bounds(nrows, nshards, shard):
+    """mbx_shard_bounds: [begin, end) of one 64-aligned row-range shard."""
+    b, e = ctypes.c_int64(), ctypes.c_int64()
+    _chk(lib().mbx_shard_bounds(nrows, nshards, shard, ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
+def comm_init_all(ctxs):
+    """mbx_comm_init_all: one process drives every context's GPU; ctxs[i]
+    becomes rank i of one clique."""
+    n = len(ctxs)
+    hs = (ctypes.c_void_p * n)(*[c.h for c in ctxs])
+    outs = (ctypes.c_void_p * n)()
+    _chk(lib().mbx_comm_init_all(hs, n, outs))
+    return [Comm(c, ctypes.c_void_p(outs[i]), n, i) for i, c in enumerate(ctxs)]
+
+
+def comm_allreduce_count_all(comms, dev_ptrs, count=1):
+    n = len(comms)
+    _chk(lib().mbx_comm_allreduce_count_all((ctypes.c_void_p * n)(*[c.h for c in comms]), n,
+                                            (ctypes.c_void_p * n)(*dev_ptrs), count))
+
+
+def comm_allreduce_agg_all(comms, dev_ptrs):
+    n = len(comms)
+    _chk(lib().mbx_comm_allreduce_agg_all((ctypes.c_void_p * n)(*[c.h for c in comms]), n,
+                                          (ctypes.c_void_p * n)(*dev_ptrs)))
+
+
+class Comm:
+    """mbx_comm: the exchange step of one context (RCCL over xGMI)."""
+    _free = "mbx_comm_free"
+
+    def __init__(self, ctx, h, nranks, rank):
+        self.ctx, self.h, self.nranks, self.rank = ctx, h, nranks, rank
+        ctx._own(self)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mbx_comm_free(self.h)
+            self.h = None
+
+    def wait(self):
+        _chk(lib().mbx_comm_wait(self.h))
+
+    def allreduce_count_async(self, dev_ptr, n=1):
+        _chk(lib().mbx_comm_allreduce_count_async(self.h, dev_ptr, n))
+
+    def allreduce_agg_async(self, dev_ptr):
+        _chk(lib().mbx_comm_allreduce_agg_async(self.h, dev_ptr))
+
+    def allgather_count_async(self, dev_count, dev_all):
+        _chk(lib().mbx_comm_allgather_count_async(self.h, dev_count, dev_all))
+
+
+class Graph:
+    """mbx_graph: captured *_async calls, replayed with one launch."""
+    _free = "mbx_graph_free"
+
+    def __init__(self, ctx, h):
+        self.ctx, self.h = ctx, h
+        ctx._own(self)
+
+    def launch(self):
+        _chk(lib().mbx_graph_launch(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().mbx_graph_free(self.h)
+            self.h = None
 
 
 class Table(_Handle):

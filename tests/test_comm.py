@@ -1,0 +1,162 @@
+"""The multi-GPU exchange step behind the C-ABI (include/mbx.h, mbx_comm_*):
+row-range shard bounds, RCCL collectives on a context's exchange stream, and
+HIP-graph capture of a repeated scan + exchange.
+
+The GPU box has one MI355X, so the RCCL tests run one-rank cliques (through
+both mbx_comm_init_rank and mbx_comm_init_all): the combine there must equal
+the host-side fold of dist.py bit for bit.  The N-rank data flow (shards,
+global positions, rank-ordered folds) is covered by tests/test_dist.py over
+gloo and by bench.py's strong-scaling run, whose global COUNT is asserted
+against the unsharded table at every N.
+"""
+import numpy as np
+import pytest
+
+import helpers  # noqa: F401  (puts oracle/ on sys.path)
+import mbx_pkg
+import oracle
+
+
+@pytest.fixture(scope="module")
+def m():
+    return mbx_pkg.load()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 7, 8])
+def test_c_shard_bounds_match_dist(m, world):
+    """mbx_shard_bounds (C) == dist.shard_bounds (the Python restatement the
+    gloo tests use), 64-aligned, tiling [0, nrows)."""
+    for n in [0, 1, 63, 64, 65, 1000, 100_003, 100_000_000, 1_000_000_000]:
+        for r in range(world):
+            assert m.mbx.shard_bounds(n, world, r) == m.dist.shard_bounds(n, world, r), (n, world, r)
+
+
+def test_c_shard_bounds_rejects_bad_arguments(m):
+    for args in [(-1, 2, 0), (10, 0, 0), (10, 2, 2), (10, 2, -1)]:
+        with pytest.raises(m.MbxError):
+            m.mbx.shard_bounds(*args)
+
+
+# ---------------------------------------------------------------- GPU
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    return torch
+
+
+def _table(m, ctx, n=1_000_003, seed=3):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cols = [(oracle.INTEGER, 4, rng.integers(-1000, 1000, n, dtype=np.int32)),
+            (oracle.REAL, 4, (rng.random(n, dtype=np.float32) - 0.5) * 100)]
+    return cols, ctx.stage(cols, row_offset=0)
+
+
+CNF = [[(oracle.GT, ("sym", 1), ("int", -100))], [(oracle.LT, ("sym", 2), ("real", 10.0))]]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("init", ["rank", "all"])
+def test_one_rank_rccl_combine_is_exact(m, torch_cuda, init):
+    """COUNT all-reduce, the aggregate all-gather + rank-ordered device fold
+    and the count all-gather on a one-rank clique equal dist.fold_aggregates
+    of the same records bit for bit."""
+    torch = torch_cuda
+    ctx = m.Context(0)
+    try:
+        cols, t = _table(m, ctx)
+        plan = ctx.compile(t, CNF)
+        if init == "rank":
+            comm = ctx.comm_init_rank(1, 0, m.mbx.comm_unique_id())
+        else:
+            (comm,) = m.mbx.comm_init_all([ctx])
+        want = ctx.scan_count(plan)
+        buf = torch.zeros(4, dtype=torch.int64, device="cuda")
+        ctx.scan_count_async(plan, buf.data_ptr())
+        comm.allreduce_count_async(buf.data_ptr(), 1)
+        allc = torch.zeros(1, dtype=torch.int64, device="cuda")
+        comm.allgather_count_async(buf.data_ptr(), allc.data_ptr())
+        ctx.sync()
+        assert int(buf[0]) == want and int(allc[0]) == want
+        for col in (0, 1):
+            rec = torch.zeros(6, dtype=torch.int64, device="cuda")
+            ctx.scan_aggregate_async(plan, col, rec.data_ptr())
+            ctx.sync()
+            local = rec.cpu().numpy().copy()
+            if init == "rank":
+                comm.allreduce_agg_async(rec.data_ptr())
+            else:
+                m.mbx.comm_allreduce_agg_all([comm], [rec.data_ptr()])
+            ctx.sync()
+            folded = m.dist.fold_aggregates(local)
+            got = m.dist.fold_aggregates(rec.cpu().numpy())
+            assert got == folded
+            ref = oracle.aggregate(oracle.Table(cols), CNF, col)
+            assert got["count"] == ref["count"] and got["min"] == ref["min"] and got["max"] == ref["max"]
+        if init == "all":
+            m.mbx.comm_allreduce_count_all([comm], [buf.data_ptr()], 1)
+            ctx.sync()
+            assert int(buf[0]) == want
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_comm_rejects_misuse(m):
+    ctx = m.Context(0)
+    try:
+        with pytest.raises(m.MbxError):
+            ctx.comm_init_rank(2, 2, m.mbx.comm_unique_id())
+        comm = ctx.comm_init_rank(1, 0, m.mbx.comm_unique_id())
+        with pytest.raises(m.MbxError):  # one communicator per context
+            ctx.comm_init_rank(1, 0, m.mbx.comm_unique_id())
+        with pytest.raises(m.MbxError):
+            m.mbx.comm_init_all([ctx])
+        comm.close()
+        ctx2 = m.Context(0)
+        with pytest.raises(m.MbxError):  # one device, two ranks
+            m.mbx.comm_init_all([ctx, ctx2])
+        ctx2.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_comm", [False, True])
+def test_graph_replays_scan_and_exchange(m, torch_cuda, with_comm):
+    """A captured batch of steps (scan -> exchange each, as bench.py times
+    them) replays to the same counts as the eager calls, launch after
+    launch; a NaN-free plan leaves mbx_sync clean."""
+    torch = torch_cuda
+    ctx = m.Context(0)
+    try:
+        cols, t = _table(m, ctx, n=3_000_017)
+        plan = ctx.compile(t, CNF)
+        comm = ctx.comm_init_rank(1, 0, m.mbx.comm_unique_id()) if with_comm else None
+        want = ctx.scan_count(plan)
+        k = 7
+        buf = torch.zeros(k, dtype=torch.int64, device="cuda")
+        ctx.scan_count_async(plan, buf.data_ptr())  # sizes scratch before the capture
+        ctx.sync()
+        ctx.graph_begin()
+        for i in range(k):
+            ctx.scan_count_async(plan, buf.data_ptr() + 8 * i)
+            if comm is not None:
+                comm.allreduce_count_async(buf.data_ptr() + 8 * i, 1)
+        g = ctx.graph_end()
+        ctx.sync()
+        for _ in range(3):
+            buf.zero_()
+            torch.cuda.synchronize()
+            g.launch()
+            ctx.sync()
+            assert buf.cpu().tolist() == [want] * k
+        with pytest.raises(m.MbxError):  # no nested capture / sync inside a capture
+            ctx.graph_begin()
+            ctx.graph_begin()
+        with pytest.raises(m.MbxError):
+            ctx.sync()
+        ctx.graph_end().close()
+        g.close()
+    finally:
+        ctx.close()
