@@ -185,8 +185,11 @@ int mbx_scan_count_async(mbx_ctx *ctx, const mbx_plan *p, int64_t *dev_count);
 int mbx_scan_bitmap(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap **out, int64_t *count);
 int mbx_scan_bitmap_async(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap *out);
 /* the get_next_tid() stream as ascending positions (TID.position, global:
- * row_offset added): BitSet + positions in ONE kernel launch for fast-kernel
- * plans (SURVEY 8(b) mbx_scan_select); host_ids holds up to cap positions */
+ * row_offset added; SURVEY 8(b) mbx_scan_select): two launches, the BitSet
+ * scan and the compaction over its segment counts (DESIGN.md section 5 has
+ * the one-launch forms measured and not kept).  host_ids holds up to cap
+ * positions; their device scratch is sized to the count and released before
+ * the call returns. */
 int mbx_scan_select(mbx_ctx *ctx, const mbx_plan *p, int64_t *host_ids, int64_t cap, int64_t *n);
 /* enqueue only: BitSet into `out` (nbits = the table's rows), positions into
  * dev_ids (capacity: the selected rows, at most the table's rows), the count
@@ -306,6 +309,14 @@ int mbx_graph_end(mbx_ctx *ctx, mbx_graph **out);
 int mbx_graph_launch(mbx_graph *g);
 int mbx_graph_free(mbx_graph *g);
 
+/* ---- device result slots for callers without a HIP allocator of their own
+ * (the JNI glue: *_async results and the collectives' buffers live in device
+ * memory).  No reference counterpart.  mbx_dev_alloc zero-fills; download
+ * waits for the context stream first. */
+int mbx_dev_alloc(mbx_ctx *ctx, int64_t bytes, void **dev);
+int mbx_dev_free(mbx_ctx *ctx, void *dev);
+int mbx_dev_download(mbx_ctx *ctx, const void *dev, void *host, int64_t bytes);
+
 /* ---- diagnostics (no reference counterpart): the scan's load pattern with
  * the predicate removed, over the 4-byte columns cols[0..ncols) (ncols <= 4)
  * of t's full 256-row tiles, enqueued on mbx_stream(ctx).  Timed by the
@@ -318,8 +329,13 @@ int mbx_probe_read(mbx_ctx *ctx, const mbx_table *t, const int32_t *cols, int32_
  * counterpart.  mbx_init reads their MBX_* environment defaults once; no
  * launch reads the environment.  knob: "tiles_per_block", "force_generic",
  * "scan_hoist", "scan_ri", "sink_lds", "ticket_groups", "fin_mode",
- * "join_plain", "distinct_lds_probes"; "reset" restores the defaults. */
+ * "join_plain", "distinct_lds_probes", "select_dbg"; "reset" restores the
+ * defaults. */
 int mbx_set_tuning(mbx_ctx *ctx, const char *knob, int64_t value);
+/* per-block wall_clock64() stamps (start, loads in, after the block barrier,
+ * end) of the last compaction launched with select_dbg bit 3: 4 * nblocks
+ * int64 into host (diagnostic of DESIGN.md section 5) */
+int mbx_diag_select_stamps(mbx_ctx *ctx, int64_t *host, int64_t nblocks);
 
 #ifdef __cplusplus
 }

@@ -82,6 +82,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.fin_mode = (int32_t)env_knob("MBX_FIN_MODE", -1);
   t.join_plain = (int32_t)env_knob("MBX_JOIN_PLAIN", 0);
   t.distinct_lds_probes = (int32_t)env_knob("MBX_DISTINCT_LDS_PROBES", -1);
+  t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
 }
 
 static int ensure_partials(mbx_ctx* c, int64_t n) {
@@ -221,6 +222,7 @@ extern "C" int mbx_free(mbx_ctx* c) {
   hipFree(c->dnan);
   hipFree(c->ticket);
   hipFree(c->ids_scratch);
+  hipFree(c->stamps);
   if (c->pinned) hipHostFree(c->pinned);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -266,11 +268,52 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "fin_mode")) t.fin_mode = v;
   else if (!strcmp(knob, "join_plain")) t.join_plain = v;
   else if (!strcmp(knob, "distinct_lds_probes")) t.distinct_lds_probes = v;
+  else if (!strcmp(knob, "select_dbg")) t.select_dbg = v;
   else return fail(MBX_E_INVALID, "mbx_set_tuning: unknown knob `%s`", knob);
   return MBX_OK;
 }
 
 extern "C" void* mbx_stream(mbx_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+extern "C" int mbx_dev_alloc(mbx_ctx* c, int64_t bytes, void** dev) {
+  NOTNULL(c);
+  NOTNULL(dev);
+  *dev = nullptr;
+  if (bytes <= 0) return fail(MBX_E_INVALID, "dev_alloc: %lld bytes", (long long)bytes);
+  if (c->capturing) return fail(MBX_E_INVALID, "dev_alloc inside a graph capture");
+  HIPCHK(hipSetDevice(c->device));
+  void* p = nullptr;
+  if (hipMalloc(&p, (size_t)bytes) != hipSuccess) return fail(MBX_E_NOMEM, "dev_alloc: %lld bytes", (long long)bytes);
+  hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    hipFree(p);
+    return fail(MBX_E_DEVICE, "dev_alloc: %s", hipGetErrorString(e));
+  }
+  *dev = p;
+  return MBX_OK;
+}
+
+extern "C" int mbx_dev_free(mbx_ctx* c, void* dev) {
+  NOTNULL(c);
+  if (!dev) return MBX_OK;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipFree(dev));
+  return MBX_OK;
+}
+
+extern "C" int mbx_dev_download(mbx_ctx* c, const void* dev, void* host, int64_t bytes) {
+  NOTNULL(c);
+  NOTNULL(dev);
+  NOTNULL(host);
+  if (bytes < 0) return fail(MBX_E_INVALID, "dev_download: %lld bytes", (long long)bytes);
+  if (c->capturing) return fail(MBX_E_INVALID, "dev_download inside a graph capture");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(host, dev, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MBX_OK;
+}
 
 extern "C" int mbx_probe_read(mbx_ctx* c, const mbx_table* t, const int32_t* cols, int32_t ncols,
                               int64_t tiles_per_block, int32_t interleave, int64_t grid) {
@@ -790,6 +833,11 @@ static bool packed_count_fits(int64_t nrows, int64_t nb, int32_t groups) {
 
 // One launch per scan: the kernel's last block finalizes (count / aggregate /
 // NaN flag) through the context's ticket.
+static int32_t ticket_groups_of(const mbx_ctx* c) {
+  const int32_t g = c->tune.ticket_groups >= 0 ? c->tune.ticket_groups : kDefaultTicketGroups;
+  return g > kMaxTicketGroups ? kDefaultTicketGroups : g;
+}
+
 static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int32_t mode, uint64_t* out_words,
                         Partial* parts, int64_t tpb, int64_t* count_out, AggOut* agg_out, int32_t* nan_out) {
   ScanLaunch L;
@@ -819,8 +867,7 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   const bool sink_fits = mode == kModeBitmap && L.ri && v.fast_k + v.fast_ks > 0 &&
                          tpb * kWordsPerTile * (int64_t)sizeof(uint64_t) <= kSinkLdsMaxBytes;
   L.sink_lds = sink_fits && (tu.sink_lds == 2 || (tu.sink_lds == 1 && tpb >= 128));
-  L.ticket_groups = tu.ticket_groups >= 0 ? tu.ticket_groups : kDefaultTicketGroups;
-  if (L.ticket_groups > kMaxTicketGroups) L.ticket_groups = kDefaultTicketGroups;
+  L.ticket_groups = ticket_groups_of(c);
   L.fin_mode = tu.fin_mode >= 0 ? tu.fin_mode : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
   if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))
     L.fin_mode = kFinWriteThrough;
@@ -910,12 +957,12 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
                            int32_t nproj, int64_t row_offset, int64_t* dev_ids, void* const* dev_out,
                            int64_t* dev_total);
 
-// BitSet + ascending positions of one scan: the BitSet scan, then
-// k_select_ids over its segment counts.  A fused one-launch form (the scan
-// publishing its segment count, summing the lower segments' counts and
-// writing its positions from LDS) measured the same -- C2 10M rows 22.9 vs
-// 24.0 us, 100M rows 102 vs 101.5 us: the tail's dependent global round trips
-// cost what the launch boundary costs -- and was not kept.
+// BitSet + ascending positions: the BitSet scan, then k_select_ids over its
+// segment counts.  One-launch forms measured slower: round F's (each block
+// summing the lower segments' counts) and round 2's decoupled look-back
+// (C2 10M rows 22-24 vs 19.8 us; 100M rows equal): polling predecessors
+// while the scan saturates HBM costs 2-11 us per block.
+// dev_ids holds every row's position.
 static int scan_select_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int64_t* dev_ids, int64_t* dev_count,
                             int32_t* dev_nan) {
   int rc = scan_bitmap_into(c, p, b, dev_nan);
@@ -941,33 +988,36 @@ extern "C" int mbx_scan_select(mbx_ctx* c, const mbx_plan* pc, int64_t* host_ids
   NOTNULL(pc);
   NOTNULL(n);
   *n = 0;
+  if (cap < 0) return fail(MBX_E_INVALID, "scan_select: capacity %lld", (long long)cap);
   mbx_plan* p = const_cast<mbx_plan*>(pc);
   int rc = set_device(c);
   if (rc) return rc;
   const int64_t nrows = p->t->nrows;
-  if (c->ids_cap < nrows) {
-    if (c->ids_scratch) HIPCHK(hipFree(c->ids_scratch));
-    c->ids_scratch = nullptr;
-    c->ids_cap = 0;
-    HIPCHK(hipMalloc(&c->ids_scratch, sizeof(int64_t) * (size_t)(nrows > 0 ? nrows : 1)));
-    c->ids_cap = nrows;
-  }
   mbx_bitmap* b = nullptr;
   if ((rc = bitmap_new(c, nrows, &b))) return rc;
+  // device positions: the count, once the BitSet scan has it (at most the
+  // caller's capacity), allocated for this call only
+  int64_t* d = nullptr;
   int64_t count = 0;
-  if (!(rc = scan_select_into(c, p, b, c->ids_scratch, c->dcount, nan_sync(c))) && !(rc = scan_result_sync(c, &count)))
-    rc = check_nan(c);
+  if (!(rc = scan_bitmap_into(c, p, b, nan_sync(c))) && !(rc = scan_result_sync(c, &count)) &&
+      !(rc = check_nan(c)) && count > 0 && count <= cap) {
+    if (hipMalloc(&d, sizeof(int64_t) * (size_t)count) != hipSuccess)
+      rc = fail(MBX_E_NOMEM, "scan_select: %lld positions of device scratch", (long long)count);
+    else
+      rc = materialize_dev(c, p->t, b, nullptr, 0, p->t->row_offset, d, nullptr, c->dcount);
+  }
   if (!rc && count > cap)
     rc = fail(MBX_E_INVALID, "scan_select: %lld positions, capacity %lld", (long long)count, (long long)cap);
   if (!rc && count > 0) {
     if (!host_ids) rc = fail(MBX_E_INVALID, "scan_select: null host_ids");
     else {
-      hipError_t e = hipMemcpyAsync(host_ids, c->ids_scratch, (size_t)count * sizeof(int64_t), hipMemcpyDeviceToHost,
-                                    c->stream);
+      hipError_t e = hipMemcpyAsync(host_ids, d, (size_t)count * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
       if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
       if (e != hipSuccess) rc = fail(MBX_E_DEVICE, "scan_select: %s", hipGetErrorString(e));
     }
   }
+  hipStreamSynchronize(c->stream);
+  if (d) hipFree(d);
   mbx_bitmap_free(b);
   if (rc) return rc;
   *n = count;
@@ -1316,8 +1366,25 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
     }
     dev_ids = c->ids_scratch;
   }
+  int64_t* stamps = nullptr;
+  if (c->tune.select_dbg & 8) {  // diagnostic stamps (mbx_diag_select_stamps)
+    if (!c->stamps) HIPCHK(hipMalloc(&c->stamps, sizeof(int64_t) * 4 * kMaxStampBlocks));
+    if (sel->nseg <= kMaxStampBlocks) stamps = c->stamps;
+  }
   HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segs, row_offset, dev_ids, pc, dev_out, nproj,
-                            dev_total, c->stream));
+                            dev_total, c->stream, c->tune.select_dbg & 3, stamps));
+  return MBX_OK;
+}
+
+extern "C" int mbx_diag_select_stamps(mbx_ctx* c, int64_t* host, int64_t nblocks) {
+  NOTNULL(c);
+  NOTNULL(host);
+  if (!c->stamps) return fail(MBX_E_INVALID, "diag_select_stamps: no stamped launch (select_dbg bit 3)");
+  if (nblocks < 0 || nblocks > kMaxStampBlocks) return fail(MBX_E_INVALID, "diag_select_stamps: %lld blocks",
+                                                            (long long)nblocks);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(host, c->stamps, sizeof(int64_t) * 4 * (size_t)nblocks, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   return MBX_OK;
 }
 

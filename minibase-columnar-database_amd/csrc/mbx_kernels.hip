@@ -292,7 +292,8 @@ __device__ __forceinline__ bool packed_arrive(uint64_t* w, uint64_t add, uint32_
   return true;
 }
 
-__device__ __forceinline__ void packed_count_finalize(uint32_t* ticket, int groups, int64_t count, int nan,
+// true for the final arriver of the launch
+__device__ __forceinline__ bool packed_count_finalize(uint32_t* ticket, int groups, int64_t count, int nan,
                                                       int64_t* count_out, int32_t* nan_out) {
   const uint32_t nb = gridDim.x;
   uint64_t add = pack_count(count, nan ? 1u : 0u), sum;
@@ -300,12 +301,12 @@ __device__ __forceinline__ void packed_count_finalize(uint32_t* ticket, int grou
     const uint32_t G = (uint32_t)groups;
     const uint32_t g = blockIdx.x % G;
     const uint32_t members = (nb - g + G - 1) / G;
-    if (!packed_arrive(reinterpret_cast<uint64_t*>(ticket + (1 + g) * kTicketStride), add, members, &sum)) return;
+    if (!packed_arrive(reinterpret_cast<uint64_t*>(ticket + (1 + g) * kTicketStride), add, members, &sum)) return false;
     const uint64_t nan_g = (sum >> kPackArrBits) & kPackNanMask;
     add = pack_count((int64_t)(sum >> (kPackArrBits + kPackNanBits)), nan_g ? 1u : 0u);
-    if (!packed_arrive(reinterpret_cast<uint64_t*>(ticket), add, G, &sum)) return;
+    if (!packed_arrive(reinterpret_cast<uint64_t*>(ticket), add, G, &sum)) return false;
   } else if (!packed_arrive(reinterpret_cast<uint64_t*>(ticket), add, nb, &sum)) {
-    return;
+    return false;
   }
   if (count_out) *count_out = (int64_t)(sum >> (kPackArrBits + kPackNanBits));
   if (nan_out) {  // [0] this launch, [1] sticky until mbx_sync reads it
@@ -313,6 +314,7 @@ __device__ __forceinline__ void packed_count_finalize(uint32_t* ticket, int grou
     nan_out[0] = nan_any;
     if (nan_any) nan_out[1] = 1;
   }
+  return true;
 }
 
 // Block-wide fixed-order reduction of per-thread accumulators into this
@@ -421,14 +423,35 @@ __device__ __forceinline__ uint64_t pack_word16(uint32_t nib, int lane) {
 
 // Positions of one step of 64 consecutive BitSet words (lane = word `base +
 // lane`, mw = its bits) to ids[off ...]; off advances by the step's count.
-// Sparse steps (2 * max popcount <= non-zero words): each lane peels its own
-// bits into the wave's LDS stage `st` (12-bit offsets within the step; at
-// most 2048 of them), then the wave copies them out with coalesced stores --
-// stored straight from the peel loop, one store instruction spreads over ~26
-// cache lines.  Dense steps: lane = bit, one coalesced store per non-zero
-// word.
-__device__ __forceinline__ void emit_step(int64_t base, uint64_t mw, int64_t& off, int64_t row_offset,
-                                          int64_t* __restrict__ ids, uint16_t* st, int lane) {
+// Steps of <= kStageIds positions go through the wave's LDS stage `st`
+// (12-bit offsets within the step) and are copied out with coalesced 512-byte
+// wave stores; the stage is filled by whichever loop is shorter -- each lane
+// peeling its own word's bits (iterations = the largest popcount) or the wave
+// visiting the non-zero words with lane = bit (iterations = non-zero words).
+// Denser steps store straight from the lane = bit loop: one store per
+// non-zero word, each with > 32 active lanes on average.  (A direct store per
+// non-zero word on moderately sparse steps made the slowest wave of a 10M-row
+// compaction 3.6x the median: profiles/r02/anatomy.)
+constexpr uint32_t kStageIds = 2048;
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int j) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// One step in two halves, so a caller can stage a step before it knows the
+// step's output offset: stage_step returns the step's count (uniform) and,
+// for <= kStageIds positions, leaves their 12-bit in-step offsets in `st`;
+// store_step writes them (or, for a denser step, stores straight from the
+// lane = bit loop) at ids[off ...].  cap: positions at or beyond it are not
+// stored (a caller buffer smaller than the selection; the count covers them).
+struct StepScan {
+  uint32_t excl;   // this lane's word's first slot within the step
+  uint32_t total;  // the step's positions (uniform)
+};
+
+__device__ __forceinline__ StepScan stage_step(uint64_t mw, uint16_t* st, int lane) {
   const uint32_t pc = (uint32_t)__popcll(mw);
   uint32_t incl = pc;
 #pragma unroll
@@ -436,36 +459,67 @@ __device__ __forceinline__ void emit_step(int64_t base, uint64_t mw, int64_t& of
     const uint32_t y = __shfl_up(incl, d);
     if (lane >= d) incl += y;
   }
-  const uint32_t excl = incl - pc;
-  const uint32_t total = __shfl(incl, 63);
+  StepScan r;
+  r.excl = incl - pc;
+  r.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  if (r.total == 0 || r.total > kStageIds) return r;
   uint64_t nz = __ballot(mw != 0ull);
   uint32_t maxpc = pc;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) maxpc = max(maxpc, (uint32_t)__shfl_xor(maxpc, m));
-  if (2 * maxpc <= (uint32_t)__popcll(nz)) {
+  if (maxpc <= (uint32_t)__popcll(nz)) {
     uint64_t m = mw;
-    uint32_t o = excl;
+    uint32_t o = r.excl;
     while (m) {
       st[o++] = (uint16_t)(lane * 64 + __builtin_ctzll(m));
       m &= m - 1ull;
     }
-    __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
-    const int64_t rbase = row_offset + base * 64;
-    for (uint32_t i = lane; i < total; i += 64) ids[off + i] = rbase + st[i];
-    __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next step
-    nz = 0;
-  }
-  while (nz) {
-    const int j = __builtin_ctzll(nz);
-    nz &= nz - 1ull;
-    const uint64_t m = __shfl(mw, j);
-    const uint32_t slot = __shfl(excl, j);
-    if ((m >> lane) & 1ull) {
-      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      ids[off + slot + below] = row_offset + (base + j) * 64 + lane;
+  } else {
+    while (nz) {
+      const int j = __builtin_ctzll(nz);
+      nz &= nz - 1ull;
+      const uint64_t m = readlane64(mw, j);
+      const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)r.excl, j);
+      if ((m >> lane) & 1ull) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        st[slot + below] = (uint16_t)(j * 64 + lane);
+      }
     }
   }
-  off += total;
+  __builtin_amdgcn_wave_barrier();  // LDS ops of one wave complete in order
+  return r;
+}
+
+__device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const StepScan& r, int64_t& off,
+                                           int64_t row_offset, int64_t* __restrict__ ids, const uint16_t* st,
+                                           int lane, int64_t cap) {
+  if (r.total == 0) return;
+  const int64_t rbase = row_offset + base * 64;
+  if (r.total <= kStageIds) {
+    for (uint32_t i = lane; i < r.total; i += 64)
+      if (off + i < cap) ids[off + i] = rbase + st[i];
+    __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next step
+  } else {
+    uint64_t nz = __ballot(mw != 0ull);
+    while (nz) {
+      const int j = __builtin_ctzll(nz);
+      nz &= nz - 1ull;
+      const uint64_t m = readlane64(mw, j);
+      const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)r.excl, j);
+      if ((m >> lane) & 1ull) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (off + slot + below < cap) ids[off + slot + below] = rbase + j * 64 + lane;
+      }
+    }
+  }
+  off += r.total;
+}
+
+__device__ __forceinline__ void emit_step(int64_t base, uint64_t mw, int64_t& off, int64_t row_offset,
+                                          int64_t* __restrict__ ids, uint16_t* st, int lane,
+                                          int64_t cap = INT64_MAX) {
+  const StepScan r = stage_step(mw, st, lane);
+  store_step(base, mw, r, off, row_offset, ids, st, lane, cap);
 }
 
 // ------------------------------------------------------------- fast scan
@@ -1114,7 +1168,12 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
                                                        int64_t words_per_block,
                                                        const Partial* __restrict__ seg_parts,
                                                        int64_t row_offset, int64_t* __restrict__ ids,
-                                                       int64_t* __restrict__ total) {
+                                                       int64_t* __restrict__ total, int32_t dbg,
+                                                       int64_t* __restrict__ stamps) {
+  // dbg (diagnostic A/B, mbx_set_tuning "select_dbg"): bit 0 skips the
+  // prefix loads, bit 1 the emission; stamps: per block wall_clock64() at
+  // start / words + prefix in / after the block barrier / end
+  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
   __shared__ int64_t wcount[kWaves];
   __shared__ int64_t wpre[kWaves];
   __shared__ uint16_t stage[kWaves][32 * 64];
@@ -1131,12 +1190,13 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   // this block's output offset: the segment counts before it, 4 loads in
   // flight per thread, issued before the word loads so both latencies overlap
   int64_t pre = 0;
-  for (int64_t i0 = 0; i0 < (int64_t)blockIdx.x; i0 += 4 * kBlock) {
+  const int64_t npre = (dbg & 1) ? 0 : (int64_t)blockIdx.x;
+  for (int64_t i0 = 0; i0 < npre; i0 += 4 * kBlock) {
     int64_t v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int64_t i = i0 + k * kBlock + threadIdx.x;
-      v[k] = i < (int64_t)blockIdx.x ? seg_parts[i].count : 0;
+      v[k] = i < npre ? seg_parts[i].count : 0;
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) pre += v[k];
@@ -1163,7 +1223,9 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
     wcount[wave] = c;
     wpre[wave] = pre;
   }
+  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 1] = wall_clock64();
   __syncthreads();
+  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
   for (int k = 0; k < kWaves; ++k) off += wpre[k];
   if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) {
@@ -1174,7 +1236,8 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   for (int k = 0; k < wave; ++k) off += wcount[k];
   // one step = 64 consecutive words, lane = word
   auto step = [&](int64_t base, uint64_t mw) { emit_step(base, mw, off, row_offset, ids, stage[wave], lane); };
-  if (cached) {
+  if (dbg & 2) {
+  } else if (cached) {
 #pragma unroll
     for (int r = 0; r < kSelRegs; ++r) {
       const int64_t base = a0 + r * 64;
@@ -1184,6 +1247,7 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   } else {
     for (int64_t base = a0; base < a1; base += 64) step(base, base + lane < a1 ? words[base + lane] : 0ull);
   }
+  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 3] = wall_clock64();
 }
 
 // Late materialisation (Heapfile.findRID + getRecord per output column,
@@ -1533,11 +1597,12 @@ hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t wo
 
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                               const Partial* seg_parts, int64_t row_offset, int64_t* ids, const ProjCol* proj,
-                              void* const* out, int32_t nproj, int64_t* total, hipStream_t s) {
+                              void* const* out, int32_t nproj, int64_t* total, hipStream_t s, int32_t dbg,
+                              int64_t* stamps) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   const int64_t g = (nwords + words_per_block - 1) / words_per_block;
   hipLaunchKernelGGL(k_select_ids, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
-                     seg_parts, row_offset, ids, total);
+                     seg_parts, row_offset, ids, total, dbg, stamps);
   if (nproj > 0) {
     MatArgs M;
     M.nproj = nproj;

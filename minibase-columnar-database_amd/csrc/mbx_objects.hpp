@@ -51,7 +51,10 @@ struct MbxTuning {
   int32_t fin_mode = -1;          // MBX_FIN_MODE (FinMode)
   int32_t join_plain = 0;         // MBX_JOIN_PLAIN: k_join_matrix instead of the fast form
   int32_t distinct_lds_probes = -1;  // MBX_DISTINCT_LDS_PROBES
+  int32_t select_dbg = 0;         // MBX_SELECT_DBG: diagnostic k_select_ids variants (bit 0 no prefix,
+                                  // bit 1 no emission: wrong output) and bit 3 per-block stamps
 };
+constexpr int64_t kMaxStampBlocks = 65536;
 
 struct mbx_ctx {
   int32_t device = 0;
@@ -65,6 +68,7 @@ struct mbx_ctx {
   uint32_t* ticket = nullptr;   // in-launch finalize ticket (always 0 between launches)
   int64_t* ids_scratch = nullptr;  // positions for a gather whose caller wants no positions
   int64_t ids_cap = 0;
+  int64_t* stamps = nullptr;    // diagnostic per-block stamps (select_dbg bit 3)
   void* pinned = nullptr;       // 256 bytes of pinned host scratch
   mbx_comm* comm = nullptr;     // multi-GPU exchange (mbx_comm.cpp), owned
   bool capturing = false;       // mbx_graph_begin .. mbx_graph_end

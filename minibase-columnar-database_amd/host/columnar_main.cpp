@@ -23,6 +23,7 @@
 // match the reference's, so a transcript can be diffed line by line.
 // Page-I/O counters (PCounter) do not exist here -- there is no buffer pool
 // on the GPU path; the driver prints the device time instead (stderr).
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <cstdio>
@@ -365,6 +366,26 @@ columnar::BitSetPtr scan_sel(columnar::Columnarfile& cf, const Cnf& cnf, size_t 
   return fs.selection();
 }
 
+// NljQuery.getIterator's COLUMNSCAN branch (R/input/NljQuery.java:245-270):
+// the columns of conjunct 0 as a TreeSet (colNums), its fields renumbered
+// into that tuple (findFieldOffset), out_indexes = the target columns; the
+// BitSet the ColumnarColumnsScan selects
+columnar::BitSetPtr columns_sel(columnar::Columnarfile& cf, const Cnf& cnf, const std::set<int>& target_cols) {
+  CondArray a = conds(cf, cnf, 0, 1, IndexType::None);
+  std::set<int> colset;
+  for (CondExpr* e = a.heads[0]; e; e = e->next) colset.insert(e->operand1.symbol.offset - 1);
+  const std::vector<int> colNums(colset.begin(), colset.end());
+  for (CondExpr* e = a.heads[0]; e; e = e->next) {
+    const int c = e->operand1.symbol.offset - 1;
+    e->operand1.symbol.offset = (int)(std::find(colNums.begin(), colNums.end(), c) - colNums.begin()) + 1;
+  }
+  std::vector<int> out_indexes(target_cols.begin(), target_cols.end());
+  std::vector<FldSpec> proj;
+  for (int c : out_indexes) proj.emplace_back(RelSpec(RelSpec::outer), c + 1);
+  iterator::ColumnarColumnsScan cs(&cf, colNums, (int)out_indexes.size(), out_indexes, proj, a.heads.data());
+  return cs.selection();
+}
+
 // the BitSet a ColumnarIndexScan over conjuncts [from, to) returns
 columnar::BitSetPtr index_sel(columnar::Columnarfile& cf, const Cnf& cnf, size_t from, size_t to, int index_type) {
   CondArray a = conds(cf, cnf, from, to, index_type);
@@ -585,18 +606,19 @@ void nlj_cmd(const std::vector<std::string>& a) {
     }
   // access path selection + pending filter (getIterator, NljQuery.java:232-300;
   // fillOuterBuffer / fillInnerBuffer, ColumnarNestedLoopJoins.java:120-158)
-  auto select = [](columnar::Columnarfile& F, const Cnf& cnf, const std::string& acc, columnar::BitSetPtr* it) {
+  auto select = [](columnar::Columnarfile& F, const Cnf& cnf, const std::string& acc, const std::set<int>& targets,
+                   columnar::BitSetPtr* it) {
     if (acc == "FILESCAN") {
       *it = scan_sel(F, cnf, 0, cnf.size());
       return *it;
     }
-    *it = acc == "COLUMNSCAN" ? scan_sel(F, cnf, 0, 1)
+    *it = acc == "COLUMNSCAN" ? columns_sel(F, cnf, targets)
                               : index_sel(F, cnf, 0, 1, acc == "BTREE" ? IndexType::B_Index : IndexType::Bitmap);
     return cnf.size() > 1 ? and_sel(*it, scan_sel(F, cnf, 1, cnf.size())) : *it;
   };
   columnar::BitSetPtr o_iter, i_iter;
-  columnar::BitSetPtr osel = select(O, oc, OA, &o_iter);
-  columnar::BitSetPtr isel = select(I, ic, IA, &i_iter);
+  columnar::BitSetPtr osel = select(O, oc, OA, tg.outer, &o_iter);
+  columnar::BitSetPtr isel = select(I, ic, IA, tg.inner, &i_iter);
   // the outer iterator's tuple (Tuple.setHdr over the TreeSet of outer
   // target columns) sizes the outer block (ColumnarNestedLoopJoins.java:122)
   int tsize = ((int)tg.outer.size() + 2) * 2;
@@ -614,6 +636,41 @@ void nlj_cmd(const std::vector<std::string>& a) {
             << "Total Outer Tuples By Iterator: " << o_iter->cardinality() << "\n"
             << "************************************************************************\n\n";
   print_results_footer(n);
+}
+
+// Test hook (no reference command): drives iterator::ColumnarColumnsScan
+// directly, as NljQuery does (R/input/NljQuery.java:269).
+//   columnsscan DB CF [COLNOS] CNF [OUTCOLS] [tid]
+// COLNOS (column names, in the given order) make the scan's tuple; CNF terms
+// name columns of it ({(C,=,6)|(A,>=,M)}^{...}); get_next prints OUTCOLS rows,
+// `tid` prints get_next_tid positions instead.
+void columnsscan_cmd(const std::vector<std::string>& a) {
+  if (a.size() < 6) throw std::runtime_error("Invalid number of attributes.");
+  columnar::Columnarfile cf = open_cf(a[1], a[2]);
+  Target cols = targets(cf, a[3]);
+  Target out = targets(cf, a[5]);
+  const Cnf cnf = parse_cnf(a[4]);
+  CondArray c = conds(cf, cnf, 0, cnf.size(), IndexType::None);
+  for (size_t k = 0; k + 1 < c.heads.size(); k++)
+    for (CondExpr* e = c.heads[k]; e; e = e->next) {
+      const int col = e->operand1.symbol.offset - 1;
+      const auto it = std::find(cols.out_indexes.begin(), cols.out_indexes.end(), col);
+      e->operand1.symbol.offset = it == cols.out_indexes.end() ? 0 : (int)(it - cols.out_indexes.begin()) + 1;
+    }
+  iterator::ColumnarColumnsScan cs(&cf, cols.out_indexes, (int)out.out_indexes.size(), out.out_indexes, out.proj,
+                                   c.heads.data());
+  if (a.size() > 6 && a[6] == "tid") {
+    int64_t n = 0;
+    std::cout << "positions\n";
+    for (global::TID t = cs.get_next_tid(); t.position >= 0; t = cs.get_next_tid()) {
+      std::cout << t.position << "\n";
+      n++;
+    }
+    cs.close();
+    print_results_footer(n);
+    return;
+  }
+  print_rows(cs, cf, out);
 }
 
 void bmj_cmd(const std::vector<std::string>& a) {
@@ -655,6 +712,7 @@ int run() {
       else if (a[0] == "nlj") nlj_cmd(a);
       else if (a[0] == "delete_query") delete_query(a);
       else if (a[0] == "bmj") bmj_cmd(a);
+      else if (a[0] == "columnsscan") columnsscan_cmd(a);
       else if (a[0] == "exit") break;
       else std::cout << "Command not supported by the GPU executor: " << a[0] << "\n";
     } catch (const std::exception& e) {

@@ -717,6 +717,91 @@ ColumnarColumnScan::ColumnarColumnScan(columnar::Columnarfile* cf, int colNo, in
                                     outFilter ? heads.data() : nullptr));
 }
 
+ColumnarColumnsScan::ColumnarColumnsScan(columnar::Columnarfile* cf, const std::vector<int>& colNos, int n_out_flds,
+                                         const std::vector<int>& out_indexes, const std::vector<FldSpec>& proj_list,
+                                         CondExpr* const* outFilter) {
+  // TupleUtils.setup_op_tuple over the file's schema and proj_list (:57-60)
+  setup_jtuple(Jtuple_, cf->getAttributeTypes(), cf->getStringSizes(), proj_list);
+  has_proj_ = true;
+  init(cf, colNos, n_out_flds, out_indexes, outFilter);
+}
+
+ColumnarColumnsScan::ColumnarColumnsScan(columnar::Columnarfile* cf, const std::vector<int>& colNos,
+                                         CondExpr* const* outFilter) {
+  init(cf, colNos, 0, {}, outFilter);
+}
+
+void ColumnarColumnsScan::init(columnar::Columnarfile* cf, const std::vector<int>& colNos, int n_out_flds,
+                               const std::vector<int>& out_indexes, CondExpr* const* outFilter) {
+  const auto types = cf->getAttributeTypes();
+  const int ncols = cf->getFieldCount();
+  colNos_ = colNos;
+  // destType / dest_s_sizes (:68-82), including its index quirk
+  size_t nstr = 0;
+  for (int c : colNos) {
+    if (c < 0 || c >= ncols) throw ArrayIndexOutOfBoundsException(std::to_string(c));
+    if (types[(size_t)c].attrType == AttrType::attrString) nstr++;
+  }
+  for (size_t i = 0; i < colNos.size(); i++)
+    if (types[(size_t)colNos[i]].attrType == AttrType::attrString && i >= nstr)
+      throw ArrayIndexOutOfBoundsException("Index " + std::to_string(i) + " out of bounds for length " +
+                                           std::to_string(nstr));
+  if ((int)out_indexes.size() < n_out_flds) throw FileScanException("ColumnarColumnsScan: out_indexes");
+  for (int i = 0; i < n_out_flds; i++)
+    if (out_indexes[(size_t)i] < 0 || out_indexes[(size_t)i] >= ncols)
+      throw ArrayIndexOutOfBoundsException(std::to_string(out_indexes[(size_t)i]));
+  // CondExpr fields address the colNos tuple (tuple1, :86): field k -> file
+  // column colNos[k-1]; a field outside it is Tuple's FieldNumberOutOfBound
+  std::vector<std::vector<CondExpr>> copies;
+  for (int i = 0; outFilter && outFilter[i]; i++) {
+    std::vector<CondExpr> chain;
+    for (const CondExpr* e = outFilter[i]; e; e = e->next) chain.push_back(*e);
+    copies.push_back(chain);
+  }
+  auto remap = [&](const AttrType& t, Operand& o) {
+    if (t.attrType != AttrType::attrSymbol) return;
+    if (o.symbol.offset < 1 || o.symbol.offset > (int)colNos.size())
+      throw FieldNumberOutOfBoundException("ColumnarColumnsScan: field " + std::to_string(o.symbol.offset));
+    o.symbol.offset = colNos[(size_t)o.symbol.offset - 1] + 1;
+  };
+  std::vector<CondExpr*> heads;
+  for (auto& chain : copies) {
+    for (size_t k = 0; k < chain.size(); k++) {
+      remap(chain[k].type1, chain[k].operand1);
+      remap(chain[k].type2, chain[k].operand2);
+      chain[k].next = k + 1 < chain.size() ? &chain[k + 1] : nullptr;
+    }
+    heads.push_back(chain.empty() ? nullptr : &chain[0]);
+  }
+  heads.push_back(nullptr);
+  std::vector<FldSpec> proj;
+  for (int i = 0; i < n_out_flds; i++) proj.push_back(FldSpec(RelSpec(RelSpec::outer), out_indexes[(size_t)i] + 1));
+  inner_.reset(new ColumnarFileScan(cf->get_fileName(), types, cf->getStringSizes(), (short)ncols, n_out_flds, proj,
+                                    outFilter ? heads.data() : nullptr));
+}
+
+heap::Tuple* ColumnarColumnsScan::get_next() {
+  if (!has_proj_) throw FileScanException("ColumnarColumnsScan: get_next without a projection (delete-query form)");
+  return inner_->get_next();
+}
+
+global::TID ColumnarColumnsScan::get_next_tid() {
+  global::TID tid = inner_->get_next_tid();
+  // findPosition on colNos[0]'s heapfile with the last column's RID (:219)
+  if (tid.position >= 0 && colNos_.size() > 1 && colNos_.front() != colNos_.back())
+    throw JavaException("Invalid RID");
+  return tid;
+}
+
+void ColumnarColumnsScan::close() {
+  if (!closeFlag) {
+    inner_->close();
+    closeFlag = true;
+  }
+}
+void ColumnarColumnsScan::restart() { inner_->restart(); }
+int ColumnarColumnsScan::getTupleSize() { return has_proj_ ? Jtuple_.size() : inner_->getTupleSize(); }
+
 heap::Tuple* ColumnarColumnScan::get_next() { return inner_->get_next(); }
 global::TID ColumnarColumnScan::get_next_tid() { return inner_->get_next_tid(); }
 void ColumnarColumnScan::close() {

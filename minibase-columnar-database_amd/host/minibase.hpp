@@ -124,6 +124,14 @@ class FieldNumberOutOfBoundException : public chainexception::ChainException {
 class InvalidRelation : public chainexception::ChainException {
   using ChainException::ChainException;
 };
+// java.lang.ArrayIndexOutOfBoundsException (unchecked, not a ChainException)
+class ArrayIndexOutOfBoundsException : public std::out_of_range {
+  using std::out_of_range::out_of_range;
+};
+// a plain java.lang.Exception (e.g. Heapfile.findPosition's "Invalid RID")
+class JavaException : public std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
 
 struct RelSpec {  // R/iterator/RelSpec.java
   enum { outer = 0, innerRel = 1 };
@@ -267,6 +275,45 @@ class ColumnarFileScan : public Iterator {
   std::vector<std::vector<uint8_t>> batch_;
   std::vector<int64_t> batch_ids_;
   int64_t batch_n_ = 0, batch_i_ = 0;
+};
+
+// R/iterator/ColumnarColumnsScan.java:39-257: a CNF over the tuple of the
+// columns colNos (CondExpr field i = colNos[i-1]), one ColumnScan per column
+// in lockstep (deleted positions skipped), late-materialised out_indexes.
+// Reference behaviour kept (drop-in):
+//  * the constructor's dest_s_sizes loop indexes an array sized by the number
+//    of string columns with the column's position (:77-82): a string column
+//    at position >= that count throws ArrayIndexOutOfBoundsException, i.e.
+//    only colNos whose string columns come first construct (NljQuery's
+//    TreeSet order over a schema with its strings first, R/input/NljQuery.java:245-268);
+//  * get_next_tid (:205-224) asks the heapfile of colNos[0] for the position
+//    of the RID the LAST column's scan returned: for colNos[0] != colNos[last]
+//    that page is not in the file and findPosition throws "Invalid RID"
+//    (R/heap/Heapfile.java:262-273) at the first selected row;
+//  * Jtuple's types come from proj_list, its values from out_indexes (:57-60,
+//    :191-199).
+// Predicate, deleted skip and projection run on the GPU like ColumnarFileScan.
+class ColumnarColumnsScan : public Iterator {
+ public:
+  ColumnarColumnsScan(columnar::Columnarfile* cf, const std::vector<int>& colNos, int n_out_flds,
+                      const std::vector<int>& out_indexes, const std::vector<FldSpec>& proj_list,
+                      CondExpr* const* outFilter);
+  // the delete-query form (:103-154): no projection, get_next_tid only
+  ColumnarColumnsScan(columnar::Columnarfile* cf, const std::vector<int>& colNos, CondExpr* const* outFilter);
+  heap::Tuple* get_next() override;
+  global::TID get_next_tid();
+  void close() override;
+  void restart() override;
+  int getTupleSize() override;
+  columnar::BitSetPtr selection() const { return inner_->selection(); }
+
+ private:
+  void init(columnar::Columnarfile* cf, const std::vector<int>& colNos, int n_out_flds,
+            const std::vector<int>& out_indexes, CondExpr* const* outFilter);
+  std::vector<int> colNos_;
+  std::unique_ptr<ColumnarFileScan> inner_;
+  heap::Tuple Jtuple_;  // typed by proj_list (getTupleSize)
+  bool has_proj_ = false;
 };
 
 // R/iterator/ColumnarColumnScan.java:39-88: predicate on one column (field 1

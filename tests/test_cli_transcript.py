@@ -179,3 +179,31 @@ def test_delete_query_md_and_pd(tmp_path):
     assert n3 == 500 - len(gone)
     assert r3 == [f"{a}, {b}, {c}, {d}" for i, (a, b, c, d) in enumerate(rows) if i not in gone]
     assert n4 == 500 - len(gone)
+
+
+def test_columns_scan_mirror_matches_oracle():
+    """iterator::ColumnarColumnsScan (R/iterator/ColumnarColumnsScan.java), the
+    outer/inner iterator NljQuery builds for COLUMNSCAN (NljQuery.java:269),
+    driven directly: rows and positions vs the oracle over minidata, and the
+    reference's two quirks -- a string column past the string prefix of
+    colNos throws ArrayIndexOutOfBounds (:77-82), get_next_tid over columns
+    whose first and last differ throws "Invalid RID" at the first match (:219)."""
+    rows = helpers.load_minidata()
+    t = oracle.Table(helpers.minidata_columns(rows))
+    cnf_s = "{(C,=,6)|(A,>=,South_Dakota)}^{(D,!=,3)}"
+    cnf = helpers.parse_cnf_string(cnf_s)
+    n_o, _, ids_o = oracle.filescan(t, cnf)
+    out = run_session([f"columnsscan db cf [A,C,D] {cnf_s} [A,B,C,D]",
+                       f"columnsscan db cf [A,D,C] {cnf_s} [D,A]",
+                       "columnsscan db cf [C] {(C,=,6)} [C] tid",
+                       f"columnsscan db cf [C,A,D] {cnf_s} [A]",
+                       f"columnsscan db cf [A,C,D] {cnf_s} [A] tid"])
+    chunks = out.split("> ")[1:][5:]  # after batchinsert + 4 index commands
+    (h1, r1, n1), (h2, r2, n2), (h3, r3, n3) = blocks("> " + "> ".join(chunks[:3]))
+    assert n1 == n_o and h1 == "A, B, C, D"
+    assert r1 == [", ".join(str(x) for x in rows[p]) for p in ids_o]
+    assert h2 == "D, A" and r2 == [f"{rows[p][3]}, {rows[p][0]}" for p in ids_o] and n2 == n_o
+    six = [i for i, r in enumerate(rows) if r[2] == 6]
+    assert n3 == len(six) and r3 == [str(p) for p in six]
+    assert "java.lang.Exception" in chunks[3] and "out of bounds" in chunks[3]
+    assert "java.lang.Exception: Invalid RID" in chunks[4]

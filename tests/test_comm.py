@@ -72,14 +72,16 @@ def test_one_rank_rccl_combine_is_exact(m, torch_cuda, init):
             (comm,) = m.mbx.comm_init_all([ctx])
         want = ctx.scan_count(plan)
         buf = torch.zeros(4, dtype=torch.int64, device="cuda")
+        allc = torch.zeros(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()  # torch's zero fills run on its own stream, not the library's
         ctx.scan_count_async(plan, buf.data_ptr())
         comm.allreduce_count_async(buf.data_ptr(), 1)
-        allc = torch.zeros(1, dtype=torch.int64, device="cuda")
         comm.allgather_count_async(buf.data_ptr(), allc.data_ptr())
         ctx.sync()
         assert int(buf[0]) == want and int(allc[0]) == want
         for col in (0, 1):
             rec = torch.zeros(6, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
             ctx.scan_aggregate_async(plan, col, rec.data_ptr())
             ctx.sync()
             local = rec.cpu().numpy().copy()

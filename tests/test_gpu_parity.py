@@ -155,6 +155,20 @@ def test_c2_range_filter_full_size(ctx, generic, tune):
     assert bm.count == n_o
     assert np.array_equal(words, w_o)
     assert np.array_equal(ctx.select(bm), ids_o)
+    # the C2 query proper: mbx_scan_select_async, launch after launch
+    import torch
+    plan = ctx.compile(t, cnf)
+    bm2 = ctx.bitmap_alloc(n)
+    dev_ids = torch.zeros(n, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        dev_ids.zero_()
+        torch.cuda.synchronize()  # torch's stream is not the library stream
+        ctx.scan_select_async(plan, bm2, dev_ids.data_ptr(), cnt.data_ptr())
+        ctx.sync()
+        assert int(cnt.item()) == n_o
+        assert np.array_equal(dev_ids[:n_o].cpu().numpy(), ids_o)
+        assert np.array_equal(bm2.download(), w_o)
 
 
 def test_c3_conjunction_count_full_size(ctx):
@@ -238,9 +252,9 @@ def test_scan_select_positions(ctx, n):
         assert np.array_equal(ctx.scan_select(plan), ids_o + 640)
 
 
-@pytest.mark.parametrize("tpb", [4, 37, 200, 512, 513, 1000])
+@pytest.mark.parametrize("tpb", [1, 4, 37, 200, 512, 513, 1000, 1025])
 def test_scan_select_segment_sizes(ctx, tpb, tune):
-    """Segments of 16..4000 words; positions and the BitSet left in the
+    """Segments of 4..4100 words; positions and the BitSet left in the
     bitmap both exact, also through the async entry point."""
     tune("tiles_per_block", tpb)
     n = 3_000_017
@@ -254,6 +268,7 @@ def test_scan_select_segment_sizes(ctx, tpb, tune):
     bm = ctx.bitmap_alloc(n)
     dev_ids = torch.zeros(n, dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # the zero fills run on torch's stream, not the library's
     ctx.scan_select_async(plan, bm, dev_ids.data_ptr(), cnt.data_ptr())
     ctx.sync()
     k = int(cnt.item())
@@ -267,15 +282,37 @@ def test_scan_select_segment_sizes(ctx, tpb, tune):
 
 @pytest.mark.parametrize("generic", [False, True])
 def test_scan_select_strings_and_floats(ctx, generic, tune):
-    """String-slot (KS > 0) and float plans, fast and generic kernels."""
+    """String-slot (KS > 0) and float plans, fast and generic kernels, with
+    and without deleted rows."""
     if generic:
         tune("force_generic", 1)
     cols, _ = mixed_table(200_003, seed=11)
+    dm = helpers.random_deleted(200_003, 0.03)
     ot, t = oracle.Table(cols), ctx.stage(cols)
-    cnf = [[(oracle.GE, ("sym", 3), ("str", "M"))], [(oracle.LT, ("sym", 2), ("real", 0.5)),
-                                                      (oracle.LT, ("sym", 1), ("int", 1000))]]
-    n_o, w_o, ids_o = oracle.filescan(ot, cnf)
-    assert np.array_equal(ctx.scan_select(ctx.compile(t, cnf)), ids_o)
+    otd, td = oracle.Table(cols, dm), ctx.stage(cols, dm)
+    cnfs = [[[(oracle.GE, ("sym", 3), ("str", "M"))], [(oracle.LT, ("sym", 2), ("real", 0.5)),
+                                                       (oracle.LT, ("sym", 1), ("int", 1000))]],
+            [[(oracle.GE, ("sym", 3), ("str", "M"))]],                                    # KS=1, K=0
+            [[(oracle.LT, ("sym", 3), ("str", "K"))], [(oracle.GT, ("sym", 2), ("real", 0.3))]],  # KS=1, K=1
+            [[(oracle.LT, ("sym", 2), ("real", 0.25))]]]                                  # K=1 float
+    for cnf in cnfs:
+        for o, g in ((ot, t), (otd, td)):
+            n_o, w_o, ids_o = oracle.filescan(o, cnf)
+            assert np.array_equal(ctx.scan_select(ctx.compile(g, cnf)), ids_o), cnf
+
+
+def test_scan_select_capacity(ctx, m):
+    """host capacity: exactly the count works, one less raises MBX_E_INVALID
+    (the device scratch is sized to the count, per call)."""
+    cols, _ = int_table(100_000, hi=100)
+    t = ctx.stage(cols)
+    plan = ctx.compile(t, [[(oracle.LT, ("sym", 1), ("int", 10))]])
+    want = np.nonzero(cols[0][2] < 10)[0]
+    assert np.array_equal(ctx.scan_select(plan, cap=len(want)), want)
+    with pytest.raises(m.MbxError) as e:
+        ctx.scan_select(plan, cap=len(want) - 1)
+    assert e.value.code == m.mbx.E_INVALID
+    assert np.array_equal(ctx.scan_select(plan, cap=len(want) + 5), want)
 
 
 @pytest.mark.parametrize("op", [oracle.EQ, oracle.LT, oracle.GT, oracle.NE, oracle.LE, oracle.GE, oracle.NOT,

@@ -138,13 +138,13 @@ def ctx(m):
 
 
 def _gpu_outcomes(m, ctx, t, cnf, agg_col):
-    """(count, words) / 'raise' through scan_count, scan_bitmap and the
-    aggregate of agg_col; all three must agree."""
+    """(count, words) / 'raise' through scan_count, scan_bitmap, the
+    aggregate of agg_col and scan_select (positions); all must agree."""
     try:
         plan = ctx.compile(t, cnf)
     except m.MbxError as e:
         assert e.code == m.mbx.E_TYPE
-        return "raise", "raise", "raise"
+        return "raise", "raise", "raise", "raise"
     out = []
     try:
         out.append(ctx.scan_count(plan))
@@ -162,19 +162,26 @@ def _gpu_outcomes(m, ctx, t, cnf, agg_col):
     except m.MbxError as e:
         assert e.code == m.mbx.E_TYPE
         out.append("raise")
+    try:
+        out.append(ctx.scan_select(plan))
+    except m.MbxError as e:
+        assert e.code == m.mbx.E_TYPE
+        out.append("raise")
     return out
 
 
 def _check(m, ctx, ot, t, cnf, agg_col=1):
     want = oracle_count(ot, cnf)
     want_agg = oracle_agg(ot, cnf, agg_col)
-    got_count, got_bm, got_agg = _gpu_outcomes(m, ctx, t, cnf, agg_col)
+    got_count, got_bm, got_agg, got_ids = _gpu_outcomes(m, ctx, t, cnf, agg_col)
     if want == "raise":
+        assert isinstance(got_ids, str) and got_ids == "raise", cnf
         assert got_count == got_bm == got_agg == "raise", cnf
         assert want_agg == "raise"
         return True
-    n_o, w_o, _ = want
+    n_o, w_o, ids_o = want
     assert got_count == n_o, cnf
+    assert not isinstance(got_ids, str) and np.array_equal(got_ids, ids_o), cnf
     assert got_bm != "raise" and got_bm[0] == n_o and np.array_equal(got_bm[1], w_o), cnf
     assert got_agg != "raise" and got_agg["count"] == want_agg["count"], cnf
     if want_agg["count"]:
@@ -256,6 +263,7 @@ def test_gpu_nan_async_surfaces_at_sync(m, ctx):
     ok = ctx.compile(t, CASES[0][1])
     bad = ctx.compile(t, CASES[1][1])
     out = torch.zeros(8, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # torch's stream is not the library stream
     ctx.sync()
     ctx.scan_count_async(ok, out.data_ptr())
     ctx.sync()  # no NaN reached
@@ -266,6 +274,7 @@ def test_gpu_nan_async_surfaces_at_sync(m, ctx):
     assert e.value.code == m.mbx.E_TYPE
     ctx.sync()  # reported once
     agg = torch.zeros(8, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
     ctx.scan_aggregate_async(bad, 1, agg.data_ptr())
     with pytest.raises(m.MbxError):
         ctx.sync()

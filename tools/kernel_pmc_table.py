@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
 """Per-kernel table from rocprofv3 CSV output: dispatches, average / median
 duration (kernel trace), median HBM read / write bytes per dispatch (PMC
-FETCH_SIZE x 2 x 1024 -- the gfx950 correction, MI355X_MICROARCH.md -- and
-WRITE_SIZE x 1024).  usage: kernel_pmc_table.py DIR [DIR...]"""
+FETCH_SIZE x 2 x 1024 and WRITE_SIZE x 1024), plus any other counter.
+
+FETCH_SIZE x 2: MI355X_MICROARCH.md states the gfx950 correction for wide
+streaming reads only; round 2 calibrated it for the random 4-byte gathers of
+k_gather too (profiles/r02/anatomy/gather_line_calibration.jsonl: BitSets with
+one row per 128-B line, per 2nd / 4th line, two per line, and C4's random 1 %):
+TCC_EA0_RDREQ = 1.000 x the 128-B lines touched, TCC_EA0_RDREQ_32B = 0, and
+FETCH_SIZE x 2 = the touched lines x 128 B within 0.1 % -- every request is one
+whole 128-B line tallied as 64 B, whatever the access width.
+usage: kernel_pmc_table.py DIR [DIR...]"""
 import collections
 import csv
 import glob
