@@ -1,0 +1,35 @@
+package global;
+
+/**
+ * The per-JVM GPU context(s), next to SystemDefs (R/global/SystemDefs.java:6-9):
+ * one mbx_ctx per GPU, created on first use.  The engine is single threaded;
+ * so is this class's contract.
+ */
+public final class GpuContext {
+  private static long[] ctxs;
+
+  private GpuContext() {}
+
+  /** the context of GPU 0 (every single-GPU operator) */
+  public static synchronized long ctx() throws Exception {
+    return ctx(0);
+  }
+
+  public static synchronized long ctx(int device) throws Exception {
+    if (ctxs == null) ctxs = new long[Math.max(1, Native.deviceCount())];
+    if (device < 0 || device >= ctxs.length) throw new IllegalArgumentException("GPU " + device);
+    if (ctxs[device] == 0) ctxs[device] = Native.init(device);
+    return ctxs[device];
+  }
+
+  public static synchronized int devices() {
+    return Math.max(1, Native.deviceCount());
+  }
+
+  /** releases every context (SystemDefs shutdown) */
+  public static synchronized void shutdown() {
+    if (ctxs == null) return;
+    for (long c : ctxs) if (c != 0) Native.free(c);
+    ctxs = null;
+  }
+}

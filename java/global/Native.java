@@ -1,0 +1,82 @@
+package global;
+
+import java.nio.ByteBuffer;
+
+import iterator.CondExpr;
+
+/**
+ * The MI355X executor's C-ABI (include/mbx.h, include/mbx_db.h) as seen from
+ * the engine: jni/mbx_jni.c implements every method.  Handles are the C-ABI's
+ * opaque pointers.  Errors arrive as the reference's checked exceptions
+ * (PredEvalException, FileScanException, IndexException,
+ * heap.FieldNumberOutOfBoundException, ChainException) carrying
+ * mbx_last_error().  Not compiled in this image (no JDK): see jni/Makefile.
+ */
+public final class Native {
+  static { System.loadLibrary("mbx_jni"); }          // libmbx_jni.so -> libmbx.so
+
+  private Native() {}
+
+  public static final int BM_AND = 0, BM_OR = 1, BM_ANDNOT = 2;   // MBX_BM_*
+  public static final int AGG_RECORD_BYTES = 48;                   // sizeof(mbx_agg)
+
+  // context: one per GPU (SystemDefs' singletons, R/global/SystemDefs.java:6-9)
+  public static native int deviceCount();
+  public static native long init(int device) throws Exception;
+  public static native void free(long ctx);
+  public static native void sync(long ctx) throws Exception;
+
+  // tables: the HBM image of a Columnarfile
+  public static native long tableStage(long ctx, int[] attrTypes, short[] sizes, long nrows, ByteBuffer[] cols,
+                                       long[] deleted, long rowOffset) throws Exception;
+  public static native void tableFree(long table);
+  /** positions of the staged table (the bits of its BitSets) */
+  public static native long tableRows(long table) throws Exception;
+  public static native long dbOpen(String path) throws Exception;
+  public static native void dbClose(long db);
+  public static native long dbStage(long ctx, long db, String columnarFile) throws Exception;
+  public static native long dbBitmapStage(long ctx, long db, String bitMapFile, long nbits) throws Exception;
+
+  // PredEval over a table (R/iterator/PredEval.java:25-183)
+  public static native long planCompile(long ctx, long table, CondExpr[] filter) throws Exception;
+  public static native void planFree(long plan);
+  public static native long scanCount(long ctx, long plan) throws Exception;
+  public static native long scanBitmap(long ctx, long plan) throws Exception;
+  public static native long[] scanSelect(long ctx, long plan, long cap) throws Exception;
+  /** {count, aggType, isum, imin, imax, doubleBits(fsum), floatBits(fmin), floatBits(fmax)} */
+  public static native long[] scanAggregate(long ctx, long plan, int col) throws Exception;
+  public static native void scanCountAsync(long ctx, long plan, long devCount) throws Exception;
+  public static native void scanAggregateAsync(long ctx, long plan, int col, long devRec) throws Exception;
+
+  // device BitSets (java.util.BitSet long[] images)
+  public static native long bitmapUpload(long ctx, long nbits, long[] words) throws Exception;
+  public static native long[] bitmapDownload(long ctx, long bitmap) throws Exception;
+  public static native long bitmapCardinality(long bitmap) throws Exception;
+  public static native long bitmapCnf(long ctx, long nbits, long[] bitmaps, int[] conjOffsets, long deleted)
+      throws Exception;
+  public static native long bitmapCombine(long ctx, int op, long a, long b) throws Exception;
+  public static native void bitmapFree(long bitmap);
+
+  // late materialisation in batches (Iterator.get_next)
+  public static native long cursorOpen(long ctx, long table, long selection, int[] proj) throws Exception;
+  public static native long cursorCount(long cursor) throws Exception;
+  /** {long[] positions, Object[] columns (int[] / float[] / String[])}, or null at the end */
+  public static native Object[] cursorNext(long cursor, int maxRows, int[] types, short[] sizes) throws Exception;
+  public static native void cursorRestart(long cursor) throws Exception;
+  public static native void cursorClose(long cursor);
+
+  // device result slots + the multi-GPU exchange (RCCL over xGMI)
+  public static native long devAlloc(long ctx, long bytes) throws Exception;
+  public static native void devFree(long ctx, long dev);
+  public static native long countDownload(long ctx, long devCount) throws Exception;
+  public static native long[] aggDownload(long ctx, long devRec) throws Exception;
+  public static native long[] shardBounds(long nrows, int nshards, int shard) throws Exception;
+  public static native byte[] commUniqueId() throws Exception;
+  public static native long commInitRank(long ctx, int nranks, int rank, byte[] id) throws Exception;
+  public static native long[] commInitAll(long[] ctxs) throws Exception;
+  public static native void commFree(long comm);
+  public static native void commAllreduceCount(long comm, long devCount) throws Exception;
+  public static native void commAllreduceAgg(long comm, long devRec) throws Exception;
+  public static native void commAllreduceCountAll(long[] comms, long[] devCounts) throws Exception;
+  public static native void commAllreduceAggAll(long[] comms, long[] devRecs) throws Exception;
+}

@@ -1,0 +1,167 @@
+package index;
+
+import java.util.ArrayList;
+import java.util.BitSet;
+import java.util.HashSet;
+import java.util.List;
+import java.util.Set;
+
+import columnar.Columnarfile;
+import columnar.GpuTables;
+import global.AttrType;
+import global.GpuContext;
+import global.IndexType;
+import global.Native;
+import heap.Tuple;
+import iterator.CondExpr;
+import iterator.FldSpec;
+import iterator.Iterator;
+import iterator.TupleUtils;
+
+/**
+ * Drop-in for ColumnarIndexScan (R/index/ColumnarIndexScan.java:79-330): same
+ * constructor, getOutputPositions(), get_next() in nextSetBit order.
+ * Bitmap-index CNFs run as ONE k_bitmap_cnf launch over the value BitSets of
+ * every term (OR within a conjunct, AND across, AND NOT cf.md).  Two cases
+ * keep the reference's own ColumnarIndexScan for the positions, so its
+ * results stay identical: a B-tree term (B-tree access is out of scope for
+ * the GPU path) and a repeated identical constraint (its duplicateConstraints
+ * cache ORs in a BitSet that a later AND mutates, :147-172).  Either way the
+ * projection of out_indexes is materialised on the GPU.
+ */
+public class GpuColumnarIndexScan extends Iterator {
+  private final long ctx, table;
+  private long output, cursor;
+  private final Tuple Jtuple = new Tuple();
+  private final AttrType[] outTypes;
+  private final int[] outIdx, projTypes;
+  private final short[] projSizes;
+  private final boolean fused;
+  private long[] ids;
+  private Object[] batch;
+  private int n, i;
+
+  public GpuColumnarIndexScan(Columnarfile columnarFile, final int[] fldNums, IndexType[] indexTypes,
+                              final String[] indNames, AttrType[] types, short[] str_sizes, int noInFlds,
+                              int noOutFlds, int[] out_indexes, FldSpec[] outFlds, CondExpr[] selects,
+                              final boolean indexOnly) throws Exception {
+    outTypes = new AttrType[noOutFlds];
+    TupleUtils.setup_op_tuple(Jtuple, outTypes, types, noInFlds, str_sizes, outFlds, noOutFlds);
+    ctx = GpuContext.ctx();
+    table = GpuTables.get(columnarFile.get_fileName());
+    final long nbits = tableRows(table);
+    outIdx = out_indexes == null ? new int[0] : out_indexes.clone();
+    projTypes = new int[outIdx.length];
+    projSizes = new short[outIdx.length];
+    for (int k = 0; k < outIdx.length; k++) {
+      projTypes[k] = columnarFile.getAttributeType(outIdx[k]).attrType;
+      projSizes[k] = projTypes[k] == AttrType.attrString ? columnarFile.getAttrSizes()[outIdx[k]] : 4;
+    }
+    fused = bitmapOnlyWithoutRepeats(columnarFile, selects);
+    if (fused) {
+      List<Long> bms = new ArrayList<>();
+      List<Integer> offs = new ArrayList<>();
+      offs.add(0);
+      for (int c = 0; selects[c] != null; c++) {
+        for (CondExpr e = selects[c]; e != null; e = e.next)
+          bms.addAll(GpuBitmapValues.of(columnarFile, fieldOf(e) - 1, e, nbits));
+        offs.add(bms.size());
+      }
+      long[] h = new long[bms.size()];
+      for (int k = 0; k < h.length; k++) h[k] = bms.get(k);
+      int[] o = new int[offs.size()];
+      for (int k = 0; k < o.length; k++) o[k] = offs.get(k);
+      long deleted = Native.bitmapUpload(ctx, nbits, columnarFile.getMarkedDeleted().getBitSet().toLongArray());
+      try {
+        output = Native.bitmapCnf(ctx, nbits, h, o, deleted);       // one kernel, any CNF shape
+      } finally {
+        Native.bitmapFree(deleted);
+      }
+    } else {
+      ColumnarIndexScan ref = new ColumnarIndexScan(columnarFile, fldNums, indexTypes, indNames, types, str_sizes,
+                                                    noInFlds, noOutFlds, out_indexes, outFlds, selects, indexOnly);
+      output = Native.bitmapUpload(ctx, nbits, ref.getOutputPositions().toLongArray());
+      ref.close();
+    }
+    cursor = Native.cursorOpen(ctx, table, output, outIdx);
+  }
+
+  private static long tableRows(long table) throws Exception {
+    return Native.tableRows(table);
+  }
+
+  private static int fieldOf(CondExpr e) throws IndexException {
+    if (e.type1.attrType == AttrType.attrSymbol && e.type2.attrType != AttrType.attrSymbol)
+      return e.operand1.symbol.offset;
+    if (e.type2.attrType == AttrType.attrSymbol && e.type1.attrType != AttrType.attrSymbol)
+      return e.operand2.symbol.offset;
+    throw new IndexException("IndexScan.java: invalid constraint");          // :135-141
+  }
+
+  /** every term a Bitmap term and no constraint string repeated (:142-146) */
+  private static boolean bitmapOnlyWithoutRepeats(Columnarfile f, CondExpr[] selects) throws Exception {
+    Set<String> seen = new HashSet<>();
+    for (int c = 0; selects[c] != null; c++)
+      for (CondExpr e = selects[c]; e != null; e = e.next) {
+        fieldOf(e);
+        if (e.indexType == null || e.indexType.indexType != IndexType.Bitmap) return false;
+        String key = f.indexToColName(e.operand1.symbol.offset - 1).concat(e.op.toString())
+            .concat(e.type2.attrType == AttrType.attrInteger ? Integer.toString(e.operand2.integer) : e.operand2.string)
+            .concat(e.indexType.toString());
+        if (!seen.add(key)) return false;
+      }
+    return true;
+  }
+
+  public BitSet getOutputPositions() throws Exception {
+    return BitSet.valueOf(Native.bitmapDownload(ctx, output));
+  }
+
+  public Tuple get_next() throws Exception {
+    if (i == n) {
+      Object[] r = Native.cursorNext(cursor, 8192, projTypes, projSizes);
+      if (r == null) return null;
+      ids = (long[]) r[0];
+      batch = (Object[]) r[1];
+      n = ids.length;
+      i = 0;
+      if (n == 0) return null;
+    }
+    for (int k = 0; k < outIdx.length; k++) {
+      switch (projTypes[k]) {
+        case AttrType.attrInteger: Jtuple.setIntFld(k + 1, ((int[]) batch[k])[i]); break;
+        case AttrType.attrReal: Jtuple.setFloFld(k + 1, ((float[]) batch[k])[i]); break;
+        default: Jtuple.setStrFld(k + 1, ((String[]) batch[k])[i]);
+      }
+    }
+    i++;
+    return Jtuple;
+  }
+
+  /** true where the CNF ran as one GPU launch (false: the reference's positions) */
+  public boolean usedFusedCnf() {
+    return fused;
+  }
+
+  public void close() {
+    if (!closeFlag) {
+      if (cursor != 0) Native.cursorClose(cursor);
+      if (output != 0) Native.bitmapFree(output);
+      cursor = output = 0;
+      closeFlag = true;
+    }
+  }
+
+  public void restart() throws iterator.FileScanException {
+    try {
+      Native.cursorRestart(cursor);
+    } catch (Exception e) {
+      throw new iterator.FileScanException(e, "restart failed");
+    }
+    n = i = 0;
+  }
+
+  public int getTupleSize() {
+    return Jtuple.size();
+  }
+}

@@ -1,0 +1,120 @@
+package iterator;
+
+import columnar.GpuTables;
+import global.AttrType;
+import global.GpuContext;
+import global.Native;
+import global.TID;
+import heap.Tuple;
+
+/**
+ * Drop-in for ColumnarFileScan (R/iterator/ColumnarFileScan.java:51-188): same
+ * constructor, same get_next / get_next_tid / close / restart contract and
+ * the same shared Jtuple.  The predicate (PredEval over the CondExpr[]), the
+ * deleted-row skip and the projection run as MI355X kernels; rows come back
+ * in batches of BATCH through a device cursor, in position order.
+ * get_next_tid's TID carries the position (numRIDs = len_in1); its recordIDs
+ * are left unset -- the reference's callers (DeleteQuery -> markTupleDeleted,
+ * R/columnar/Columnarfile.java:812-830) read only the position.
+ */
+public class GpuColumnarFileScan extends Iterator {
+  static final int BATCH = 8192;
+
+  private final long ctx, table, plan;
+  private long selection, cursor;
+  private final Tuple Jtuple = new Tuple();
+  private final AttrType[] outTypes;
+  private final int[] proj, projTypes;
+  private final short[] projSizes;
+  private final short len_in1;
+  private long[] ids;
+  private Object[] batch;
+  private int n, i;
+
+  public GpuColumnarFileScan(String file_name, AttrType[] in1, short[] s1_sizes, short len_in1, int n_out_flds,
+                             FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
+    this.len_in1 = len_in1;
+    outTypes = new AttrType[n_out_flds];
+    TupleUtils.setup_op_tuple(Jtuple, outTypes, in1, len_in1, s1_sizes, proj_list, n_out_flds);  // :66-71
+    ctx = GpuContext.ctx();
+    table = GpuTables.get(file_name);
+    // per-column char(n) sizes: s1_sizes lists the string columns' sizes in order
+    short[] colSize = new short[len_in1];
+    for (int c = 0, k = 0; c < len_in1; c++)
+      colSize[c] = in1[c].attrType == AttrType.attrString ? s1_sizes[k++] : 4;
+    proj = new int[n_out_flds];
+    projTypes = new int[n_out_flds];
+    projSizes = new short[n_out_flds];
+    for (int k = 0; k < n_out_flds; k++) {
+      if (proj_list[k].relation.key != RelSpec.outer) throw new InvalidRelation("Invalid relation -innerRel");
+      proj[k] = proj_list[k].offset - 1;
+      projTypes[k] = in1[proj[k]].attrType;
+      projSizes[k] = colSize[proj[k]];
+    }
+    plan = Native.planCompile(ctx, table, outFilter);                    // PredEvalException on type errors
+    try {
+      selection = Native.scanBitmap(ctx, plan);                         // one kernel launch
+      cursor = Native.cursorOpen(ctx, table, selection, proj);          // positions + projected values in HBM
+    } catch (Exception e) {
+      close();
+      throw new FileScanException(e, "GPU scan failed");
+    }
+  }
+
+  private boolean fill() throws Exception {
+    if (i < n) return true;
+    Object[] r = Native.cursorNext(cursor, BATCH, projTypes, projSizes);
+    if (r == null) return false;
+    ids = (long[]) r[0];
+    batch = (Object[]) r[1];
+    n = ids.length;
+    i = 0;
+    return n > 0;
+  }
+
+  public Tuple get_next() throws Exception {
+    if (!fill()) return null;
+    for (int k = 0; k < outTypes.length; k++) {
+      switch (outTypes[k].attrType) {
+        case AttrType.attrInteger: Jtuple.setIntFld(k + 1, ((int[]) batch[k])[i]); break;
+        case AttrType.attrReal: Jtuple.setFloFld(k + 1, ((float[]) batch[k])[i]); break;
+        default: Jtuple.setStrFld(k + 1, ((String[]) batch[k])[i]);
+      }
+    }
+    i++;
+    return Jtuple;
+  }
+
+  public TID get_next_tid() throws Exception {
+    if (!fill()) return null;
+    return new TID(len_in1, (int) ids[i++]);
+  }
+
+  /** the whole selection's size (Query's resultCount) without materialising it */
+  public long resultCount() throws Exception {
+    return Native.cursorCount(cursor);
+  }
+
+  public void close() {
+    if (!closeFlag) {
+      if (cursor != 0) Native.cursorClose(cursor);
+      if (selection != 0) Native.bitmapFree(selection);
+      if (plan != 0) Native.planFree(plan);
+      cursor = selection = 0;
+      closeFlag = true;
+    }
+  }
+
+  public void restart() throws FileScanException {
+    try {
+      Native.cursorRestart(cursor);
+    } catch (Exception e) {
+      throw new FileScanException(e, "restart failed");
+    }
+    n = i = 0;
+  }
+
+  public int getTupleSize() {
+    return Jtuple.size();
+  }
+}

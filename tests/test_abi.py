@@ -61,3 +61,24 @@ def test_null_arguments_are_rejected_without_a_device():
     assert L.mbx_sync(None) == m.mbx.E_INVALID
     assert b"null" in L.mbx_last_error()
     assert L.mbx_table_free(None) == 0 and L.mbx_bitmap_free(None) == 0
+
+
+def test_jni_glue_covers_the_java_side_and_calls_only_the_boundary():
+    """jni/mbx_jni.c cannot be compiled here (no JDK): check statically that
+    every `native` method of java/global/Native.java has its
+    Java_global_Native_<name> implementation, that the glue defines nothing
+    else, and that every mbx_* function it calls is declared by include/*.h
+    (and so exported by libmbx.so, test above)."""
+    root = helpers.ROOT
+    java = open(os.path.join(root, "java", "global", "Native.java")).read()
+    natives = set(re.findall(r"\bnative\s+[\w\[\]<>]+\s+(\w+)\s*\(", java))
+    glue = open(os.path.join(root, "jni", "mbx_jni.c")).read()
+    impl = set(re.findall(r"JNICALL\s+Java_global_Native_(\w+)\s*\(", glue))
+    assert natives and natives == impl, (sorted(natives - impl), sorted(impl - natives))
+    calls = set(re.findall(r"\b(mbx_[a-z_0-9]+)\s*\(", re.sub(r"/\*.*?\*/", "", glue, flags=re.S)))
+    undeclared = sorted(calls - set(declared_functions()))
+    assert not undeclared, undeclared
+    # the Java drop-ins keep the reference constructors' parameter lists
+    fs = open(os.path.join(root, "java", "iterator", "GpuColumnarFileScan.java")).read()
+    assert re.search(r"GpuColumnarFileScan\(String file_name, AttrType\[\] in1, short\[\] s1_sizes, short len_in1, "
+                     r"int n_out_flds,\s+FldSpec\[\] proj_list, CondExpr\[\] outFilter\)", fs)
