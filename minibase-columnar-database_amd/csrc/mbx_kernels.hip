@@ -490,14 +490,44 @@ __device__ __forceinline__ StepScan stage_step(uint64_t mw, uint16_t* st, int la
   return r;
 }
 
+// Late materialisation fused into the compaction (C4: positions + projected
+// int / float columns): where a step's positions are written, the values of
+// up to 4 four-byte columns at those rows are loaded (every load of two rows
+// per lane issued before their stores) and written beside them.
+struct Gather4 {
+  const int32_t* col[4];
+  uint32_t* out[4];
+  int32_t n;  // projected columns (0: positions only)
+};
+
+template <int G4>
 __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const StepScan& r, int64_t& off,
                                            int64_t row_offset, int64_t* __restrict__ ids, const uint16_t* st,
-                                           int lane, int64_t cap) {
+                                           int lane, const Gather4& G) {
   if (r.total == 0) return;
-  const int64_t rbase = row_offset + base * 64;
+  const int64_t lbase = base * 64;  // table-local row of bit 0 of word `base`
   if (r.total <= kStageIds) {
-    for (uint32_t i = lane; i < r.total; i += 64)
-      if (off + i < cap) ids[off + i] = rbase + st[i];
+    for (uint32_t i0 = lane; i0 < r.total; i0 += 128) {
+      const uint32_t i1 = i0 + 64;
+      const bool two = i1 < r.total;
+      const int64_t p0 = lbase + st[i0];
+      const int64_t p1 = two ? lbase + st[i1] : p0;
+      uint32_t v0[G4 > 0 ? G4 : 1], v1[G4 > 0 ? G4 : 1];
+#pragma unroll
+      for (int g = 0; g < G4; ++g)
+        if (g < G.n) {
+          v0[g] = (uint32_t)G.col[g][p0];
+          v1[g] = (uint32_t)G.col[g][p1];
+        }
+      ids[off + i0] = row_offset + p0;
+      if (two) ids[off + i1] = row_offset + p1;
+#pragma unroll
+      for (int g = 0; g < G4; ++g)
+        if (g < G.n) {
+          G.out[g][off + i0] = v0[g];
+          if (two) G.out[g][off + i1] = v1[g];
+        }
+    }
     __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next step
   } else {
     uint64_t nz = __ballot(mw != 0ull);
@@ -508,18 +538,23 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
       const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)r.excl, j);
       if ((m >> lane) & 1ull) {
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (off + slot + below < cap) ids[off + slot + below] = rbase + j * 64 + lane;
+        const int64_t p = lbase + j * 64 + lane;
+        const int64_t o = off + slot + below;
+        ids[o] = row_offset + p;
+#pragma unroll
+        for (int g = 0; g < G4; ++g)
+          if (g < G.n) G.out[g][o] = (uint32_t)G.col[g][p];
       }
     }
   }
   off += r.total;
 }
 
+template <int G4 = 0>
 __device__ __forceinline__ void emit_step(int64_t base, uint64_t mw, int64_t& off, int64_t row_offset,
-                                          int64_t* __restrict__ ids, uint16_t* st, int lane,
-                                          int64_t cap = INT64_MAX) {
+                                          int64_t* __restrict__ ids, uint16_t* st, int lane, const Gather4& G) {
   const StepScan r = stage_step(mw, st, lane);
-  store_step(base, mw, r, off, row_offset, ids, st, lane, cap);
+  store_step<G4>(base, mw, r, off, row_offset, ids, st, lane, G);
 }
 
 // ------------------------------------------------------------- fast scan
@@ -1164,12 +1199,13 @@ __global__ __launch_bounds__(kBlock) void k_seg_popcount(const uint64_t* __restr
 // launch); the last block also writes the total.
 constexpr int kSelRegs = 8;  // a wave's words (x64) held in registers between the count and the write pass
 
+template <int G4>
 __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restrict__ words, int64_t nwords,
                                                        int64_t words_per_block,
                                                        const Partial* __restrict__ seg_parts,
                                                        int64_t row_offset, int64_t* __restrict__ ids,
                                                        int64_t* __restrict__ total, int32_t dbg,
-                                                       int64_t* __restrict__ stamps) {
+                                                       int64_t* __restrict__ stamps, Gather4 G) {
   // dbg (diagnostic A/B, mbx_set_tuning "select_dbg"): bit 0 skips the
   // prefix loads, bit 1 the emission; stamps: per block wall_clock64() at
   // start / words + prefix in / after the block barrier / end
@@ -1235,7 +1271,7 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   }
   for (int k = 0; k < wave; ++k) off += wcount[k];
   // one step = 64 consecutive words, lane = word
-  auto step = [&](int64_t base, uint64_t mw) { emit_step(base, mw, off, row_offset, ids, stage[wave], lane); };
+  auto step = [&](int64_t base, uint64_t mw) { emit_step<G4>(base, mw, off, row_offset, ids, stage[wave], lane, G); };
   if (dbg & 2) {
   } else if (cached) {
 #pragma unroll
@@ -1598,11 +1634,26 @@ hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t wo
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                               const Partial* seg_parts, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                               void* const* out, int32_t nproj, int64_t* total, hipStream_t s, int32_t dbg,
-                              int64_t* stamps) {
+                              int64_t* stamps, bool fuse_gather) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   const int64_t g = (nwords + words_per_block - 1) / words_per_block;
-  hipLaunchKernelGGL(k_select_ids, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
-                     seg_parts, row_offset, ids, total, dbg, stamps);
+  // up to 4 int / float columns: gathered by the compaction itself (no
+  // second launch, no re-read of the positions)
+  bool all4 = nproj <= 4;
+  for (int j = 0; j < nproj && j < kMaxProj; ++j) all4 = all4 && proj[j].stride_w == 1;
+  Gather4 G{};
+  if (nproj > 0 && all4 && fuse_gather) {
+    for (int j = 0; j < nproj; ++j) {
+      G.col[j] = (const int32_t*)proj[j].base;
+      G.out[j] = (uint32_t*)out[j];
+    }
+    G.n = nproj;
+    hipLaunchKernelGGL(k_select_ids<4>, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
+                       seg_parts, row_offset, ids, total, dbg, stamps, G);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_select_ids<0>, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
+                     seg_parts, row_offset, ids, total, dbg, stamps, G);
   if (nproj > 0) {
     MatArgs M;
     M.nproj = nproj;
@@ -1610,8 +1661,6 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
       M.proj[j] = proj[j];
       M.out[j] = out[j];
     }
-    bool all4 = nproj <= 4;
-    for (int j = 0; j < nproj && j < kMaxProj; ++j) all4 = all4 && proj[j].stride_w == 1;
     if (all4)
       hipLaunchKernelGGL(k_gather<4>, dim3(1024), dim3(kBlock), 0, s, ids, total, row_offset, M);
     else

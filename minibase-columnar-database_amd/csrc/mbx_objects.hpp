@@ -51,6 +51,7 @@ struct MbxTuning {
   int32_t fin_mode = -1;          // MBX_FIN_MODE (FinMode)
   int32_t join_plain = 0;         // MBX_JOIN_PLAIN: k_join_matrix instead of the fast form
   int32_t distinct_lds_probes = -1;  // MBX_DISTINCT_LDS_PROBES
+  int32_t gather_fused = 1;       // MBX_GATHER_FUSED: 0 = compaction, then k_gather (two launches)
   int32_t select_dbg = 0;         // MBX_SELECT_DBG: diagnostic k_select_ids variants (bit 0 no prefix,
                                   // bit 1 no emission: wrong output) and bit 3 per-block stamps
 };
