@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--variants", default="base")
     ap.add_argument("--gather-rows", type=int, default=100_000_000)
     ap.add_argument("--c2-rows", type=int, default=10_000_000)
+    ap.add_argument("--c3-rows", default="12500000,25000000")
     args = ap.parse_args()
 
     import numpy as np
@@ -152,7 +153,7 @@ def main():
     if "c3small" in args.parts:
         # the strong-scaling shard (12.5M rows = 100M / 8 GPUs) and 25M: C3
         # COUNT scan vs its read probe, finalize / ticket / grid variants
-        for n in (12_500_000, 25_000_000):
+        for n in map(int, args.c3_rows.split(",")):
             cols = [gen_int(n, 1 << 20, 42 + j) for j in range(2)]
             t = ctx.wrap([(M.INTEGER, 4)] * 2, [c.data_ptr() for c in cols], n)
             plan = ctx.compile(t, [[(M.LT, ("sym", 1), ("int", 1 << 19))], [(M.GE, ("sym", 2), ("int", 1 << 19))]])
@@ -173,6 +174,30 @@ def main():
                      "scan_tbs": round(8 * n / statistics.median(res[name]["scan"]) / 1e6, 3)})
             del cols, t, plan
             torch.cuda.empty_cache()
+        apply({})
+
+    if "bitset" in args.parts:
+        # BitSet vs COUNT scan of one column at 100M rows
+        n = 100_000_000
+        c0 = gen_int(n, 1 << 20, 42)
+        t = ctx.wrap([(M.INTEGER, 4)], [c0.data_ptr()], n)
+        plan = ctx.compile(t, [[(M.LT, ("sym", 1), ("int", 104858))]])
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        res = {}
+        for _ in range(args.rounds):
+            for name, kv in variants:
+                apply(kv)
+                bm = ctx.bitmap_alloc(n)
+                r = res.setdefault(name, {"count": [], "bitset": [], "probe": []})
+                r["count"].append(timed(lambda: ctx.scan_count_async(plan, cnt.data_ptr())))
+                r["bitset"].append(timed(lambda: ctx.scan_bitmap_async(plan, bm)))
+                r["probe"].append(timed(lambda: ctx.probe_read(t, [0])))
+                bm.close()
+        for name, _ in variants:
+            out({"part": "bitset", "rows": n, "variant": name,
+                 **{k + "_us": round(statistics.median(v), 2) for k, v in res[name].items()}})
+        del c0, t, plan
+        torch.cuda.empty_cache()
         apply({})
 
     if "gather" in args.parts:

@@ -12,11 +12,14 @@ against a torch reduction of the same device data.
 One process per GPU: launched by torch.distributed.run, C4
 and C5 shard the global table by 64-aligned row ranges (dist.shard_bounds,
 positions global through row_offset) and run with no data-path collective;
-the one exchange step per query is on a side stream:
-  C4  all_gather of the per-rank selected counts (the concatenation offsets
+the one exchange step per query is libmbx's RCCL communicator
+(mbx_comm_*, on its exchange stream after the query's kernels):
+  C4  all-gather of the per-rank selected counts (the concatenation offsets
       of the per-rank outputs, shard order = ascending positions)
-  C5  all_gather of every rank's 48-byte aggregate record straight from
-      device memory (dist.combine_aggregate_device), folded in rank order
+  C5  all-gather of every rank's 48-byte aggregate record straight from
+      device memory, folded in rank order on the device (in place)
+torch.distributed (gloo) only bootstraps the communicator id and runs the
+barriers / max-over-ranks clock.
 Reported per config (rank 0, one JSON line): max-over-ranks wall time per
 query with the exchange included (barrier + synchronize around K queries),
 the per-phase kernel times (max over ranks) and global rows/s.
@@ -64,11 +67,8 @@ def main():
     backend = os.environ.get("MBX_BENCH_BACKEND", "nccl")
     device = 0 if os.environ.get("MBX_BENCH_SAME_DEVICE") == "1" else local_rank
     torch.cuda.set_device(device)
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
-        else:
-            dist.init_process_group(backend)
+    if world > 1:  # host bootstrap, barriers and the clock only
+        dist.init_process_group("gloo")
     m = mbx_pkg.load()
     M = m.mbx
     D = m.dist
@@ -76,11 +76,16 @@ def main():
     ctx = m.Context(device)
     ext = torch.cuda.ExternalStream(ctx.stream)
     xs = torch.cuda.Stream() if world > 1 else None
+    comm = None
+    if world > 1 and backend == "nccl":  # libmbx's RCCL communicator carries the exchange
+        box = [M.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        comm = ctx.comm_init_rank(world, rank, box[0])
 
     def rmax(x):
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -118,8 +123,9 @@ def main():
         return rmax((time.perf_counter() - t0) * 1e3 / steps)
 
     def exchange(k, src_words, out_rows):
-        """The one collective of a query, on the side stream after the library
-        stream's work: all_gather of `src_words` (int64) into out_rows[k]."""
+        """The one collective of a query (gloo rehearsal only; with RCCL the
+        queries call the communicator): all_gather of `src_words` (int64) into
+        out_rows[k] on a side stream after the library stream's work."""
         if world == 1:
             return
         ev = torch.cuda.Event()
@@ -151,7 +157,7 @@ def main():
         ids = torch.zeros(n, dtype=torch.int64, device="cuda")
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
 
-        def step(k=0):  # BitSet + positions + COUNT: one launch (mbx_scan_select_async)
+        def step(k=0):  # BitSet + positions + COUNT: mbx_scan_select_async (BitSet scan, then the compaction)
             M._chk(L.mbx_scan_select_async(ctx.h, plan.h, bm.h, ids.data_ptr(), cnt.data_ptr()))
 
         ms = kernel_ms(step, args.steps, args.warmup)
@@ -197,7 +203,10 @@ def main():
         def query(k):
             and_()
             M._chk(L.mbx_materialize_async(ctx.h, t.h, out.h, proj, 2, ids.data_ptr(), outs, cnts.data_ptr() + 8 * k))
-            exchange(k, cnts[k:k + 1], counts_all)
+            if comm is not None:
+                comm.allgather_count_async(cnts.data_ptr() + 8 * k, counts_all[k].data_ptr())
+            else:
+                exchange(k, cnts[k:k + 1], counts_all)
 
         ms = wall_ms(query, steps, warmup)
         sel = (c2 == 3) & (c3 == 7)
@@ -206,7 +215,7 @@ def main():
         assert got == want and got <= cap, (got, want)
         assert bool((o0[:got] == c0[sel]).all()) and bool((o1[:got] == c1[sel]).all())
         assert bool((ids[:got] == torch.nonzero(sel).flatten() + s).all())
-        glob = got if world == 1 else int(D.combine_count(want, device="cuda" if backend == "nccl" else None))
+        glob = got if world == 1 else int(D.combine_count(want))
         if world > 1:
             assert bool((counts_all[:, rank] == want).all()) and int(counts_all[-1].sum().item()) == glob
         and_ms = kernel_ms(and_, steps, warmup)
@@ -217,7 +226,8 @@ def main():
               "ms_per_query": ms, "rows_per_s": N / ms * 1e3, "algorithmic_gbs": byts / ms / 1e6,
               "phases_ms": {"bitmap_and": and_ms, "positions_and_gather": sel_ms},
               "bitmap_and_gbs": 3 * n / 8 / and_ms / 1e6,
-              "exchange": "none" if world == 1 else "all_gather of per-rank counts (side stream)",
+              "exchange": "none" if world == 1 else ("RCCL all-gather of per-rank counts (libmbx mbx_comm)"
+                                                     if comm is not None else "gloo all_gather (rehearsal)"),
               "backend": backend if world > 1 else None})
         del c0, c1, c2, c3, t, bm2, bm3, a, b, out, ids, o0, o1
         torch.cuda.empty_cache()
@@ -252,14 +262,18 @@ def main():
 
             def query(k):
                 ctx.scan_aggregate_async(plan, 1, recs[k].data_ptr())
-                exchange(k, recs[k], gathered)
+                if comm is not None:  # all-gather + rank-ordered fold into recs[k], on the device
+                    comm.allreduce_agg_async(recs[k].data_ptr())
+                else:
+                    exchange(k, recs[k], gathered)
 
             ms = wall_ms(query, steps, warmup)
+            glob_rec = recs[-1].cpu().numpy().copy()
             scan_ms = kernel_ms(lambda: ctx.scan_aggregate_async(plan, 1, recs[0].data_ptr()), steps, warmup)
             # check: this rank's record vs torch, the folded global vs torch combined
             sel = (c0 < (1 << 19)) & (c1 >= 0.25) & (c2[:, 0] >= ord("M"))
             want = int(sel.sum().item())
-            mine = D.fold_aggregates(recs[-1].cpu().numpy())
+            mine = D.fold_aggregates(recs[0].cpu().numpy())
             assert mine["count"] == want, (mine["count"], want)
             # elementwise + reductions only (no masked-select launch over the table)
             ref_sum = float(torch.where(sel, c1.double(), 0.0).sum().item())
@@ -268,8 +282,8 @@ def main():
                        max=float(torch.where(sel, c1, float("-inf")).max().item()))
             assert mine["min"] == ref["min"] and mine["max"] == ref["max"]
             if world > 1:
-                glob = D.fold_aggregates(gathered[-1].cpu().numpy())
-                gref = D.combine_aggregate(ref, device="cuda" if backend == "nccl" else None)
+                glob = D.fold_aggregates(glob_rec if comm is not None else gathered[-1].cpu().numpy())
+                gref = D.combine_aggregate(ref)
                 assert glob["count"] == gref["count"] and glob["min"] == gref["min"] and glob["max"] == gref["max"]
                 assert abs(glob["sum"] - gref["sum"]) <= 1e-6 * abs(gref["sum"])
             else:
@@ -280,10 +294,13 @@ def main():
                   "phases_ms": {"scan_aggregate": scan_ms},
                   "scan_gbs_per_gpu": n * 24 / scan_ms / 1e6,
                   "sum": glob["sum"], "min": glob["min"], "max": glob["max"],
-                  "exchange": "none" if world == 1 else "one all_gather of the 48-byte aggregate records (side stream)",
+                  "exchange": "none" if world == 1 else ("RCCL all-gather of the 48-byte records + device fold (libmbx)"
+                                                         if comm is not None else "gloo all_gather (rehearsal)"),
                   "backend": backend if world > 1 else None})
             del c0, c1, c2, t, plan, sel
             torch.cuda.empty_cache()
+    if comm is not None:
+        comm.close()
     ctx.close()
     if world > 1:
         dist.barrier()
