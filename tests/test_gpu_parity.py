@@ -472,6 +472,35 @@ def test_bitmap_ops_and_materialize(ctx):
     assert np.array_equal(np.concatenate([p[1] for p in parts]), c0)
 
 
+@pytest.mark.parametrize("density", [0.0, 0.001, 0.01, 0.1, 0.6, 1.0])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_materialize_gather_shapes(ctx, density, fused, tune):
+    """The compaction's own gather (<= 4 int / float columns) and the
+    two-launch form: sparse, LDS-staged and dense (> 2048 positions per step)
+    steps, 1..5 projected columns (5: k_gather), int and float columns, a
+    ragged size and a shard's row_offset; numpy gathers are the check."""
+    tune("gather_fused", fused)
+    n = 700_013
+    rng = np.random.Generator(np.random.PCG64(int(density * 1000) + 7))
+    bits = rng.random(n) < density
+    w = np.zeros(((n + 63) // 64) * 64, dtype=bool)
+    w[:n] = bits
+    words = np.packbits(w, bitorder="little").view(np.uint64)
+    ints = helpers.synthetic_int_table(n, 3, 1 << 30, 5)
+    f0 = rng.random(n, dtype=np.float32)
+    f1 = rng.standard_normal(n).astype(np.float32)
+    cols = [(oracle.INTEGER, 4, ints[0]), (oracle.REAL, 4, f0), (oracle.INTEGER, 4, ints[1]), (oracle.REAL, 4, f1),
+            (oracle.INTEGER, 4, ints[2])]
+    t = ctx.stage(cols, row_offset=6400)
+    bm = ctx.bitmap_upload(n, words)
+    pos = np.nonzero(bits)[0]
+    for proj in ([0], [1, 3], [3, 0, 2], [4, 3, 2, 1], [0, 1, 2, 3, 4]):
+        ids, outs = ctx.materialize(t, bm, proj)
+        assert np.array_equal(ids, pos + 6400), proj
+        for j, o in zip(proj, outs):
+            assert np.array_equal(np.asarray(o).view(np.uint32), np.asarray(cols[j][2])[pos].view(np.uint32)), (proj, j)
+
+
 def test_index_build_matches_oracle(ctx):
     cols, _ = mixed_table(300_001)
     ot, t = oracle.Table(cols), ctx.stage(cols)
