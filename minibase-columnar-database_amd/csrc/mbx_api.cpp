@@ -46,6 +46,11 @@ int mbx::fail(int code, const char* fmt, ...) {
 
 // ----------------------------------------------------------------- helpers
 
+// A bitmap's segment = the BitSet scan's block and the unit of its compact
+// segment counts (~1024 segments).  Capping segments at 48 tiles (one column,
+// 100M rows) speeds the BitSet scan 78.1 -> 71.2 us but slows the AND over
+// such bitmaps 7.2 -> 10.2 us and the compaction 20.9 -> 24.4 us, both of
+// which want ~1024 blocks (profiles/r02/anatomy/segment_cap_48.jsonl): not kept.
 static int64_t tiles_per_block_for(const mbx_ctx* c, int64_t nrows) {
   if (c->tune.tiles_per_block > 0) return c->tune.tiles_per_block;
   return choose_tiles_per_block(nrows);
@@ -146,14 +151,14 @@ int mbx::bitmap_new(mbx_ctx* c, int64_t nbits, mbx_bitmap** out) {
   b->wpb = tiles_per_block_for(c, nbits) * kWordsPerTile;
   b->nseg = b->nwords == 0 ? 1 : (b->nwords + b->wpb - 1) / b->wpb;
   hipError_t e = hipMalloc(&b->words, sizeof(uint64_t) * (size_t)(b->nwords > 0 ? b->nwords : 1));
-  if (e == hipSuccess) e = hipMalloc(&b->segs, sizeof(Partial) * (size_t)b->nseg);
+  if (e == hipSuccess) e = hipMalloc(&b->segc, sizeof(int64_t) * (size_t)b->nseg);
   if (e != hipSuccess) {
     hipFree(b->words);
-    hipFree(b->segs);
+    hipFree(b->segc);
     delete b;
     return fail(MBX_E_NOMEM, "bitmap of %lld bits: %s", (long long)nbits, hipGetErrorString(e));
   }
-  if (b->nwords == 0) hipMemsetAsync(b->segs, 0, sizeof(Partial), c->stream);
+  if (b->nwords == 0) hipMemsetAsync(b->segc, 0, sizeof(int64_t), c->stream);
   *out = b;
   return MBX_OK;
 }
@@ -841,7 +846,8 @@ static int32_t ticket_groups_of(const mbx_ctx* c) {
 }
 
 static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int32_t mode, uint64_t* out_words,
-                        Partial* parts, int64_t tpb, int64_t* count_out, AggOut* agg_out, int32_t* nan_out) {
+                        Partial* parts, int64_t tpb, int64_t* count_out, AggOut* agg_out, int32_t* nan_out,
+                        int64_t* seg_counts = nullptr) {
   ScanLaunch L;
   L.plan = v.dev;
   L.nrows = p->t->nrows;
@@ -870,6 +876,7 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
                          tpb * kWordsPerTile * (int64_t)sizeof(uint64_t) <= kSinkLdsMaxBytes;
   L.sink_lds = sink_fits && (tu.sink_lds == 2 || (tu.sink_lds == 1 && tpb >= 128));
   L.ticket_groups = ticket_groups_of(c);
+  L.seg_counts = seg_counts;
   L.fin_mode = tu.fin_mode >= 0 ? tu.fin_mode : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
   if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))
     L.fin_mode = kFinWriteThrough;
@@ -934,7 +941,8 @@ static int scan_bitmap_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int32_t* dev
   if (rc) return rc;
   const int64_t tpb = b->wpb / kWordsPerTile;
   if (grid_blocks(p->t->nrows, tpb) != b->nseg) return fail(MBX_E_INVALID, "scan_bitmap: segment mismatch");
-  return enqueue_scan(c, p, *v, kModeBitmap, b->words, b->segs, tpb, c->dcount, nullptr, dev_nan);
+  if ((rc = ensure_partials(c, b->nseg))) return rc;
+  return enqueue_scan(c, p, *v, kModeBitmap, b->words, c->partials, tpb, c->dcount, nullptr, dev_nan, b->segc);
 }
 
 // read back the count + NaN flag the last scan's final block wrote
@@ -1027,17 +1035,17 @@ extern "C" int mbx_scan_select(mbx_ctx* c, const mbx_plan* pc, int64_t* host_ids
 }
 
 static int bitmap_count_sync(mbx_ctx* c, mbx_bitmap* b, bool with_nan) {
-  HIPCHK(launch_finalize(b->segs, b->nseg, kInt, nullptr, c->dcount, nan_sync(c), c->stream));
+  (void)with_nan;  // segment counts carry no NaN flag: scans report theirs through their own finalize
+  HIPCHK(launch_count_sum(b->segc, b->nseg, c->dcount, c->stream));
   int64_t* h = (int64_t*)c->pinned;
   HIPCHK(hipMemcpyAsync(h, c->dcount, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipMemcpyAsync((int32_t*)c->pinned + 8, nan_sync(c), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   b->count = h[0];
-  return with_nan ? check_nan(c) : MBX_OK;
+  return MBX_OK;
 }
 
 int mbx::bitmap_recount(mbx_ctx* c, mbx_bitmap* b) {
-  HIPCHK(launch_seg_popcount(b->words, b->nwords, b->wpb, b->segs, c->stream));
+  HIPCHK(launch_seg_popcount(b->words, b->nwords, b->wpb, b->segc, c->stream));
   return bitmap_count_sync(c, b, false);
 }
 
@@ -1114,7 +1122,7 @@ extern "C" int mbx_bitmap_free(mbx_bitmap* b) {
   hipSetDevice(b->ctx->device);
   hipStreamSynchronize(b->ctx->stream);
   hipFree(b->words);
-  hipFree(b->segs);
+  hipFree(b->segc);
   delete b;
   return MBX_OK;
 }
@@ -1140,7 +1148,7 @@ extern "C" int mbx_bitmap_upload(mbx_ctx* c, int64_t nbits, const uint64_t* host
       return fail(MBX_E_DEVICE, "bitmap_upload: %s", hipGetErrorString(e));
     }
   }
-  hipError_t e = launch_seg_popcount(b->words, b->nwords, b->wpb, b->segs, c->stream);
+  hipError_t e = launch_seg_popcount(b->words, b->nwords, b->wpb, b->segc, c->stream);
   if (e != hipSuccess || (rc = bitmap_count_sync(c, b, false))) {
     mbx_bitmap_free(b);
     return rc ? rc : fail(MBX_E_DEVICE, "bitmap_upload: %s", hipGetErrorString(e));
@@ -1184,7 +1192,7 @@ extern "C" int mbx_bitmap_combine(mbx_ctx* c, int32_t op, const mbx_bitmap* a, c
   if (rc) return rc;
   mbx_bitmap* r = nullptr;
   if ((rc = bitmap_new(c, a->nbits, &r))) return rc;
-  hipError_t e = launch_bitmap_combine(op, a->words, b->words, r->nwords, r->nbits, r->wpb, r->words, r->segs,
+  hipError_t e = launch_bitmap_combine(op, a->words, b->words, r->nwords, r->nbits, r->wpb, r->words, r->segc,
                                        c->stream);
   if (e != hipSuccess) {
     mbx_bitmap_free(r);
@@ -1235,7 +1243,7 @@ extern "C" int mbx_bitmap_cnf(mbx_ctx* c, int64_t nbits, const mbx_bitmap* const
   mbx_bitmap* r = nullptr;
   if ((rc = bitmap_new(c, nbits, &r))) return rc;
   hipError_t e = launch_bitmap_cnf(C, deleted ? deleted->words : nullptr, r->nwords, r->nbits, r->wpb, r->words,
-                                   r->segs, c->stream);
+                                   r->segc, c->stream);
   if (e != hipSuccess) {
     mbx_bitmap_free(r);
     return fail(MBX_E_DEVICE, "bitmap_cnf: %s", hipGetErrorString(e));
@@ -1258,7 +1266,7 @@ extern "C" int mbx_bitmap_cnf_async(mbx_ctx* c, const mbx_bitmap* const* bms, co
   if (rc) return rc;
   out->count = -1;
   HIPCHK(launch_bitmap_cnf(C, deleted ? deleted->words : nullptr, out->nwords, out->nbits, out->wpb, out->words,
-                           out->segs, c->stream));
+                           out->segc, c->stream));
   return MBX_OK;
 }
 
@@ -1316,14 +1324,14 @@ int mbx::index_build_encoded(mbx_ctx* c, const mbx_table* t, int32_t col, const 
     kc.kind = col_kind(tc.attr_type);
     kc.stride_w = tc.stride_w;
     if (kc.kind != kStr && tc.stride_w == 1 && !(reinterpret_cast<uintptr_t>(tc.dev) & 15)) {
-      std::vector<Partial*> segs((size_t)nvalues);
-      for (int32_t v = 0; v < nvalues; v++) segs[(size_t)v] = out[v]->segs;
+      std::vector<int64_t*> segs((size_t)nvalues);
+      for (int32_t v = 0; v < nvalues; v++) segs[(size_t)v] = out[v]->segc;
       e = launch_index_build4(kc, t->nrows, t->deleted, dvals, nvalues, outs.data(), segs.data(), out[0]->wpb,
                               c->stream);
     } else {
       e = launch_index_build(kc, t->nrows, t->deleted, dvals, nvalues, vw, outs.data(), out[0]->wpb, c->stream);
       for (int32_t v = 0; v < nvalues && e == hipSuccess; v++)
-        e = launch_seg_popcount(out[v]->words, out[v]->nwords, out[v]->wpb, out[v]->segs, c->stream);
+        e = launch_seg_popcount(out[v]->words, out[v]->nwords, out[v]->wpb, out[v]->segc, c->stream);
     }
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1373,7 +1381,7 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
     if (!c->stamps) HIPCHK(hipMalloc(&c->stamps, sizeof(int64_t) * 4 * kMaxStampBlocks));
     if (sel->nseg <= kMaxStampBlocks) stamps = c->stamps;
   }
-  HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segs, row_offset, dev_ids, pc, dev_out, nproj,
+  HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segc, row_offset, dev_ids, pc, dev_out, nproj,
                             dev_total, c->stream, c->tune.select_dbg & 3, stamps, c->tune.gather_fused != 0));
   return MBX_OK;
 }

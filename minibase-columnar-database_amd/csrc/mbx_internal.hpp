@@ -99,7 +99,7 @@ struct AggOut {
   float fmin, fmax;
 };
 
-// per-segment counts live in the `count` field of a Partial array
+// COUNT / BitSet finalize partials store only these words of a Partial
 constexpr int kSegStride = (int)(sizeof(Partial) / sizeof(int64_t));
 
 enum ScanMode : int32_t { kModeCount = 0, kModeBitmap = 1, kModeAgg = 2 };
@@ -128,6 +128,7 @@ struct ScanLaunch {
   int32_t ri;                 // 1: row-interleaved tile layout (register j of lane l = row 64j + l)
   int32_t sink_lds;           // 1: BitSet words of the block's full tiles staged in dynamic LDS
                               //    (tiles_per_block x 32 B) and stored in one burst at the block's end
+  int64_t* seg_counts;        // BitSet scans: the output bitmap's per-segment counts (one per block)
 };
 
 // dynamic LDS per block for the staged BitSet (4 blocks per CU: <= 128 KB of
@@ -281,21 +282,24 @@ hipError_t launch_scan(const ScanLaunch& L, hipStream_t s);
 hipError_t launch_finalize(const Partial* partials, int64_t nblocks, int32_t agg_kind, AggOut* out,
                            int64_t* count_out, int32_t* nan_flag, hipStream_t s);
 hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
-                             int64_t words_per_block, uint64_t* out, Partial* seg_parts, hipStream_t s);
+                             int64_t words_per_block, uint64_t* out, int64_t* segc, hipStream_t s);
 hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* b, int64_t nwords,
-                                 int64_t nbits, int64_t words_per_block, uint64_t* out, Partial* seg_parts,
+                                 int64_t nbits, int64_t words_per_block, uint64_t* out, int64_t* segc,
                                  hipStream_t s);
+// per-segment counts of a BitSet (segments of words_per_block words): a
+// compact int64 array, one per segment
 hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t words_per_block,
-                               Partial* seg_parts, hipStream_t s);
+                               int64_t* segc, hipStream_t s);
+hipError_t launch_count_sum(const int64_t* segc, int64_t n, int64_t* out, hipStream_t s);
 // positions (ascending) of the set bits + gather of the projected columns;
 // *total = the number of set bits (written on the stream)
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
-                              const Partial* seg_parts, int64_t row_offset, int64_t* ids,
+                              const int64_t* segc, int64_t row_offset, int64_t* ids,
                               const ProjCol* proj, void* const* out, int32_t nproj, int64_t* total,
                               hipStream_t s, int32_t dbg = 0, int64_t* stamps = nullptr, bool fuse_gather = true);
 // 4-byte columns (int / float): also writes every output's segment counts
 hipError_t launch_index_build4(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
-                               int32_t nvalues, uint64_t* const* outs, Partial* const* segs, int64_t words_per_block,
+                               int32_t nvalues, uint64_t* const* outs, int64_t* const* segs, int64_t words_per_block,
                                hipStream_t s);
 hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
                               int32_t nvalues,

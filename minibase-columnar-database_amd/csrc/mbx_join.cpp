@@ -57,7 +57,7 @@ int positions(mbx_ctx* c, const mbx_bitmap* sel, int64_t** dev, int64_t* n) {
   *n = sel->count;
   HIPCHK(hipMalloc(dev, sizeof(int64_t) * (size_t)(*n > 0 ? *n : 1)));
   int64_t* dtotal = c->dcount + 1;
-  hipError_t e = launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segs, 0, *dev, nullptr, nullptr, 0, dtotal,
+  hipError_t e = launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segc, 0, *dev, nullptr, nullptr, 0, dtotal,
                                     c->stream);
   if (e != hipSuccess) {
     hipFree(*dev);
@@ -194,9 +194,9 @@ extern "C" int mbx_join(mbx_ctx* c, const mbx_table* outer, const mbx_bitmap* ou
     // uses a prefix of the scratch BitSet: its segments are the same)
     const int64_t nw = rows * wpr;
     const int64_t nseg = (nw + m->wpb - 1) / m->wpb;
-    if (e == hipSuccess) e = launch_seg_popcount(m->words, nw, m->wpb, m->segs, s);
+    if (e == hipSuccess) e = launch_seg_popcount(m->words, nw, m->wpb, m->segc, s);
     int64_t* dtotal = c->dcount + 1;
-    if (e == hipSuccess) e = launch_finalize(m->segs, nseg, kInt, nullptr, dtotal, nullptr, s);
+    if (e == hipSuccess) e = launch_count_sum(m->segc, nseg, dtotal, s);
     int64_t got = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&got, dtotal, sizeof(int64_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -209,7 +209,7 @@ extern "C" int mbx_join(mbx_ctx* c, const mbx_table* outer, const mbx_bitmap* ou
       if (e != hipSuccess) break;
       ids_cap = got;
     }
-    e = launch_materialize(m->words, nw, m->wpb, m->segs, 0, ids, nullptr, nullptr, 0, dtotal, s);
+    e = launch_materialize(m->words, nw, m->wpb, m->segc, 0, ids, nullptr, nullptr, 0, dtotal, s);
     if (e != hipSuccess || (rc = grow(r, r->count + got, s))) break;
     JoinDecode D;
     memset(&D, 0, sizeof(D));

@@ -348,15 +348,8 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
       Acc r = sh[0];
 #pragma unroll
       for (int w = 1; w < kWaves; ++w) acc_merge(r, sh[w]);
-      if (L.mode == kModeBitmap) {
-        // the segment count for the compaction launch that follows: only a
-        // later launch reads it, so the store is not waited for here
-        Partial p;
-        p.count = r.count;
-        p.nan_seen = r.nan;
-        p.pad_ = 0;
-        store_count_sc1(L.partials + blockIdx.x, p);
-      }
+      if (L.seg_counts)  // the BitSet's segment count, for a later compaction launch: not waited for
+        __hip_atomic_store(L.seg_counts + blockIdx.x, r.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       packed_count_finalize(L.ticket, L.ticket_groups, r.count, r.nan, L.count_out, L.nan_out);
     }
     return;
@@ -365,6 +358,8 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
     Acc r = sh[0];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) acc_merge(r, sh[w]);
+    if (L.seg_counts)
+      __hip_atomic_store(L.seg_counts + blockIdx.x, r.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     Partial p;
     p.count = r.count;
     p.isum = r.isum;
@@ -1073,7 +1068,7 @@ constexpr int kCnfBatch = 4;  // operand bitmaps whose loads k_bitmap_cnf issues
 __global__ __launch_bounds__(kBlock) void k_bitmap_cnf(BitmapCnf C, const uint64_t* __restrict__ del,
                                                        int64_t nwords, uint64_t tail_mask,
                                                        int64_t words_per_block, uint64_t* __restrict__ out,
-                                                       Partial* __restrict__ seg_parts) {
+                                                       int64_t* __restrict__ segc) {
   const int64_t w0 = (int64_t)blockIdx.x * words_per_block;
   const int64_t w1 = min(w0 + words_per_block, nwords);
   int64_t cnt = 0;
@@ -1138,7 +1133,7 @@ __global__ __launch_bounds__(kBlock) void k_bitmap_cnf(BitmapCnf C, const uint64
   if (threadIdx.x == 0) {
     int64_t s = 0;
     for (int i = 0; i < kWaves; ++i) s += sh[i];
-    seg_parts[blockIdx.x].count = s;
+    segc[blockIdx.x] = s;
   }
 }
 
@@ -1146,7 +1141,7 @@ __global__ __launch_bounds__(kBlock) void k_bitmap_combine(int32_t op, const uin
                                                            const uint64_t* __restrict__ b, int64_t nwords,
                                                            uint64_t tail_mask, int64_t words_per_block,
                                                            uint64_t* __restrict__ out,
-                                                           Partial* __restrict__ seg_parts) {
+                                                           int64_t* __restrict__ segc) {
   const int64_t w0 = (int64_t)blockIdx.x * words_per_block;
   const int64_t w1 = min(w0 + words_per_block, nwords);
   int64_t cnt = 0;
@@ -1164,13 +1159,13 @@ __global__ __launch_bounds__(kBlock) void k_bitmap_combine(int32_t op, const uin
   if (threadIdx.x == 0) {
     int64_t s = 0;
     for (int i = 0; i < kWaves; ++i) s += sh[i];
-    seg_parts[blockIdx.x].count = s;
+    segc[blockIdx.x] = s;
   }
 }
 
 __global__ __launch_bounds__(kBlock) void k_seg_popcount(const uint64_t* __restrict__ words, int64_t nwords,
                                                          int64_t words_per_block,
-                                                         Partial* __restrict__ seg_parts) {
+                                                         int64_t* __restrict__ segc) {
   const int64_t w0 = (int64_t)blockIdx.x * words_per_block;
   const int64_t w1 = min(w0 + words_per_block, nwords);
   int64_t cnt = 0;
@@ -1183,7 +1178,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_popcount(const uint64_t* __restr
   if (threadIdx.x == 0) {
     int64_t s = 0;
     for (int i = 0; i < kWaves; ++i) s += sh[i];
-    seg_parts[blockIdx.x].count = s;
+    segc[blockIdx.x] = s;
   }
 }
 
@@ -1202,7 +1197,7 @@ constexpr int kSelRegs = 8;  // a wave's words (x64) held in registers between t
 template <int G4>
 __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restrict__ words, int64_t nwords,
                                                        int64_t words_per_block,
-                                                       const Partial* __restrict__ seg_parts,
+                                                       const int64_t* __restrict__ segc, int64_t segs_per_block,
                                                        int64_t row_offset, int64_t* __restrict__ ids,
                                                        int64_t* __restrict__ total, int32_t dbg,
                                                        int64_t* __restrict__ stamps, Gather4 G) {
@@ -1223,20 +1218,24 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   // a wave range of <= 64 * kSelRegs words is loaded once, all loads in
   // flight together, and kept in registers for the write pass
   const bool cached = a1 - a0 <= 64 * kSelRegs;
-  // this block's output offset: the segment counts before it, 4 loads in
-  // flight per thread, issued before the word loads so both latencies overlap
+  // this block's output offset: the segment counts before it (a compact
+  // int64 array, two per 16-byte load, 4 loads in flight per thread), issued
+  // before the word loads so both latencies overlap
+  const int64_t npre = (dbg & 1) ? 0 : (int64_t)blockIdx.x * segs_per_block;
+  const int64_t npairs = npre >> 1;
+  const ulonglong2* __restrict__ sp = reinterpret_cast<const ulonglong2*>(segc);
   int64_t pre = 0;
-  const int64_t npre = (dbg & 1) ? 0 : (int64_t)blockIdx.x;
-  for (int64_t i0 = 0; i0 < npre; i0 += 4 * kBlock) {
-    int64_t v[4];
+  for (int64_t i0 = 0; i0 < npairs; i0 += 4 * kBlock) {
+    ulonglong2 v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int64_t i = i0 + k * kBlock + threadIdx.x;
-      v[k] = i < npre ? seg_parts[i].count : 0;
+      v[k] = i < npairs ? sp[i] : ulonglong2{0ull, 0ull};
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) pre += v[k];
+    for (int k = 0; k < 4; ++k) pre += (int64_t)(v[k].x + v[k].y);
   }
+  if ((npre & 1) && threadIdx.x == 0) pre += segc[npre - 1];
   uint64_t wr[kSelRegs];
   int64_t c = 0;
   if (cached) {
@@ -1396,7 +1395,7 @@ __global__ __launch_bounds__(kBlock) void k_index_build(KCol col, int64_t nrows,
 // slots (no separate popcount pass).
 struct IndexArgs4 {
   uint64_t* out[64];
-  Partial* segs[64];
+  int64_t* segs[64];
 };
 
 template <int U>
@@ -1453,7 +1452,7 @@ __global__ __launch_bounds__(kBlock) void k_index_build4(const int32_t* __restri
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < kWaves; ++k) c += cnt[k][threadIdx.x];
-    A.segs[threadIdx.x][blockIdx.x].count = c;
+    A.segs[threadIdx.x][blockIdx.x] = c;
   }
 }
 
@@ -1607,36 +1606,58 @@ static uint64_t tail_mask_of(int64_t nbits) {
 }
 
 hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
-                             int64_t words_per_block, uint64_t* out, Partial* seg_parts, hipStream_t s) {
+                             int64_t words_per_block, uint64_t* out, int64_t* segc, hipStream_t s) {
   const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
   hipLaunchKernelGGL(k_bitmap_cnf, dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,
-                     tail_mask_of(nbits), words_per_block, out, seg_parts);
+                     tail_mask_of(nbits), words_per_block, out, segc);
   return hipGetLastError();
 }
 
 hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* b, int64_t nwords, int64_t nbits,
-                                 int64_t words_per_block, uint64_t* out, Partial* seg_parts, hipStream_t s) {
+                                 int64_t words_per_block, uint64_t* out, int64_t* segc, hipStream_t s) {
   const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
   hipLaunchKernelGGL(k_bitmap_combine, dim3((unsigned)g), dim3(kBlock), 0, s, op, a, b, nwords,
-                     tail_mask_of(nbits), words_per_block, out, seg_parts);
+                     tail_mask_of(nbits), words_per_block, out, segc);
   return hipGetLastError();
 }
 
-hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t words_per_block, Partial* seg_parts,
+hipError_t launch_seg_popcount(const uint64_t* words, int64_t nwords, int64_t words_per_block, int64_t* segc,
                                hipStream_t s) {
   const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;
   hipLaunchKernelGGL(k_seg_popcount, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
-                     seg_parts);
+                     segc);
+  return hipGetLastError();
+}
+
+// the sum of n segment counts (a BitSet's cardinality), one block, fixed order
+__global__ __launch_bounds__(kBlock) void k_count_sum(const int64_t* __restrict__ segc, int64_t n,
+                                                     int64_t* __restrict__ out) {
+  __shared__ int64_t sh[kWaves];
+  int64_t c = 0;
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) c += segc[i];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+hipError_t launch_count_sum(const int64_t* segc, int64_t n, int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_count_sum, dim3(1), dim3(kBlock), 0, s, segc, n, out);
   return hipGetLastError();
 }
 
 
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
-                              const Partial* seg_parts, int64_t row_offset, int64_t* ids, const ProjCol* proj,
+                              const int64_t* segc, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                               void* const* out, int32_t nproj, int64_t* total, hipStream_t s, int32_t dbg,
                               int64_t* stamps, bool fuse_gather) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
-  const int64_t g = (nwords + words_per_block - 1) / words_per_block;
+  // ~1024 compaction blocks whatever the segment size: S segments per block
+  const int64_t nseg = (nwords + words_per_block - 1) / words_per_block;
+  const int64_t S = (nseg + 1023) / 1024;
+  const int64_t wpb = S * words_per_block;
+  const int64_t g = (nwords + wpb - 1) / wpb;
   // up to 4 int / float columns: gathered by the compaction itself (no
   // second launch, no re-read of the positions)
   bool all4 = nproj <= 4;
@@ -1648,12 +1669,12 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
       G.out[j] = (uint32_t*)out[j];
     }
     G.n = nproj;
-    hipLaunchKernelGGL(k_select_ids<4>, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
-                       seg_parts, row_offset, ids, total, dbg, stamps, G);
+    hipLaunchKernelGGL(k_select_ids<4>, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, wpb, segc, S,
+                       row_offset, ids, total, dbg, stamps, G);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(k_select_ids<0>, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, words_per_block,
-                     seg_parts, row_offset, ids, total, dbg, stamps, G);
+  hipLaunchKernelGGL(k_select_ids<0>, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, wpb, segc, S,
+                     row_offset, ids, total, dbg, stamps, G);
   if (nproj > 0) {
     MatArgs M;
     M.nproj = nproj;
@@ -1670,7 +1691,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 }
 
 hipError_t launch_index_build4(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
-                               int32_t nvalues, uint64_t* const* outs, Partial* const* segs, int64_t words_per_block,
+                               int32_t nvalues, uint64_t* const* outs, int64_t* const* segs, int64_t words_per_block,
                                hipStream_t s) {
   const int64_t nwords = (nrows + 63) >> 6;
   const int64_t g = nwords == 0 ? 1 : (nwords + words_per_block - 1) / words_per_block;

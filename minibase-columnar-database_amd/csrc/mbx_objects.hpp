@@ -118,7 +118,7 @@ struct mbx_bitmap {
   uint64_t* words = nullptr;
   int64_t wpb = 4;        // words per segment
   int64_t nseg = 1;
-  Partial* segs = nullptr;  // per-segment counts (Partial.count)
+  int64_t* segc = nullptr;  // per-segment counts, compact (one int64 per segment of wpb words)
   int64_t count = -1;     // host copy of the cardinality, -1 = unknown
 };
 
