@@ -7,10 +7,13 @@ One "step" = one ColumnarFileScan COUNT pass over the resident table:
 `query ... {(c0 < 2^19)} ^ {(c1 >= 2^19)} FILESCAN` -> Total Results Count,
 executed as ONE kernel launch per GPU (k_scan_fast<2, COUNT>; its last block
 folds the per-block counts), plus -- on N > 1 GPUs -- the path's one exchange
-step: an in-place RCCL all-reduce of the step's COUNT over xGMI, issued by
-libmbx (mbx_comm_allreduce_count_async) on the communicator's exchange
-stream, so the next step's scan overlaps it.  Inputs are resident in HBM
-before the timed region.
+step: an in-place RCCL all-reduce of the COUNTs over xGMI, issued by libmbx
+(mbx_comm_allreduce_count_async) on the communicator's exchange stream, so
+the next scans overlap it.  The exchange is bucketed (--exchange-bucket,
+default 10 = one captured graph): every step's COUNT is combined over all
+ranks, 10 steps per collective -- a tiny all-reduce costs its latency, not
+its bytes, so 10x fewer collectives (--exchange-bucket 1: one per step).
+Inputs are resident in HBM before the timed region.
 
 Scaling:
   --scaling strong (default): the metric's config -- ONE 100M-row table, split
@@ -20,7 +23,7 @@ Scaling:
       N and is checked against a torch reduction of the whole table.
   --scaling weak: every rank owns its own --rows-row table.
 The timed steps replay HIP graphs (mbx_graph_*) of --graph-steps captured
-steps (scan + exchange each): launch-bound small shards (12.5M rows/GPU at
+steps (scans + their exchange): launch-bound small shards (12.5M rows/GPU at
 N=8, ~18 us per scan) would otherwise wait on the host.  value = global rows
 scanned by all ranks / max-over-ranks wall time.  stdout carries only the
 JSON line.
@@ -167,6 +170,8 @@ def main():
                     help="global rows (strong scaling) or rows per GPU (weak)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured HIP graph (0: eager launches)")
+    ap.add_argument("--exchange-bucket", type=int, default=10,
+                    help="steps whose COUNTs share one all-reduce (1: one collective per step)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -238,12 +243,20 @@ def main():
     base = counts.data_ptr()
     gloo_works = []
 
-    def step(k):
-        ctx.scan_count_async(plan, base + 8 * k)
-        if comm is not None:
-            comm.allreduce_count_async(base + 8 * k, 1)
-        elif exchange:  # same-device rehearsal: gloo over host copies
-            gloo_works.append(k)
+    B = max(1, args.exchange_bucket)
+
+    def run_steps(k0, k1):
+        """steps k0..k1-1: one scan each; the exchange all-reduces the COUNTs
+        of every B consecutive steps in one collective (bucketed: each step's
+        count is still combined over all ranks, B per collective)"""
+        for j in range(k0, k1, B):
+            je = min(j + B, k1)
+            for k in range(j, je):
+                ctx.scan_count_async(plan, base + 8 * k)
+            if comm is not None:
+                comm.allreduce_count_async(base + 8 * j, je - j)
+            elif exchange:  # same-device rehearsal: gloo over host copies
+                gloo_works.extend(range(j, je))
 
     def drain():
         ctx.sync()
@@ -253,8 +266,7 @@ def main():
             counts[gloo_works] = h.cuda()
             gloo_works.clear()
 
-    for k in range(warmup):
-        step(k)
+    run_steps(0, warmup)
     drain()
 
     # HIP graphs of G steps each (the timed region replays them); captured
@@ -266,8 +278,7 @@ def main():
         while k0 < warmup + steps:
             g = min(G, warmup + steps - k0)
             ctx.graph_begin()
-            for k in range(k0, k0 + g):
-                step(k)
+            run_steps(k0, k0 + g)
             graphs.append(ctx.graph_end())
             k0 += g
         for gr in graphs:  # one untimed replay
@@ -285,8 +296,7 @@ def main():
         for gr in graphs:
             gr.launch()
     else:
-        for k in range(steps):
-            step(warmup + k)
+        run_steps(warmup, warmup + steps)
     t_enq = time.perf_counter() - t0  # host enqueue time of the steps (diagnostic, stderr)
     drain()
     torch.cuda.synchronize()
@@ -329,7 +339,8 @@ def main():
         ms_per_step = t_max * 1e3 / steps
         algo_bytes = 2 * 4 * n  # c0 + c1 read once per launch (rank 0's shard)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        xchg = "RCCL all-reduce of the step's COUNT (libmbx mbx_comm, exchange stream)" if comm is not None else (
+        xchg = (f"RCCL all-reduce of the COUNTs of every {B} steps (libmbx mbx_comm, exchange stream)"
+                if comm is not None else None) or (
             "gloo all-reduce (same-device rehearsal)" if exchange else "none")
         out = {
             "metric": METRIC,
@@ -355,6 +366,7 @@ def main():
                 "parallelism": f"row-range shards x{world}",
                 "exchange": xchg,
                 "graph_steps": G,
+                "exchange_bucket_steps": B if exchange else None,
             },
             "phases_us": {
                 "step_wall": ms_per_step * 1e3,
