@@ -598,7 +598,9 @@ __device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const u
 // the row is live (TupleScan skips deleted rows, R/columnar/TupleScan.java:80-87),
 // every required conjunct before the term held and no earlier term of its
 // own conjunct did (R/iterator/PredEval.java:164-175); KTerm.req_below.
-template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool RI = false>
+// WHOLE: the tile is one of the table's full tiles (the main loop's): no row
+// bound checks -- only the one partial tile needs them
+template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool RI = false, bool WHOLE = false>
 __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, KS>& D,
                                           int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
                                           Acc& acc, uint64_t& wave_count, const KTerm* th = nullptr,
@@ -670,16 +672,16 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
 
   bool live[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) live[j] = row0 + j * kRowStep < nrows;
+  for (int j = 0; j < 4; ++j) live[j] = WHOLE || row0 + j * kRowStep < nrows;
   const int64_t word = t * kWordsPerTile + (RI ? 0 : (lane >> 4));
   if (DEL && RI) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint64_t dw = word + j < nwords ? L.deleted[word + j] : 0ull;  // uniform: one scalar load
+      const uint64_t dw = (WHOLE || word + j < nwords) ? L.deleted[word + j] : 0ull;  // uniform: one scalar load
       live[j] = live[j] && !((dw >> lane) & 1ull);
     }
   } else if (DEL) {
-    const uint64_t dw = word < nwords ? L.deleted[word] : 0ull;
+    const uint64_t dw = (WHOLE || word < nwords) ? L.deleted[word] : 0ull;
     const uint32_t dn = (uint32_t)(dw >> ((lane & 15) * 4)) & 0xFu;
 #pragma unroll
     for (int j = 0; j < 4; ++j) live[j] = live[j] && !((dn >> j) & 1u);
@@ -701,12 +703,12 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
       ws[3] = w3;
     } else {
       const uint64_t w = lane == 0 ? w0 : (lane == 1 ? w1 : (lane == 2 ? w2 : w3));
-      if (lane < 4 && word + lane < nwords) L.out_words[word + lane] = w;
+      if (lane < 4 && (WHOLE || word + lane < nwords)) L.out_words[word + lane] = w;
     }
   } else if (MODE == kModeBitmap) {
     const uint32_t nib = (uint32_t)p[0] | ((uint32_t)p[1] << 1) | ((uint32_t)p[2] << 2) | ((uint32_t)p[3] << 3);
     const uint64_t w = pack_word16(nib, lane);
-    if ((lane & 15) == 0 && word < nwords) L.out_words[word] = w;
+    if ((lane & 15) == 0 && (WHOLE || word < nwords)) L.out_words[word] = w;
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) wave_count += __popcll(__ballot(p[j]));
@@ -929,7 +931,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
       if (t < tf) {
         if constexpr (kSink) {
           uint64_t w[4];
-          fast_tile<K, KS, MODE, DEL, TQ, RI>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
+          fast_tile<K, KS, MODE, DEL, TQ, RI, true>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
                                               th, w);
           if ((lane >> 2) == sink_n) {
             const int j = lane & 3;
@@ -937,7 +939,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
           }
           if (++sink_n == 16) sink_flush();
         } else {
-          fast_tile<K, KS, MODE, DEL, TQ, RI>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
+          fast_tile<K, KS, MODE, DEL, TQ, RI, true>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
                                               th);
         }
       }
