@@ -228,6 +228,18 @@ int mbx_bitmap_cnf_async(mbx_ctx *ctx, const mbx_bitmap *const *bms, const int32
 int mbx_bitmap_index_build(mbx_ctx *ctx, const mbx_table *t, int32_t col, const mbx_operand *values,
                            int32_t nvalues, mbx_bitmap **out);
 
+/* ColumnarIndexScan end to end in ONE kernel launch (R/index/ColumnarIndexScan.java:130-181, then the
+ * nextSetBit + getRecord loop :287-308): the CNF of index BitSets exactly as mbx_bitmap_cnf (the CNF's
+ * BitSet itself is never stored), then the positions (dev_ids, may be NULL) and the values of up to 4
+ * projected 4-byte (int / float) columns of every selected row, as mbx_materialize_async, and the
+ * count in *dev_count.  Each block publishes its count and takes its output offset from its
+ * predecessors' counts (decoupled look-back) -- the one-launch form of mbx_bitmap_cnf_async +
+ * mbx_materialize_async.  Strings or > 4 columns: MBX_E_UNSUPPORTED (use the two calls). */
+int mbx_cnf_materialize_async(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *const *bms,
+                              const int32_t *conj_offsets, int32_t nconj, const mbx_bitmap *deleted,
+                              const int32_t *proj, int32_t nproj, int64_t *dev_ids,
+                              void *const *dev_out, int64_t *dev_count);
+
 /* ---- late materialisation: the nextSetBit loops + Heapfile.findRID/getRecord
  * per output column (R/index/ColumnarIndexScan.java:287-308,
  * R/iterator/ColumnarColumnScan.java:151-176, R/iterator/Projection.java:103-146) */

@@ -229,6 +229,7 @@ extern "C" int mbx_free(mbx_ctx* c) {
   hipFree(c->ticket);
   hipFree(c->ids_scratch);
   hipFree(c->stamps);
+  hipFree(c->lookback);
   if (c->pinned) hipHostFree(c->pinned);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -1383,6 +1384,47 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
   }
   HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segc, row_offset, dev_ids, pc, dev_out, nproj,
                             dev_total, c->stream, c->tune.select_dbg & 3, stamps, c->tune.gather_fused != 0));
+  return MBX_OK;
+}
+
+extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* const* bms,
+                                         const int32_t* conj_offsets, int32_t nconj, const mbx_bitmap* deleted,
+                                         const int32_t* proj, int32_t nproj, int64_t* dev_ids,
+                                         void* const* dev_out, int64_t* dev_count) {
+  NOTNULL(c);
+  NOTNULL(t);
+  NOTNULL(dev_count);
+  BitmapCnf C;
+  int rc = cnf_args(t->nrows, bms, conj_offsets, nconj, deleted, &C);
+  if (rc) return rc;
+  if (nproj < 0 || nproj > 4)
+    return fail(MBX_E_UNSUPPORTED, "cnf_materialize: %d columns (0..4; more: mbx_bitmap_cnf_async + "
+                "mbx_materialize_async)", nproj);
+  ProjCol pc[4];
+  if (nproj > 0) {
+    NOTNULL(proj);
+    NOTNULL(dev_out);
+  }
+  for (int32_t j = 0; j < nproj; j++) {
+    if (proj[j] < 0 || proj[j] >= (int32_t)t->cols.size())
+      return fail(MBX_E_RANGE, "cnf_materialize: column %d outside 0..%zu", proj[j], t->cols.size() - 1);
+    const TCol& tc = t->cols[(size_t)proj[j]];
+    if (tc.attr_type == MBX_ATTR_STRING || tc.stride_w != 1)
+      return fail(MBX_E_UNSUPPORTED, "cnf_materialize: column %d is not a 4-byte column (strings: "
+                  "mbx_bitmap_cnf_async + mbx_materialize_async)", proj[j]);
+    if (!dev_out[j]) return fail(MBX_E_INVALID, "cnf_materialize: dev_out[%d] null", j);
+    pc[j].base = tc.dev;
+    pc[j].stride_w = 1;
+    pc[j].pad_ = 0;
+  }
+  if ((rc = set_device(c))) return rc;
+  if (!c->lookback) {
+    HIPCHK(hipMalloc(&c->lookback, sizeof(int64_t) * kLookbackWords));
+    HIPCHK(hipMemsetAsync(c->lookback, 0, sizeof(int64_t) * kLookbackWords, c->stream));
+  }
+  const int64_t nwords = (t->nrows + 63) >> 6;
+  HIPCHK(launch_cnf_materialize(C, deleted ? deleted->words : nullptr, nwords, t->nrows, c->lookback,
+                                t->row_offset, dev_ids, pc, dev_out, nproj, dev_count, c->stream));
   return MBX_OK;
 }
 

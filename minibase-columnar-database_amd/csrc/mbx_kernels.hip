@@ -514,8 +514,10 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
           v0[g] = (uint32_t)G.col[g][p0];
           v1[g] = (uint32_t)G.col[g][p1];
         }
-      ids[off + i0] = row_offset + p0;
-      if (two) ids[off + i1] = row_offset + p1;
+      if (ids) {
+        ids[off + i0] = row_offset + p0;
+        if (two) ids[off + i1] = row_offset + p1;
+      }
 #pragma unroll
       for (int g = 0; g < G4; ++g)
         if (g < G.n) {
@@ -535,7 +537,7 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         const int64_t p = lbase + j * 64 + lane;
         const int64_t o = off + slot + below;
-        ids[o] = row_offset + p;
+        if (ids) ids[o] = row_offset + p;
 #pragma unroll
         for (int g = 0; g < G4; ++g)
           if (g < G.n) G.out[g][o] = (uint32_t)G.col[g][p];
@@ -1287,6 +1289,150 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 3] = wall_clock64();
 }
 
+// ColumnarIndexScan in one launch (mbx_cnf_materialize_async,
+// R/index/ColumnarIndexScan.java:130-181 then :287-308): each block forms its
+// words of the CNF of index BitSets in registers (as k_bitmap_cnf; the CNF's
+// BitSet is never stored), publishes its count at once, sums its
+// predecessors' published counts for its output offset (decoupled look-back:
+// blocks are dispatched in index order, so every predecessor is resident or
+// done and publishes without waiting on anything) and writes its positions
+// (ids may be null) + up to 4 projected 4-byte columns as k_select_ids<4>.
+// The look-back sits between a short load phase and the gathers, so its
+// round trips overlap other blocks' gathers rather than a scan's stream.
+// lb[0] = the epoch of the previous launch; lb[1 + b] = epoch << 32 | count
+// of block b.  Every launch's epoch differs from the stale flags it finds,
+// so nothing is cleared between launches (graph replays included: the
+// epoch is read from lb[0], not baked into the launch); the last block,
+// having seen every other block's flag (so every block has read lb[0]),
+// stores the new epoch.
+constexpr int kLookbackBlocks = 4 * kBlock;  // one poll load per thread per 256 predecessors
+
+__device__ __forceinline__ uint64_t cnf_word(const BitmapCnf& C, int64_t w) {
+  uint64_t r = ~0ull;
+  for (int c = 0; c < C.nconj; ++c) {
+    uint64_t o = 0;
+    for (int k = C.conj_off[c]; k < C.conj_off[c + 1]; ++k) o |= C.bms[k][w];
+    r &= o;
+  }
+  return r;
+}
+
+template <int G4>
+__global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
+                                                       int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
+                                                       int64_t* __restrict__ lb, int64_t row_offset,
+                                                       int64_t* __restrict__ ids, int64_t* __restrict__ total,
+                                                       Gather4 G) {
+  __shared__ int64_t wcount[kWaves];
+  __shared__ int64_t wpre[kWaves];
+  __shared__ uint16_t stage[kWaves][32 * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  const uint32_t prev = (uint32_t)lb[0];
+  const int64_t epoch = prev == 0xffffffffu ? 1 : (int64_t)prev + 1;
+  const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
+  const int64_t s1 = min(s0 + words_per_block, nwords);
+  const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
+  const int64_t a0 = min(s0 + wave * per, s1);
+  const int64_t a1 = min(a0 + per, s1);
+  const bool cached = a1 - a0 <= 64 * kSelRegs;
+  const int nbm = C.conj_off[C.nconj];
+  auto word_at = [&](int64_t w) -> uint64_t {
+    uint64_t r = cnf_word(C, w);
+    if (del) r &= ~del[w];
+    if (w == nwords - 1) r &= tail_mask;
+    return r;
+  };
+  uint64_t wr[kSelRegs];
+  int64_t c = 0;
+  if (cached && nbm <= kCnfBatch) {
+    // every operand word of the wave's range in flight at once
+    uint64_t q[kSelRegs][kCnfBatch + 1];
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t w = a0 + r * 64 + lane;
+#pragma unroll
+      for (int k = 0; k < kCnfBatch; ++k) q[r][k] = (k < nbm && w < a1) ? C.bms[k][w] : 0ull;
+      q[r][kCnfBatch] = (del && w < a1) ? del[w] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t w = a0 + r * 64 + lane;
+      uint64_t x = ~0ull;
+      for (int cj = 0; cj < C.nconj; ++cj) {
+        uint64_t o = 0;
+#pragma unroll
+        for (int k = 0; k < kCnfBatch; ++k)
+          if (k >= C.conj_off[cj] && k < C.conj_off[cj + 1]) o |= q[r][k];
+        x &= o;
+      }
+      x &= ~q[r][kCnfBatch];
+      if (w == nwords - 1) x &= tail_mask;
+      wr[r] = w < a1 ? x : 0ull;
+      c += __popcll(wr[r]);
+    }
+  } else if (cached) {
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t w = a0 + r * 64 + lane;
+      wr[r] = w < a1 ? word_at(w) : 0ull;
+      c += __popcll(wr[r]);
+    }
+  } else {
+    for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(word_at(w));
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+  if (lane == 0) wcount[wave] = c;
+  __syncthreads();
+  int64_t bc = 0;
+  for (int k = 0; k < kWaves; ++k) bc += wcount[k];
+  if (threadIdx.x == 0)
+    __hip_atomic_store(&lb[1 + blockIdx.x], (epoch << 32) | bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // look-back: the predecessors' counts, all polls of a thread in flight together
+  int64_t pre = 0;
+  {
+    int64_t v[kLookbackBlocks / kBlock];
+#pragma unroll
+    for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
+      const int64_t j = (int64_t)k * kBlock + threadIdx.x;
+      v[k] = j < (int64_t)blockIdx.x ? __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : (epoch << 32);
+    }
+#pragma unroll
+    for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
+      const int64_t j = (int64_t)k * kBlock + threadIdx.x;
+      while ((v[k] >> 32) != epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        v[k] = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      pre += v[k] & 0xffffffffll;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
+  if (lane == 0) wpre[wave] = pre;
+  __syncthreads();
+  int64_t off = 0;
+  for (int k = 0; k < kWaves; ++k) off += wpre[k];
+  if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) {
+    *total = off + bc;
+    lb[0] = epoch;
+  }
+  for (int k = 0; k < wave; ++k) off += wcount[k];
+  auto step = [&](int64_t base, uint64_t mw) { emit_step<G4>(base, mw, off, row_offset, ids, stage[wave], lane, G); };
+  if (cached) {
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t base = a0 + r * 64;
+      if (base >= a1) break;
+      step(base, wr[r]);
+    }
+  } else {
+    for (int64_t base = a0; base < a1; base += 64) step(base, base + lane < a1 ? word_at(base + lane) : 0ull);
+  }
+}
+
 // Late materialisation (Heapfile.findRID + getRecord per output column,
 // R/index/ColumnarIndexScan.java:292-297): out_p[i] = column_p[ids[i]] for
 // the *total selected rows; thread per output row, 4 rows in flight per
@@ -1689,6 +1835,26 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
     else
       hipLaunchKernelGGL(k_gather<0>, dim3(1024), dim3(kBlock), 0, s, ids, total, row_offset, M);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
+                                  int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
+                                  void* const* out, int32_t nproj, int64_t* total, hipStream_t s) {
+  if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
+  if (nproj < 0 || nproj > 4) return hipErrorInvalidValue;
+  Gather4 G{};
+  for (int j = 0; j < nproj; ++j) {
+    if (proj[j].stride_w != 1) return hipErrorInvalidValue;
+    G.col[j] = (const int32_t*)proj[j].base;
+    G.out[j] = (uint32_t*)out[j];
+  }
+  G.n = nproj;
+  // <= kLookbackBlocks blocks: one poll load per thread per 256 predecessors
+  const int64_t wpb = (nwords + kLookbackBlocks - 1) / kLookbackBlocks;
+  const int64_t g = (nwords + wpb - 1) / wpb;
+  hipLaunchKernelGGL(k_cnf_select<4>, dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,
+                     tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G);
   return hipGetLastError();
 }
 

@@ -70,6 +70,7 @@ struct mbx_ctx {
   int64_t* ids_scratch = nullptr;  // positions for a gather whose caller wants no positions
   int64_t ids_cap = 0;
   int64_t* stamps = nullptr;    // diagnostic per-block stamps (select_dbg bit 3)
+  int64_t* lookback = nullptr;  // k_cnf_select's epoch + per-block counts (kLookbackWords, zeroed once)
   void* pinned = nullptr;       // 256 bytes of pinned host scratch
   mbx_comm* comm = nullptr;     // multi-GPU exchange (mbx_comm.cpp), owned
   bool capturing = false;       // mbx_graph_begin .. mbx_graph_end

@@ -84,7 +84,7 @@ EXPORTS = [
     "mbx_scan_count", "mbx_scan_count_async", "mbx_scan_bitmap", "mbx_scan_bitmap_async", "mbx_scan_select",
     "mbx_scan_select_async", "mbx_scan_aggregate",
     "mbx_scan_aggregate_async", "mbx_bitmap_alloc", "mbx_bitmap_upload", "mbx_bitmap_download", "mbx_bitmap_info",
-    "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_bitmap_index_build",
+    "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_cnf_materialize_async", "mbx_bitmap_index_build",
     "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
     "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close", "mbx_probe_read", "mbx_set_tuning",
     "mbx_diag_select_stamps", "mbx_dev_alloc", "mbx_dev_free", "mbx_dev_download", "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
@@ -159,6 +159,7 @@ def lib():
         "mbx_bitmap_select": ([V, V, I64, V, I64, P(I64)], ctypes.c_int),
         "mbx_materialize": ([V, V, V, P(I32), I32, V, P(V), I64, P(I64)], ctypes.c_int),
         "mbx_materialize_async": ([V, V, V, P(I32), I32, V, P(V), V], ctypes.c_int),
+        "mbx_cnf_materialize_async": ([V, V, P(V), P(I32), I32, V, P(I32), I32, V, P(V), V], ctypes.c_int),
         "mbx_cursor_open": ([V, V, V, P(I32), I32, P(V)], ctypes.c_int),
         "mbx_cursor_count": ([V, P(I64)], ctypes.c_int),
         "mbx_cursor_next": ([V, I64, V, P(V), P(I64)], ctypes.c_int),
@@ -515,6 +516,24 @@ class Context:
         offs[len(conjuncts)] = k
         _chk(lib().mbx_bitmap_cnf_async(self.h, bms, offs, len(conjuncts),
                                         None if deleted is None else deleted.h, out.h))
+
+    def cnf_materialize_async(self, table, conjuncts, proj, dev_ids, dev_outs, dev_count, deleted=None):
+        """mbx_cnf_materialize_async: CNF of index BitSets + positions + <= 4
+        projected 4-byte columns in one launch (device pointers as ints;
+        dev_ids may be None)."""
+        flat = [b for conj in conjuncts for b in conj]
+        bms = (ctypes.c_void_p * max(1, len(flat)))(*[b.h.value for b in flat])
+        offs = (ctypes.c_int32 * (len(conjuncts) + 1))()
+        k = 0
+        for i, conj in enumerate(conjuncts):
+            offs[i] = k
+            k += len(conj)
+        offs[len(conjuncts)] = k
+        pj = (ctypes.c_int32 * max(1, len(proj)))(*proj)
+        outs = (ctypes.c_void_p * max(1, len(proj)))(*dev_outs)
+        _chk(lib().mbx_cnf_materialize_async(self.h, table.h, bms, offs, len(conjuncts),
+                                             None if deleted is None else deleted.h, pj, len(proj), dev_ids,
+                                             outs, dev_count))
 
     def index_build(self, table, col, values):
         keep = []
