@@ -203,6 +203,8 @@ extern "C" int mbx_init(int32_t device, mbx_ctx** out) {
     if (e == hipSuccess) e = hipMalloc(&c->ticket, sizeof(uint32_t) * kTicketWords);
     if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(uint32_t) * kTicketWords);
     if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 256, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&c->lookback, sizeof(int64_t) * kLookbackWords);
+    if (e == hipSuccess) e = hipMemset(c->lookback, 0, sizeof(int64_t) * kLookbackWords);
     if (e != hipSuccess) {
       rc = fail(MBX_E_DEVICE, "mbx_init: %s", hipGetErrorString(e));
       break;
@@ -1418,13 +1420,14 @@ extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const m
     pc[j].pad_ = 0;
   }
   if ((rc = set_device(c))) return rc;
-  if (!c->lookback) {
-    HIPCHK(hipMalloc(&c->lookback, sizeof(int64_t) * kLookbackWords));
-    HIPCHK(hipMemsetAsync(c->lookback, 0, sizeof(int64_t) * kLookbackWords, c->stream));
-  }
   const int64_t nwords = (t->nrows + 63) >> 6;
+  int64_t* stamps = nullptr;
+  if (c->tune.select_dbg & 8) {  // diagnostic stamps (mbx_diag_select_stamps), <= 1024 blocks
+    if (!c->stamps) HIPCHK(hipMalloc(&c->stamps, sizeof(int64_t) * 4 * kMaxStampBlocks));
+    stamps = c->stamps;
+  }
   HIPCHK(launch_cnf_materialize(C, deleted ? deleted->words : nullptr, nwords, t->nrows, c->lookback,
-                                t->row_offset, dev_ids, pc, dev_out, nproj, dev_count, c->stream));
+                                t->row_offset, dev_ids, pc, dev_out, nproj, dev_count, c->stream, stamps));
   return MBX_OK;
 }
 

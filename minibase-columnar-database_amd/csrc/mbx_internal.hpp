@@ -282,12 +282,13 @@ hipError_t launch_scan(const ScanLaunch& L, hipStream_t s);
 hipError_t launch_finalize(const Partial* partials, int64_t nblocks, int32_t agg_kind, AggOut* out,
                            int64_t* count_out, int32_t* nan_flag, hipStream_t s);
 // one launch: words of the CNF (never stored) -> positions (ids may be null)
-// + <= 4 projected 4-byte columns; lb = 1 + 1024 int64 look-back words,
+// + <= 4 projected 4-byte columns; lb = kLookbackWords int64 look-back words,
 // zeroed once at allocation (k_cnf_select)
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
-                                  void* const* out, int32_t nproj, int64_t* total, hipStream_t s);
-constexpr int64_t kLookbackWords = 1 + 1024;
+                                  void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
+                                  int64_t* stamps = nullptr);
+constexpr int64_t kLookbackWords = 1 + 1024;  // epoch, per-block counts
 hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                              int64_t words_per_block, uint64_t* out, int64_t* segc, hipStream_t s);
 hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* b, int64_t nwords,

@@ -446,7 +446,10 @@ struct StepScan {
   uint32_t total;  // the step's positions (uniform)
 };
 
-__device__ __forceinline__ StepScan stage_step(uint64_t mw, uint16_t* st, int lane) {
+// sbase / pbase: stage from st[sbase] on, offsets + pbase; nothing is staged
+// unless the step's positions fit below kStageIds
+__device__ __forceinline__ StepScan stage_step(uint64_t mw, uint16_t* st, int lane, uint32_t sbase = 0,
+                                               uint32_t pbase = 0) {
   const uint32_t pc = (uint32_t)__popcll(mw);
   uint32_t incl = pc;
 #pragma unroll
@@ -457,7 +460,8 @@ __device__ __forceinline__ StepScan stage_step(uint64_t mw, uint16_t* st, int la
   StepScan r;
   r.excl = incl - pc;
   r.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  if (r.total == 0 || r.total > kStageIds) return r;
+  if (r.total == 0 || sbase + r.total > kStageIds) return r;
+  st += sbase;
   uint64_t nz = __ballot(mw != 0ull);
   uint32_t maxpc = pc;
 #pragma unroll
@@ -466,7 +470,7 @@ __device__ __forceinline__ StepScan stage_step(uint64_t mw, uint16_t* st, int la
     uint64_t m = mw;
     uint32_t o = r.excl;
     while (m) {
-      st[o++] = (uint16_t)(lane * 64 + __builtin_ctzll(m));
+      st[o++] = (uint16_t)(pbase + lane * 64 + __builtin_ctzll(m));
       m &= m - 1ull;
     }
   } else {
@@ -477,7 +481,7 @@ __device__ __forceinline__ StepScan stage_step(uint64_t mw, uint16_t* st, int la
       const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)r.excl, j);
       if ((m >> lane) & 1ull) {
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        st[slot + below] = (uint16_t)(j * 64 + lane);
+        st[slot + below] = (uint16_t)(pbase + j * 64 + lane);
       }
     }
   }
@@ -498,11 +502,12 @@ struct Gather4 {
 template <int G4>
 __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const StepScan& r, int64_t& off,
                                            int64_t row_offset, int64_t* __restrict__ ids, const uint16_t* st,
-                                           int lane, const Gather4& G) {
+                                           int lane, const Gather4& G, uint32_t first = 0) {
   if (r.total == 0) return;
   const int64_t lbase = base * 64;  // table-local row of bit 0 of word `base`
   if (r.total <= kStageIds) {
-    for (uint32_t i0 = lane; i0 < r.total; i0 += 128) {
+    // staged positions from `first` on (the caller wrote those below it)
+    for (uint32_t i0 = first + lane; i0 < r.total; i0 += 128) {
       const uint32_t i1 = i0 + 64;
       const bool two = i1 < r.total;
       const int64_t p0 = lbase + st[i0];
@@ -1296,16 +1301,23 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
 // predecessors' published counts for its output offset (decoupled look-back:
 // blocks are dispatched in index order, so every predecessor is resident or
 // done and publishes without waiting on anything) and writes its positions
-// (ids may be null) + up to 4 projected 4-byte columns as k_select_ids<4>.
-// The look-back sits between a short load phase and the gathers, so its
-// round trips overlap other blocks' gathers rather than a scan's stream.
+// (ids may be null) + up to G4 projected 4-byte columns.
+// Each wave stages the positions of its leading steps together (while they
+// fit the stage) and loads the values of the first 256 of them BEFORE the
+// look-back resolves: the look-back's round trips overlap those gathers, and
+// a sparse wave (C4: ~250 rows) needs one gather round trip, not one per
+// 64-word step.
 // lb[0] = the epoch of the previous launch; lb[1 + b] = epoch << 32 | count
 // of block b.  Every launch's epoch differs from the stale flags it finds,
-// so nothing is cleared between launches (graph replays included: the
-// epoch is read from lb[0], not baked into the launch); the last block,
-// having seen every other block's flag (so every block has read lb[0]),
-// stores the new epoch.
+// so nothing is cleared between launches (graph replays included: the epoch
+// is read from lb[0], not baked into the launch); the last block, having
+// seen every other block's flag (so every block has read lb[0]), stores the
+// new epoch.
 constexpr int kLookbackBlocks = 4 * kBlock;  // one poll load per thread per 256 predecessors
+// staged rows per lane whose values load before the look-back: 6 x 64 covers
+// a 1 % wave of ~245 rows with 9 sd to spare; 4 columns hold fewer (occupancy)
+template <int G4>
+constexpr int prefetch_rows() { return G4 <= 2 ? 6 : 3; }
 
 __device__ __forceinline__ uint64_t cnf_word(const BitmapCnf& C, int64_t w) {
   uint64_t r = ~0ull;
@@ -1317,12 +1329,15 @@ __device__ __forceinline__ uint64_t cnf_word(const BitmapCnf& C, int64_t w) {
   return r;
 }
 
-template <int G4>
+template <int G4, int NB>  // G4: projected columns the registers hold; NB: 1..4 operands batched, 0: any
 __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
                                                        int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
                                                        int64_t* __restrict__ lb, int64_t row_offset,
                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                       Gather4 G) {
+                                                       Gather4 G, int64_t* __restrict__ stamps) {
+  // stamps (diagnostic, select_dbg bit 3): per block wall_clock64() at start /
+  // count published / offset known / end
+  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
   __shared__ int64_t wcount[kWaves];
   __shared__ int64_t wpre[kWaves];
   __shared__ uint16_t stage[kWaves][32 * 64];
@@ -1336,7 +1351,6 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   const int64_t a0 = min(s0 + wave * per, s1);
   const int64_t a1 = min(a0 + per, s1);
   const bool cached = a1 - a0 <= 64 * kSelRegs;
-  const int nbm = C.conj_off[C.nconj];
   auto word_at = [&](int64_t w) -> uint64_t {
     uint64_t r = cnf_word(C, w);
     if (del) r &= ~del[w];
@@ -1345,15 +1359,15 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   };
   uint64_t wr[kSelRegs];
   int64_t c = 0;
-  if (cached && nbm <= kCnfBatch) {
-    // every operand word of the wave's range in flight at once
-    uint64_t q[kSelRegs][kCnfBatch + 1];
+  if (NB > 0 && cached) {
+    // every operand word of the wave's range in flight at once (NB x 8
+    // register pairs: sized to the operand count)
+    uint64_t q[kSelRegs][NB > 0 ? NB : 1];
 #pragma unroll
     for (int r = 0; r < kSelRegs; ++r) {
       const int64_t w = a0 + r * 64 + lane;
 #pragma unroll
-      for (int k = 0; k < kCnfBatch; ++k) q[r][k] = (k < nbm && w < a1) ? C.bms[k][w] : 0ull;
-      q[r][kCnfBatch] = (del && w < a1) ? del[w] : 0ull;
+      for (int k = 0; k < NB; ++k) q[r][k] = w < a1 ? C.bms[k][w] : 0ull;
     }
 #pragma unroll
     for (int r = 0; r < kSelRegs; ++r) {
@@ -1362,11 +1376,11 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
       for (int cj = 0; cj < C.nconj; ++cj) {
         uint64_t o = 0;
 #pragma unroll
-        for (int k = 0; k < kCnfBatch; ++k)
+        for (int k = 0; k < NB; ++k)
           if (k >= C.conj_off[cj] && k < C.conj_off[cj + 1]) o |= q[r][k];
         x &= o;
       }
-      x &= ~q[r][kCnfBatch];
+      if (del && w < a1) x &= ~del[w];
       if (w == nwords - 1) x &= tail_mask;
       wr[r] = w < a1 ? x : 0ull;
       c += __popcll(wr[r]);
@@ -1387,32 +1401,60 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   __syncthreads();
   int64_t bc = 0;
   for (int k = 0; k < kWaves; ++k) bc += wcount[k];
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
     __hip_atomic_store(&lb[1 + blockIdx.x], (epoch << 32) | bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (stamps) stamps[4 * blockIdx.x + 1] = wall_clock64();
+  }
   // look-back: the predecessors' counts, all polls of a thread in flight together
-  int64_t pre = 0;
-  {
-    int64_t v[kLookbackBlocks / kBlock];
+  int64_t v[kLookbackBlocks / kBlock];
 #pragma unroll
-    for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
-      const int64_t j = (int64_t)k * kBlock + threadIdx.x;
-      v[k] = j < (int64_t)blockIdx.x ? __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : (epoch << 32);
+  for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
+    const int64_t j = (int64_t)k * kBlock + threadIdx.x;
+    v[k] = j < (int64_t)blockIdx.x ? __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : (epoch << 32);
+  }
+  // meanwhile: stage the wave's leading steps together, load the first
+  // kPrefetch x 64 rows' values
+  uint16_t* const st = stage[wave];
+  uint32_t tot = 0;  // staged positions (offsets from bit 0 of word a0: < 8 x 4096)
+  int nst = 0;       // steps staged
+  constexpr int kPrefetch = prefetch_rows<G4>();
+  uint32_t pv[kPrefetch][G4 > 0 ? G4 : 1];
+  if (cached) {
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      if (a0 + r * 64 >= a1) break;
+      const StepScan q = stage_step(wr[r], st, lane, tot, (uint32_t)r * 4096u);
+      if (tot + q.total > kStageIds) break;
+      tot += q.total;
+      nst = r + 1;
     }
 #pragma unroll
-    for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
-      const int64_t j = (int64_t)k * kBlock + threadIdx.x;
-      while ((v[k] >> 32) != epoch) {
-        __builtin_amdgcn_s_sleep(1);
-        v[k] = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < kPrefetch; ++k) {
+      const uint32_t i = (uint32_t)lane + 64u * k;
+      if (i < tot) {
+        const int64_t p = a0 * 64 + st[i];
+#pragma unroll
+        for (int g = 0; g < G4; ++g)
+          if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p];
       }
-      pre += v[k] & 0xffffffffll;
     }
+  }
+  int64_t pre = 0;
+#pragma unroll
+  for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
+    const int64_t j = (int64_t)k * kBlock + threadIdx.x;
+    while ((v[k] >> 32) != epoch) {
+      __builtin_amdgcn_s_sleep(1);
+      v[k] = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    pre += v[k] & 0xffffffffll;
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
   if (lane == 0) wpre[wave] = pre;
   __syncthreads();
+  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
   for (int k = 0; k < kWaves; ++k) off += wpre[k];
   if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) {
@@ -1420,16 +1462,35 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
     lb[0] = epoch;
   }
   for (int k = 0; k < wave; ++k) off += wcount[k];
-  auto step = [&](int64_t base, uint64_t mw) { emit_step<G4>(base, mw, off, row_offset, ids, stage[wave], lane, G); };
   if (cached) {
+    // the prefetched rows, then the rest of the staged ones, then the steps
+    // that did not fit the stage one by one
+#pragma unroll
+    for (int k = 0; k < kPrefetch; ++k) {
+      const uint32_t i = (uint32_t)lane + 64u * k;
+      if (i < tot) {
+        if (ids) ids[off + i] = row_offset + a0 * 64 + st[i];
+#pragma unroll
+        for (int g = 0; g < G4; ++g)
+          if (g < G.n) G.out[g][off + i] = pv[k][g];
+      }
+    }
+    const StepScan all{0u, tot};
+    store_step<G4>(a0, 0ull, all, off, row_offset, ids, st, lane, G, 64u * kPrefetch);
 #pragma unroll
     for (int r = 0; r < kSelRegs; ++r) {
       const int64_t base = a0 + r * 64;
+      if (r < nst) continue;
       if (base >= a1) break;
-      step(base, wr[r]);
+      emit_step<G4>(base, wr[r], off, row_offset, ids, st, lane, G);
     }
   } else {
-    for (int64_t base = a0; base < a1; base += 64) step(base, base + lane < a1 ? word_at(base + lane) : 0ull);
+    for (int64_t base = a0; base < a1; base += 64)
+      emit_step<G4>(base, base + lane < a1 ? word_at(base + lane) : 0ull, off, row_offset, ids, st, lane, G);
+  }
+  if (stamps) {
+    __syncthreads();
+    if (threadIdx.x == 0) stamps[4 * blockIdx.x + 3] = wall_clock64();
   }
 }
 
@@ -1840,7 +1901,8 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
-                                  void* const* out, int32_t nproj, int64_t* total, hipStream_t s) {
+                                  void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
+                                  int64_t* stamps) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   if (nproj < 0 || nproj > 4) return hipErrorInvalidValue;
   Gather4 G{};
@@ -1853,8 +1915,23 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   // <= kLookbackBlocks blocks: one poll load per thread per 256 predecessors
   const int64_t wpb = (nwords + kLookbackBlocks - 1) / kLookbackBlocks;
   const int64_t g = (nwords + wpb - 1) / wpb;
-  hipLaunchKernelGGL(k_cnf_select<4>, dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,
-                     tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G);
+  const int nbm = c.conj_off[c.nconj];
+  // the prefetch registers sized to the projection: <= 2 columns or <= 4
+#define MBX_CNF_SELECT(NB)                                                                                  \
+  if (nproj <= 2)                                                                                           \
+    hipLaunchKernelGGL((k_cnf_select<2, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
+                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps);                    \
+  else                                                                                                      \
+    hipLaunchKernelGGL((k_cnf_select<4, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
+                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps)
+  switch (nbm) {
+    case 1: MBX_CNF_SELECT(1); break;
+    case 2: MBX_CNF_SELECT(2); break;
+    case 3: MBX_CNF_SELECT(3); break;
+    case 4: MBX_CNF_SELECT(4); break;
+    default: MBX_CNF_SELECT(0); break;
+  }
+#undef MBX_CNF_SELECT
   return hipGetLastError();
 }
 

@@ -40,9 +40,10 @@ def words_of(bits):
 
 
 def cnf_bits(conj_bits, deleted=None):
+    n = len(next(c for c in conj_bits if c)[0])
     r = None
     for conj in conj_bits:
-        o = np.zeros_like(conj[0]) if conj else None
+        o = np.zeros(n, dtype=bool)
         for b in conj:
             o = o | b
         r = o if r is None else r & o

@@ -45,6 +45,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--configs", default="C2,C4,C5")
     ap.add_argument("--c4-rows", type=int, default=100_000_000, help="global rows")
+    ap.add_argument("--c4-positions", action="store_true",
+                    help="C4 query also writes the selected positions (default: the projected rows only)")
+    ap.add_argument("--c4-two-call", action="store_true",
+                    help="C4 query as mbx_bitmap_cnf_async + mbx_materialize_async (default: one launch)")
     ap.add_argument("--c5-rows", default="125000000,1000000000", help="global rows, comma separated")
     args = ap.parse_args()
     # JSON lines only on stdout: libraries (RCCL's version banner) write to fd 1
@@ -200,9 +204,25 @@ def main():
         def and_():
             M._chk(L.mbx_bitmap_cnf_async(ctx.h, bms, offs, 2, None, out.h))
 
-        def query(k):
+        def query_two_call(k):
             and_()
             M._chk(L.mbx_materialize_async(ctx.h, t.h, out.h, proj, 2, ids.data_ptr(), outs, cnts.data_ptr() + 8 * k))
+
+        def query_fused(k, with_ids=False):  # one launch: CNF words + look-back + gather (+ positions)
+            M._chk(L.mbx_cnf_materialize_async(ctx.h, t.h, bms, offs, 2, None, proj, 2,
+                                               ids.data_ptr() if with_ids else None, outs, cnts.data_ptr() + 8 * k))
+
+        # the query: ColumnarIndexScan's output, the projected rows (its
+        # get_next returns tuples; the positions are an intermediate), in one
+        # launch; --c4-positions also writes the positions, --c4-two-call runs
+        # the two-launch form (AND BitSet, then positions + gather)
+        mode = "two_call" if args.c4_two_call else ("positions" if args.c4_positions else "projection")
+
+        def query(k):
+            if mode == "two_call":
+                query_two_call(k)
+            else:
+                query_fused(k, with_ids=mode == "positions")
             if comm is not None:
                 comm.allgather_count_async(cnts.data_ptr() + 8 * k, counts_all[k].data_ptr())
             else:
@@ -214,16 +234,34 @@ def main():
         got = int(cnts[-1].item())
         assert got == want and got <= cap, (got, want)
         assert bool((o0[:got] == c0[sel]).all()) and bool((o1[:got] == c1[sel]).all())
-        assert bool((ids[:got] == torch.nonzero(sel).flatten() + s).all())
         glob = got if world == 1 else int(D.combine_count(want))
         if world > 1:
             assert bool((counts_all[:, rank] == want).all()) and int(counts_all[-1].sum().item()) == glob
+        o0.zero_(), o1.zero_(), ids.zero_()
+        torch.cuda.synchronize()
+        proj_ms = kernel_ms(lambda: query_fused(0), steps, warmup)
+        pos_ms = kernel_ms(lambda: query_fused(0, with_ids=True), steps, warmup)
+        assert int(cnts[0].item()) == want
+        assert bool((o0[:got] == c0[sel]).all()) and bool((o1[:got] == c1[sel]).all())
+        assert bool((ids[:got] == torch.nonzero(sel).flatten() + s).all())
+        two_ms = kernel_ms(lambda: query_two_call(0), steps, warmup)
+        assert bool((ids[:got] == torch.nonzero(sel).flatten() + s).all())
         and_ms = kernel_ms(and_, steps, warmup)
         sel_ms = kernel_ms(lambda: M._chk(L.mbx_materialize_async(ctx.h, t.h, out.h, proj, 2, ids.data_ptr(), outs,
                                                                    cnts.data_ptr())), steps, warmup)
-        byts = 3 * N / 8 + glob * (8 + 8)
+        # algorithmic bytes: the two operand BitSets read once, the projected
+        # values (+ positions) written once; the two-call form also writes and
+        # re-reads the AND BitSet
+        byts = 2 * N / 8 + glob * 8 + (glob * 8 if mode != "projection" else 0) + (2 * N / 8 if mode == "two_call"
+                                                                                    else 0)
         emit({"config": "C4", "rows": N, "gpus": world, "rows_per_gpu": n, "selected": glob,
               "ms_per_query": ms, "rows_per_s": N / ms * 1e3, "algorithmic_gbs": byts / ms / 1e6,
+              "query": {"projection": "one launch (mbx_cnf_materialize_async): projected rows c0, c1",
+                        "positions": "one launch (mbx_cnf_materialize_async): positions + c0, c1",
+                        "two_call": "two launches (mbx_bitmap_cnf_async + mbx_materialize_async): positions + c0, c1"
+                        }[mode],
+              "kernel_ms": {"one_launch_projection": proj_ms, "one_launch_positions_and_projection": pos_ms,
+                            "two_launch_positions_and_projection": two_ms},
               "phases_ms": {"bitmap_and": and_ms, "positions_and_gather": sel_ms},
               "bitmap_and_gbs": 3 * n / 8 / and_ms / 1e6,
               "exchange": "none" if world == 1 else ("RCCL all-gather of per-rank counts (libmbx mbx_comm)"
