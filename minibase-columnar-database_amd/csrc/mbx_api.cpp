@@ -1427,7 +1427,8 @@ extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const m
     stamps = c->stamps;
   }
   HIPCHK(launch_cnf_materialize(C, deleted ? deleted->words : nullptr, nwords, t->nrows, c->lookback,
-                                t->row_offset, dev_ids, pc, dev_out, nproj, dev_count, c->stream, stamps));
+                                t->row_offset, dev_ids, pc, dev_out, nproj, dev_count, c->stream, stamps,
+                                c->tune.select_dbg >> 4));
   return MBX_OK;
 }
 

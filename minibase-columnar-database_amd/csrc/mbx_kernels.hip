@@ -1334,7 +1334,9 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
                                                        int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
                                                        int64_t* __restrict__ lb, int64_t row_offset,
                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                       Gather4 G, int64_t* __restrict__ stamps) {
+                                                       Gather4 G, int64_t* __restrict__ stamps, int32_t dbg) {
+  // dbg (diagnostic A/B, select_dbg >> 4): bit 0 polls with a 1024-clock
+  // back-off, bit 1 skips the look-back's wait (wrong output: its cost)
   // stamps (diagnostic, select_dbg bit 3): per block wall_clock64() at start /
   // count published / offset known / end
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
@@ -1444,8 +1446,11 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
 #pragma unroll
   for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
     const int64_t j = (int64_t)k * kBlock + threadIdx.x;
-    while ((v[k] >> 32) != epoch) {
-      __builtin_amdgcn_s_sleep(1);
+    while (!(dbg & 2) && (v[k] >> 32) != epoch) {
+      if (dbg & 1)
+        __builtin_amdgcn_s_sleep(16);
+      else
+        __builtin_amdgcn_s_sleep(1);
       v[k] = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     pre += v[k] & 0xffffffffll;
@@ -1902,7 +1907,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
-                                  int64_t* stamps) {
+                                  int64_t* stamps, int32_t dbg) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   if (nproj < 0 || nproj > 4) return hipErrorInvalidValue;
   Gather4 G{};
@@ -1920,10 +1925,10 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
 #define MBX_CNF_SELECT(NB)                                                                                  \
   if (nproj <= 2)                                                                                           \
     hipLaunchKernelGGL((k_cnf_select<2, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
-                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps);                    \
+                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg);                    \
   else                                                                                                      \
     hipLaunchKernelGGL((k_cnf_select<4, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
-                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps)
+                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg)
   switch (nbm) {
     case 1: MBX_CNF_SELECT(1); break;
     case 2: MBX_CNF_SELECT(2); break;

@@ -53,7 +53,8 @@ struct MbxTuning {
   int32_t distinct_lds_probes = -1;  // MBX_DISTINCT_LDS_PROBES
   int32_t gather_fused = 1;       // MBX_GATHER_FUSED: 0 = compaction, then k_gather (two launches)
   int32_t select_dbg = 0;         // MBX_SELECT_DBG: diagnostic k_select_ids variants (bit 0 no prefix,
-                                  // bit 1 no emission: wrong output) and bit 3 per-block stamps
+                                  // bit 1 no emission: wrong output), bit 3 per-block stamps, bits 4-5
+                                  // k_cnf_select look-back variants (16 back-off, 32 no wait: wrong output)
 };
 constexpr int64_t kMaxStampBlocks = 65536;
 

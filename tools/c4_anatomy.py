@@ -85,6 +85,20 @@ def main():
     assert int(cnt.item()) == want
     print(json.dumps({"part": "c4_times_us", "rows": n, "selected": want, **r}), flush=True)
 
+    # look-back variants (select_dbg bits 4-5): polls with a 1024-clock
+    # back-off; no wait at all (wrong output: the look-back's own cost)
+    for name, dbg in (("backoff", 16), ("no_wait", 32)):
+        ctx.set_tuning("select_dbg", dbg)
+        print(json.dumps({"part": "c4_lookback_variant", "variant": name,
+                          "one_launch_projection": timed(lambda: M._chk(L.mbx_cnf_materialize_async(
+                              ctx.h, t.h, bms, offs, 2, None, proj, 2, None, outs, cnt.data_ptr()))),
+                          "one_launch_no_columns_no_ids": timed(fused_count_only)}), flush=True)
+    ctx.set_tuning("reset", 0)
+    for _ in range(3):
+        fused()
+    ctx.sync()
+    assert int(cnt.item()) == want
+
     ctx.set_tuning("select_dbg", 8)
     for _ in range(5):
         fused()
