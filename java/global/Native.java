@@ -55,6 +55,10 @@ public final class Native {
   public static native long bitmapCnf(long ctx, long nbits, long[] bitmaps, int[] conjOffsets, long deleted)
       throws Exception;
   public static native long bitmapCombine(long ctx, int op, long a, long b) throws Exception;
+  /** ColumnarIndexScan in one launch: CNF + positions (devIds 0: none) + up to 4 int / float columns into
+   *  device slots (devAlloc); returns the selected row count (mbx_cnf_materialize_async) */
+  public static native long cnfMaterialize(long ctx, long table, long[] bitmaps, int[] conjOffsets, long deleted,
+                                           int[] proj, long devIds, long[] devOut, long devCount) throws Exception;
   public static native void bitmapFree(long bitmap);
 
   // late materialisation in batches (Iterator.get_next)

@@ -477,6 +477,49 @@ JNIEXPORT jlong JNICALL Java_global_Native_bitmapCnf(JNIEnv *env, jclass cls, jl
   return H(out);
 }
 
+/* ColumnarIndexScan in one launch: the CNF of index BitSets + positions (devIds 0: none) + up to 4 int /
+ * float projected columns into device slots (devAlloc); waits, returns the selected row count */
+JNIEXPORT jlong JNICALL Java_global_Native_cnfMaterialize(JNIEnv *env, jclass cls, jlong ctx, jlong table,
+                                                          jlongArray bms, jintArray conj_offsets, jlong deleted,
+                                                          jintArray proj, jlong dev_ids, jlongArray dev_out,
+                                                          jlong dev_count) {
+  (void)cls;
+  const jsize nb = (*env)->GetArrayLength(env, bms);
+  const jsize no = (*env)->GetArrayLength(env, conj_offsets);
+  const jsize np = (*env)->GetArrayLength(env, proj);
+  if (no < 1 || (*env)->GetArrayLength(env, dev_out) != np) {
+    throw_chain(env, kIndex, "cnfMaterialize: conj_offsets needs nconj + 1 entries, devOut one per column");
+    return 0;
+  }
+  const mbx_bitmap **v = (const mbx_bitmap **)calloc((size_t)(nb > 0 ? nb : 1), sizeof(void *));
+  void **outs = (void **)calloc((size_t)(np > 0 ? np : 1), sizeof(void *));
+  jlong *h = nb > 0 ? (*env)->GetLongArrayElements(env, bms, NULL) : NULL;
+  jint *o = (*env)->GetIntArrayElements(env, conj_offsets, NULL);
+  jint *pj = np > 0 ? (*env)->GetIntArrayElements(env, proj, NULL) : NULL;
+  jlong *d = np > 0 ? (*env)->GetLongArrayElements(env, dev_out, NULL) : NULL;
+  int64_t count = 0;
+  if (v && outs && o && (nb == 0 || h) && (np == 0 || (pj && d))) {
+    for (jsize i = 0; i < nb; i++) v[i] = P(const mbx_bitmap, h[i]);
+    for (jsize j = 0; j < np; j++) outs[j] = P(void, d[j]);
+    if (!check(env, mbx_cnf_materialize_async(P(mbx_ctx, ctx), P(const mbx_table, table), v, (const int32_t *)o,
+                                              (int32_t)(no - 1), P(const mbx_bitmap, deleted),
+                                              (const int32_t *)pj, (int32_t)np, P(int64_t, dev_ids), outs,
+                                              P(int64_t, dev_count)),
+               kIndex) &&
+        !check(env, mbx_sync(P(mbx_ctx, ctx)), kIndex))
+      check(env, mbx_dev_download(P(mbx_ctx, ctx), P(void, dev_count), &count, sizeof(count)), kChain);
+  } else {
+    throw_chain(env, kChain, "cnfMaterialize: host allocation");
+  }
+  if (h) (*env)->ReleaseLongArrayElements(env, bms, h, JNI_ABORT);
+  if (o) (*env)->ReleaseIntArrayElements(env, conj_offsets, o, JNI_ABORT);
+  if (pj) (*env)->ReleaseIntArrayElements(env, proj, pj, JNI_ABORT);
+  if (d) (*env)->ReleaseLongArrayElements(env, dev_out, d, JNI_ABORT);
+  free(v);
+  free(outs);
+  return count;
+}
+
 /* BitSet.and / or / andNot (MBX_BM_AND / _OR / _ANDNOT) */
 JNIEXPORT jlong JNICALL Java_global_Native_bitmapCombine(JNIEnv *env, jclass cls, jlong ctx, jint op, jlong a,
                                                          jlong b) {
