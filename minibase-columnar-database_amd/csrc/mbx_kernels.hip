@@ -1336,7 +1336,8 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
                                                        Gather4 G, int64_t* __restrict__ stamps, int32_t dbg) {
   // dbg (diagnostic A/B, select_dbg >> 4): bit 0 polls with a 1024-clock
-  // back-off, bit 1 skips the look-back's wait (wrong output: its cost)
+  // back-off, bit 1 skips the look-back's wait (wrong output: its cost),
+  // bit 2 takes the first poll round as plain nontemporal loads
   // stamps (diagnostic, select_dbg bit 3): per block wall_clock64() at start /
   // count published / offset known / end
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
@@ -1412,8 +1413,12 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
 #pragma unroll
   for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
     const int64_t j = (int64_t)k * kBlock + threadIdx.x;
-    v[k] = j < (int64_t)blockIdx.x ? __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : (epoch << 32);
+    if (j >= (int64_t)blockIdx.x)
+      v[k] = epoch << 32;
+    else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
+      v[k] = __builtin_nontemporal_load(&lb[1 + j]);
+    else
+      v[k] = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // meanwhile: stage the wave's leading steps together, load the first
   // kPrefetch x 64 rows' values

@@ -87,7 +87,7 @@ def main():
 
     # look-back variants (select_dbg bits 4-5): polls with a 1024-clock
     # back-off; no wait at all (wrong output: the look-back's own cost)
-    for name, dbg in (("backoff", 16), ("no_wait", 32)):
+    for name, dbg in (("backoff", 16), ("no_wait", 32), ("first_round_plain", 64)):
         ctx.set_tuning("select_dbg", dbg)
         print(json.dumps({"part": "c4_lookback_variant", "variant": name,
                           "one_launch_projection": timed(lambda: M._chk(L.mbx_cnf_materialize_async(
@@ -99,26 +99,33 @@ def main():
     ctx.sync()
     assert int(cnt.item()) == want
 
-    ctx.set_tuning("select_dbg", 8)
-    for _ in range(5):
-        fused()
-    ctx.sync()
-    nwords = (n + 63) // 64
-    wpb = (nwords + 1023) // 1024
-    nb = (nwords + wpb - 1) // wpb
-    st = np.zeros(4 * nb, dtype=np.int64)
-    M._chk(L.mbx_diag_select_stamps(ctx.h, st.ctypes.data, nb))
-    ctx.set_tuning("reset", 0)
-    st = st.reshape(nb, 4).astype(np.float64) * 10.0 / 1e3  # us
-    st -= st[:, 0].min()
-    q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]
-    dec = lambda col: [round(float(np.median(col[i * nb // 10:(i + 1) * nb // 10])), 2) for i in range(10)]
-    print(json.dumps({"part": "c4_stamps", "blocks": nb, "start": q(st[:, 0]), "published": q(st[:, 1]),
+    for label, fn, dbg in (("count_only", fused_count_only, 8), ("positions_and_projection", fused, 8),
+                           ("count_only_first_round_plain", fused_count_only, 8 | 64)):
+      ctx.set_tuning("select_dbg", dbg)
+      for _ in range(5):
+        fn()
+      ctx.sync()
+      nwords = (n + 63) // 64
+      wpb = (nwords + 1023) // 1024
+      nb = (nwords + wpb - 1) // wpb
+      st = np.zeros(4 * nb, dtype=np.int64)
+      M._chk(L.mbx_diag_select_stamps(ctx.h, st.ctypes.data, nb))
+      ctx.set_tuning("select_dbg", dbg & ~8)
+      ku = timed(fn)
+      ctx.set_tuning("reset", 0)
+      st = st.reshape(nb, 4).astype(np.float64) * 10.0 / 1e3  # us
+      st -= st[:, 0].min()
+      q = lambda x: [round(float(np.percentile(x, p)), 2) for p in (0, 10, 50, 90, 100)]
+      dec = lambda col: [round(float(np.median(col[i * nb // 10:(i + 1) * nb // 10])), 2) for i in range(10)]
+      print(json.dumps({"part": "c4_stamps", "form": label, "blocks": nb, "start": q(st[:, 0]),
+                      "published": q(st[:, 1]),
                       "offset_known": q(st[:, 2]), "end": q(st[:, 3]),
                       "words_phase": q(st[:, 1] - st[:, 0]), "lookback": q(st[:, 2] - st[:, 1]),
                       "write_phase": q(st[:, 3] - st[:, 2]),
                       "published_by_decile": dec(st[:, 1]), "offset_by_decile": dec(st[:, 2]),
-                      "end_by_decile": dec(st[:, 3])}), flush=True)
+                      "end_by_decile": dec(st[:, 3]),
+                      "kernel_us": ku}), flush=True)
+      ctx.set_tuning("reset", 0)
 
 
 if __name__ == "__main__":
