@@ -89,6 +89,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.distinct_lds_probes = (int32_t)env_knob("MBX_DISTINCT_LDS_PROBES", -1);
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
+  t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
 }
 
 static int ensure_partials(mbx_ctx* c, int64_t n) {
@@ -279,6 +280,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "distinct_lds_probes")) t.distinct_lds_probes = v;
   else if (!strcmp(knob, "select_dbg")) t.select_dbg = v;
   else if (!strcmp(knob, "gather_fused")) t.gather_fused = v;
+  else if (!strcmp(knob, "select_blocks")) t.select_blocks = v < 1 ? 1024 : (int32_t)v;
   else return fail(MBX_E_INVALID, "mbx_set_tuning: unknown knob `%s`", knob);
   return MBX_OK;
 }
@@ -1385,7 +1387,8 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
     if (sel->nseg <= kMaxStampBlocks) stamps = c->stamps;
   }
   HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segc, row_offset, dev_ids, pc, dev_out, nproj,
-                            dev_total, c->stream, c->tune.select_dbg & 3, stamps, c->tune.gather_fused != 0));
+                            dev_total, c->stream, c->tune.select_dbg & 3, stamps, c->tune.gather_fused != 0,
+                            c->tune.select_blocks));
   return MBX_OK;
 }
 

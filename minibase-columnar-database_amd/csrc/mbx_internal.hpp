@@ -304,7 +304,8 @@ hipError_t launch_count_sum(const int64_t* segc, int64_t n, int64_t* out, hipStr
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                               const int64_t* segc, int64_t row_offset, int64_t* ids,
                               const ProjCol* proj, void* const* out, int32_t nproj, int64_t* total,
-                              hipStream_t s, int32_t dbg = 0, int64_t* stamps = nullptr, bool fuse_gather = true);
+                              hipStream_t s, int32_t dbg = 0, int64_t* stamps = nullptr, bool fuse_gather = true,
+                              int64_t max_blocks = 1024);
 // 4-byte columns (int / float): also writes every output's segment counts
 hipError_t launch_index_build4(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
                                int32_t nvalues, uint64_t* const* outs, int64_t* const* segs, int64_t words_per_block,

@@ -1870,11 +1870,11 @@ hipError_t launch_count_sum(const int64_t* segc, int64_t n, int64_t* out, hipStr
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                               const int64_t* segc, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                               void* const* out, int32_t nproj, int64_t* total, hipStream_t s, int32_t dbg,
-                              int64_t* stamps, bool fuse_gather) {
+                              int64_t* stamps, bool fuse_gather, int64_t max_blocks) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
-  // ~1024 compaction blocks whatever the segment size: S segments per block
+  // ~max_blocks (1024) compaction blocks whatever the segment size: S segments per block
   const int64_t nseg = (nwords + words_per_block - 1) / words_per_block;
-  const int64_t S = (nseg + 1023) / 1024;
+  const int64_t S = (nseg + max_blocks - 1) / max_blocks;
   const int64_t wpb = S * words_per_block;
   const int64_t g = (nwords + wpb - 1) / wpb;
   // up to 4 int / float columns: gathered by the compaction itself (no
