@@ -1308,8 +1308,9 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
 // a sparse wave (C4: ~250 rows) needs one gather round trip, not one per
 // 64-word step.
 // lb[0] = the epoch of the previous launch; lb[1 + b] = epoch << 32 | count
-// of block b.  Every launch's epoch differs from the stale flags it finds,
-// so nothing is cleared between launches (graph replays included: the epoch
+// of block b (the last block stamps the flags past the grid too).  Every
+// launch's epoch differs from the stale flags it finds (they carry the
+// previous launch's), so nothing is cleared between launches (graph replays included: the epoch
 // is read from lb[0], not baked into the launch); the last block, having
 // seen every other block's flag (so every block has read lb[0]), stores the
 // new epoch.
@@ -1346,8 +1347,9 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   __shared__ uint16_t stage[kWaves][32 * 64];
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
+  // epochs 1 .. 2^31 - 1: epoch << 32 stays a positive int64
   const uint32_t prev = (uint32_t)lb[0];
-  const int64_t epoch = prev == 0xffffffffu ? 1 : (int64_t)prev + 1;
+  const int64_t epoch = prev >= 0x7fffffffu ? 1 : (int64_t)prev + 1;
   const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
   const int64_t s1 = min(s0 + words_per_block, nwords);
   const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
@@ -1467,9 +1469,14 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
   for (int k = 0; k < kWaves; ++k) off += wpre[k];
-  if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) {
-    *total = off + bc;
-    lb[0] = epoch;
+  if (blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x == 0) {
+      *total = off + bc;
+      lb[0] = epoch;
+    }
+    // the flags of blocks this launch does not have carry its epoch too, so a
+    // later, larger launch never finds a flag older than the previous launch
+    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += kBlock) lb[1 + j] = epoch << 32;
   }
   for (int k = 0; k < wave; ++k) off += wcount[k];
   if (cached) {

@@ -233,3 +233,21 @@ def test_cnf_materialize_rejects_what_it_cannot_fuse(ctx, m):
     B = ctx.bitmap_upload(n + 1, words_of(np.ones(n + 1, dtype=bool)))
     with pytest.raises(m.MbxError):  # bitmap / table size mismatch
         ctx.cnf_materialize_async(t, [[B]], [0], None, [buf.data_ptr()], cnt.data_ptr())
+
+
+def test_cnf_materialize_grid_sizes_alternate(ctx):
+    """launches of different grid sizes on one context (small tables use few
+    blocks, so flags past their grid must never be mistaken for this
+    launch's): every result exact"""
+    runs = []
+    for n in (100, 3_000_017, 5_000, 3_000_017, 64, 1_000_003, 70_001, 3_000_017):
+        rng = np.random.Generator(np.random.PCG64(n))
+        a, b = rng.random(n) < 0.3, rng.random(n) < 0.6
+        A, B = ctx.bitmap_upload(n, words_of(a)), ctx.bitmap_upload(n, words_of(b))
+        cols, t = table(ctx, n, 3)
+        runs.append((n, A, B, cols, t, np.nonzero(a & b)[0]))
+    for _ in range(2):
+        for n, A, B, cols, t, pos in runs:
+            ids, (o0,), k = run(ctx, t, [[A], [B]], [0])
+            assert k == len(pos), n
+            assert np.array_equal(ids, pos) and np.array_equal(o0, np.asarray(cols[0][2])[pos]), n
