@@ -169,9 +169,19 @@ def main():
         got = int(cnt.item())
         assert got == want, (got, want)
         assert bool((ids[:got] == torch.nonzero(cols[0] < 104858).flatten()).all())
+        # the same queries replayed from a HIP graph of 10 (mbx_graph_*: no host launches between them)
+        ctx.sync()
+        ctx.graph_begin()
+        for _ in range(10):
+            step()
+        gr = ctx.graph_end()
+        graph_ms = kernel_ms(gr.launch, max(1, args.steps // 10), 2) / 10
+        gr.close()
+        assert int(cnt.item()) == want
         scan_ms = kernel_ms(lambda: ctx.scan_bitmap_async(plan, bm), args.steps, args.warmup)
         byts = n * 4 + n / 8 + got * 8
         emit({"config": "C2", "rows": n, "gpus": 1, "selected": got, "ms_per_query": ms, "rows_per_s": n / ms * 1e3,
+              "graph_replay_ms_per_query": graph_ms,
               "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
               "scan_gbs": (n * 4 + n / 8) / scan_ms / 1e6})
         del cols, t, plan, bm, ids
