@@ -288,7 +288,7 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
                                   int64_t* stamps = nullptr, int32_t dbg = 0);
-constexpr int64_t kLookbackWords = 1 + 1024;  // epoch, per-block counts
+constexpr int64_t kLookbackWords = 1 + 2 * 1024;  // epoch, per-block counts, per-block inclusive prefixes
 hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                              int64_t words_per_block, uint64_t* out, int64_t* segc, hipStream_t s);
 hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* b, int64_t nwords,

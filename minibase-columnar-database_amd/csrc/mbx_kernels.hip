@@ -1336,9 +1336,13 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
                                                        int64_t* __restrict__ lb, int64_t row_offset,
                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
                                                        Gather4 G, int64_t* __restrict__ stamps, int32_t dbg) {
-  // dbg (diagnostic A/B, select_dbg >> 4): bit 0 polls with a 1024-clock
-  // back-off, bit 1 skips the look-back's wait (wrong output: its cost),
-  // bit 2 takes the first poll round as plain nontemporal loads
+  // dbg bit 3: the chained look-back -- each block also publishes its
+  // inclusive prefix, and wave 0 walks back 64 predecessors per round to the
+  // nearest published one (~4 flag lines per block instead of every
+  // predecessor's); without it, every thread polls its predecessors' counts
+  // (diagnostic A/B of that form, select_dbg >> 4: bit 0 polls with a
+  // 1024-clock back-off, bit 1 skips the look-back's wait (wrong output: its
+  // cost), bit 2 takes the first poll round as plain nontemporal loads)
   // stamps (diagnostic, select_dbg bit 3): per block wall_clock64() at start /
   // count published / offset known / end
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
@@ -1348,6 +1352,7 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
   // epochs 1 .. 2^31 - 1: epoch << 32 stays a positive int64
+  int64_t* const inc = lb + 1 + kLookbackBlocks;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
   const uint32_t prev = (uint32_t)lb[0];
   const int64_t epoch = prev >= 0x7fffffffu ? 1 : (int64_t)prev + 1;
   const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
@@ -1415,7 +1420,7 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
 #pragma unroll
   for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
     const int64_t j = (int64_t)k * kBlock + threadIdx.x;
-    if (j >= (int64_t)blockIdx.x)
+    if ((dbg & 8) || j >= (int64_t)blockIdx.x)
       v[k] = epoch << 32;
     else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
       v[k] = __builtin_nontemporal_load(&lb[1 + j]);
@@ -1450,6 +1455,40 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
     }
   }
   int64_t pre = 0;
+  if (dbg & 8) {
+    // chained form: wave 0 reads 64 predecessors per round (one line group),
+    // stops at the nearest one whose inclusive prefix is published and adds
+    // the counts after it; other waves contribute 0
+    if (wave == 0) {
+      int64_t e = blockIdx.x;
+      while (e > 0) {
+        const int64_t j = e - 64 + lane;
+        const bool live = j >= 0;
+        int64_t in = live ? __hip_atomic_load(&inc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        int64_t a = live ? __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (epoch << 32);
+        for (;;) {
+          const bool ok_in = live && (in >> 32) == epoch;
+          const bool ok_a = (a >> 32) == epoch;
+          const uint64_t im = __ballot(ok_in);
+          if (im) {
+            const int L = 63 - __clzll((long long)im);
+            if (!__any(lane > L && !ok_a)) {
+              pre += lane == L ? (in & 0xffffffffll) : (lane > L ? (a & 0xffffffffll) : 0);
+              e = 0;
+              break;
+            }
+          } else if (!__any(!ok_a)) {
+            pre += a & 0xffffffffll;
+            e -= 64;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          if (live && !ok_in) in = __hip_atomic_load(&inc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!ok_a) a = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
     const int64_t j = (int64_t)k * kBlock + threadIdx.x;
@@ -1462,6 +1501,7 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
     }
     pre += v[k] & 0xffffffffll;
   }
+  }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
   if (lane == 0) wpre[wave] = pre;
@@ -1469,6 +1509,8 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
   for (int k = 0; k < kWaves; ++k) off += wpre[k];
+  if ((dbg & 8) && threadIdx.x == 0)
+    __hip_atomic_store(&inc[blockIdx.x], (epoch << 32) | (off + bc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x == gridDim.x - 1) {
     if (threadIdx.x == 0) {
       *total = off + bc;
@@ -1476,7 +1518,10 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
     }
     // the flags of blocks this launch does not have carry its epoch too, so a
     // later, larger launch never finds a flag older than the previous launch
-    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += kBlock) lb[1 + j] = epoch << 32;
+    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += kBlock) {
+      lb[1 + j] = epoch << 32;
+      if (dbg & 8) inc[j] = epoch << 32;
+    }
   }
   for (int k = 0; k < wave; ++k) off += wcount[k];
   if (cached) {
@@ -1933,6 +1978,10 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   const int64_t wpb = (nwords + kLookbackBlocks - 1) / kLookbackBlocks;
   const int64_t g = (nwords + wpb - 1) / wpb;
   const int nbm = c.conj_off[c.nconj];
+  // kernel dbg bit 3 = the chained look-back (default): inclusive prefixes
+  // are 32-bit, so tables of >= 2^32 rows poll every predecessor, as does
+  // select_dbg bit 7 (the A/B knob: MBX_SELECT_DBG=128)
+  dbg = (dbg & ~8) | ((!(dbg & 8) && nbits < (int64_t(1) << 32)) ? 8 : 0);
   // the prefetch registers sized to the projection: <= 2 columns or <= 4
 #define MBX_CNF_SELECT(NB)                                                                                  \
   if (nproj <= 2)                                                                                           \

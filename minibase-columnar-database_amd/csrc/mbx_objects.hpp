@@ -55,7 +55,8 @@ struct MbxTuning {
   int32_t select_blocks = 1024;   // MBX_SELECT_BLOCKS: compaction blocks at most (segments per block = nseg / this)
   int32_t select_dbg = 0;         // MBX_SELECT_DBG: diagnostic k_select_ids variants (bit 0 no prefix,
                                   // bit 1 no emission: wrong output), bit 3 per-block stamps, bits 4-5
-                                  // k_cnf_select look-back variants (16 back-off, 32 no wait: wrong output)
+                                  // k_cnf_select look-back variants (16 back-off, 32 no wait: wrong output,
+                                  // 128 every-predecessor poll instead of the chained look-back)
 };
 constexpr int64_t kMaxStampBlocks = 65536;
 
