@@ -1,5 +1,6 @@
-# k_cnf_select chained look-back (MBX_SELECT_DBG=128) vs the all-predecessor
-# poll: its parity tests under the knob, then C4 A/B/A/B
+# First A/B of k_cnf_select's chained look-back, run while it was opt-in
+# (MBX_SELECT_DBG=128 selected it then; it is the default now and the knob
+# selects the every-predecessor poll -- see tools/gpu_r2_chain2.sh)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${TAG:-r2_chain}
