@@ -230,11 +230,13 @@ int mbx_bitmap_index_build(mbx_ctx *ctx, const mbx_table *t, int32_t col, const 
 
 /* ColumnarIndexScan end to end in ONE kernel launch (R/index/ColumnarIndexScan.java:130-181, then the
  * nextSetBit + getRecord loop :287-308): the CNF of index BitSets exactly as mbx_bitmap_cnf (the CNF's
- * BitSet itself is never stored), then the positions (dev_ids, may be NULL) and the values of up to 4
- * projected 4-byte (int / float) columns of every selected row, as mbx_materialize_async, and the
- * count in *dev_count.  Each block publishes its count and takes its output offset from its
- * predecessors' counts (decoupled look-back) -- the one-launch form of mbx_bitmap_cnf_async +
- * mbx_materialize_async.  Strings or > 4 columns: MBX_E_UNSUPPORTED (use the two calls). */
+ * BitSet itself is never stored), then the positions (dev_ids, may be NULL) and the rows of the
+ * projected columns (proj: 0-based, at most 16; dev_out[j] receives column proj[j] in the table's
+ * device row layout -- 4 bytes for int / float, the padded device string image for char(n), as
+ * mbx_materialize_async) of every selected row, and the count in *dev_count.  Each block publishes its
+ * count and takes its output offset from its predecessors' counts (decoupled look-back) -- the
+ * one-launch form of mbx_bitmap_cnf_async + mbx_materialize_async.  Up to 4 four-byte columns are
+ * loaded into registers before the look-back resolves; other projections copy rows. */
 int mbx_cnf_materialize_async(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *const *bms,
                               const int32_t *conj_offsets, int32_t nconj, const mbx_bitmap *deleted,
                               const int32_t *proj, int32_t nproj, int64_t *dev_ids,
@@ -266,6 +268,27 @@ int mbx_cursor_next(mbx_cursor *c, int64_t max_rows, int64_t *host_ids, void *co
                     int64_t *n);
 int mbx_cursor_restart(mbx_cursor *c); /* Iterator.restart() */
 int mbx_cursor_close(mbx_cursor *c);   /* Iterator.close(), idempotent via free */
+/* Delivery is double buffered: mbx_cursor_next returns batch k from pinned
+ * host memory and has already enqueued the device -> host copy of batch k+1
+ * (same max_rows) into a second pinned buffer, so the caller's consumption of
+ * batch k overlaps the copy.  Statistics: rows handed out so far, bytes copied
+ * device -> host (no reference counterpart). */
+int mbx_cursor_stats(const mbx_cursor *c, int64_t *delivered, int64_t *d2h_bytes);
+/* ColumnarIndexScan (R/index/ColumnarIndexScan.java:79-182 + get_next :287-308) as a cursor in ONE
+ * kernel launch: the CNF of index BitSets (as mbx_bitmap_cnf) straight into the cursor's positions and
+ * projected rows (k_cnf_select, as mbx_cnf_materialize_async, any projection); mbx_cursor_next then
+ * hands out get_next() batches in nextSetBit order. */
+int mbx_cnf_cursor_open(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *const *bms,
+                        const int32_t *conj_offsets, int32_t nconj, const mbx_bitmap *deleted,
+                        const int32_t *proj, int32_t nproj, mbx_cursor **out);
+/* The same, launch only: the cursor's rows are written on the context
+ * stream, the count lands in the cursor's device slot *dev_count (may be
+ * NULL) -- e.g. for mbx_comm_allgather_count_async, whose result gives every
+ * shard its offset in the concatenated stream; the first mbx_cursor_count or
+ * mbx_cursor_next waits for it.  One launch per GPU, all GPUs in flight. */
+int mbx_cnf_cursor_launch(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *const *bms,
+                          const int32_t *conj_offsets, int32_t nconj, const mbx_bitmap *deleted,
+                          const int32_t *proj, int32_t nproj, mbx_cursor **out, int64_t **dev_count);
 
 /* ---- multi-GPU: row-range shards + one RCCL combine over xGMI ------------
  * SURVEY.md 8(e), DESIGN.md section 6.  The reference engine is one process

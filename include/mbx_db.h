@@ -156,6 +156,24 @@ int mbx_db_bitmap_stage(mbx_ctx* ctx, mbx_db* db, const char* filename, int64_t 
  * positions (Columnarfile.java:480-482 raises the same). */
 int mbx_db_stage(mbx_ctx* ctx, mbx_db* db, const char* name, mbx_table** out);
 
+/* One shard of a Columnarfile: positions [row_begin, row_end) (row_begin a
+ * multiple of 64, row_end clipped to the file's positions) staged exactly as
+ * mbx_db_stage stages the whole file -- same decode, same deleted rows -- into
+ * a table with row_offset = row_begin.  Only the directory pages and this
+ * range's data pages are read and copied: the shards of one file can be
+ * staged by one process per GPU, or one process driving every GPU, without
+ * any of them holding the others' rows (TupleScan / heap.Scan over a
+ * position range, R/columnar/TupleScan.java:29-89, R/heap/Heapfile.java:262-289). */
+int mbx_db_stage_range(mbx_ctx* ctx, mbx_db* db, const char* name, int64_t row_begin, int64_t row_end,
+                       mbx_table** out);
+
+/* Bits [bit_begin, bit_begin + nbits) of BitMapFile `filename` (bit_begin a
+ * multiple of 64) as a device bitmap of nbits bits: one shard's slice of
+ * BitMapFile.getBitSet() (BM.readBitSet, R/bitmap/BM.java:179-215) for a
+ * table staged with mbx_db_stage_range. */
+int mbx_db_bitmap_stage_range(mbx_ctx* ctx, mbx_db* db, const char* filename, int64_t bit_begin, int64_t nbits,
+                              mbx_bitmap** out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -189,7 +189,7 @@ static int cnf_of(JNIEnv *env, jobjectArray filter, mbx_condexpr *conds, int32_t
 
 JNIEXPORT jint JNICALL Java_global_Native_deviceCount(JNIEnv *env, jclass cls) {
   int32_t n = 0;
-  (void)cls;
+  (void)env, (void)cls;
   if (mbx_device_count(&n)) return 0;
   return n;
 }

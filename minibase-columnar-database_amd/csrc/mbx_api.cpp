@@ -1392,6 +1392,27 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
   return MBX_OK;
 }
 
+// the projection of a one-launch ColumnarIndexScan: any columns (<= kMaxProj)
+// in their device row layout (4 bytes; char(n): stride_w words)
+static int cnf_proj_args(const mbx_table* t, const int32_t* proj, int32_t nproj, void* const* dev_out, ProjCol* pc) {
+  if (nproj < 0 || nproj > kMaxProj)
+    return fail(MBX_E_UNSUPPORTED, "cnf_materialize: %d columns (max %d)", nproj, kMaxProj);
+  if (nproj > 0) {
+    NOTNULL(proj);
+    NOTNULL(dev_out);
+  }
+  for (int32_t j = 0; j < nproj; j++) {
+    if (proj[j] < 0 || proj[j] >= (int32_t)t->cols.size())
+      return fail(MBX_E_RANGE, "cnf_materialize: column %d outside 0..%zu", proj[j], t->cols.size() - 1);
+    const TCol& tc = t->cols[(size_t)proj[j]];
+    if (!dev_out[j]) return fail(MBX_E_INVALID, "cnf_materialize: dev_out[%d] null", j);
+    pc[j].base = tc.dev;
+    pc[j].stride_w = tc.stride_w;
+    pc[j].pad_ = 0;
+  }
+  return MBX_OK;
+}
+
 extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* const* bms,
                                          const int32_t* conj_offsets, int32_t nconj, const mbx_bitmap* deleted,
                                          const int32_t* proj, int32_t nproj, int64_t* dev_ids,
@@ -1402,26 +1423,8 @@ extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const m
   BitmapCnf C;
   int rc = cnf_args(t->nrows, bms, conj_offsets, nconj, deleted, &C);
   if (rc) return rc;
-  if (nproj < 0 || nproj > 4)
-    return fail(MBX_E_UNSUPPORTED, "cnf_materialize: %d columns (0..4; more: mbx_bitmap_cnf_async + "
-                "mbx_materialize_async)", nproj);
-  ProjCol pc[4];
-  if (nproj > 0) {
-    NOTNULL(proj);
-    NOTNULL(dev_out);
-  }
-  for (int32_t j = 0; j < nproj; j++) {
-    if (proj[j] < 0 || proj[j] >= (int32_t)t->cols.size())
-      return fail(MBX_E_RANGE, "cnf_materialize: column %d outside 0..%zu", proj[j], t->cols.size() - 1);
-    const TCol& tc = t->cols[(size_t)proj[j]];
-    if (tc.attr_type == MBX_ATTR_STRING || tc.stride_w != 1)
-      return fail(MBX_E_UNSUPPORTED, "cnf_materialize: column %d is not a 4-byte column (strings: "
-                  "mbx_bitmap_cnf_async + mbx_materialize_async)", proj[j]);
-    if (!dev_out[j]) return fail(MBX_E_INVALID, "cnf_materialize: dev_out[%d] null", j);
-    pc[j].base = tc.dev;
-    pc[j].stride_w = 1;
-    pc[j].pad_ = 0;
-  }
+  ProjCol pc[kMaxProj];
+  if ((rc = cnf_proj_args(t, proj, nproj, dev_out, pc))) return rc;
   if ((rc = set_device(c))) return rc;
   const int64_t nwords = (t->nrows + 63) >> 6;
   int64_t* stamps = nullptr;
@@ -1516,11 +1519,66 @@ extern "C" int mbx_cursor_open(mbx_ctx* c, const mbx_table* t, const mbx_bitmap*
   return MBX_OK;
 }
 
-extern "C" int mbx_cursor_count(const mbx_cursor* k, int64_t* count) {
-  NOTNULL(k);
+// a launched CNF cursor: wait for its launch and read the count
+static int cursor_resolve(mbx_cursor* k) {
+  if (!k->count_pending) return MBX_OK;
+  mbx_ctx* c = k->ctx;
+  int rc = set_device(c);
+  if (rc) return rc;
+  int64_t* h = (int64_t*)c->pinned + 20;
+  HIPCHK(hipMemcpyAsync(h, k->dcount, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  k->count_pending = false;
+  k->count = *h;
+  if (k->count < 0 || k->count > k->bound)  // cannot happen: the bound holds for any CNF
+    return fail(MBX_E_DEVICE, "cnf_cursor: %lld rows outside the bound %lld", (long long)k->count,
+                (long long)k->bound);
+  return MBX_OK;
+}
+
+extern "C" int mbx_cursor_count(const mbx_cursor* kc, int64_t* count) {
+  NOTNULL(kc);
   NOTNULL(count);
+  mbx_cursor* k = const_cast<mbx_cursor*>(kc);
+  if (int rc = cursor_resolve(k)) return rc;
   *count = k->count;
   return MBX_OK;
+}
+
+// enqueue the device -> pinned copies of rows [from, from + n) into pin[b]
+static int cursor_fetch(mbx_cursor* k, int b, int64_t from, int64_t n) {
+  mbx_ctx* c = k->ctx;
+  uint8_t* dst = k->pin[b];
+  HIPCHK(hipMemcpyAsync(dst, k->ids + from, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  dst += (size_t)k->batch_rows * sizeof(int64_t);
+  int64_t bytes = n * (int64_t)sizeof(int64_t);
+  for (size_t j = 0; j < k->outs.size(); j++) {
+    const int64_t w = col_bytes(k->t, k->proj[j]);
+    HIPCHK(hipMemcpyAsync(dst, (uint8_t*)k->outs[j] + from * w, (size_t)(n * w), hipMemcpyDeviceToHost, c->stream));
+    dst += (size_t)(k->batch_rows * w);
+    bytes += n * w;
+  }
+  HIPCHK(hipEventRecord(k->ev[b], c->stream));
+  k->d2h_bytes += bytes;
+  return MBX_OK;
+}
+
+// wait for (and forget) a batch still in flight
+static int cursor_drain(mbx_cursor* k) {
+  if (k->pf_start < 0) return MBX_OK;
+  k->pf_start = -1;
+  HIPCHK(hipEventSynchronize(k->ev[k->pf_buf]));
+  return MBX_OK;
+}
+
+static void cursor_release_pinned(mbx_cursor* k) {
+  for (int b = 0; b < 2; b++) {
+    if (k->ev[b]) hipEventDestroy(k->ev[b]);
+    if (k->pin[b]) hipHostFree(k->pin[b]);
+    k->ev[b] = nullptr;
+    k->pin[b] = nullptr;
+  }
+  k->batch_rows = 0;
 }
 
 extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_ids, void* const* host_out,
@@ -1529,34 +1587,58 @@ extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_id
   NOTNULL(n);
   *n = 0;
   if (max_rows <= 0) return fail(MBX_E_INVALID, "cursor_next: max_rows %lld", (long long)max_rows);
+  if (int rc0 = cursor_resolve(k)) return rc0;
   const int64_t take = k->count - k->next < max_rows ? k->count - k->next : max_rows;
   if (take <= 0) return MBX_OK;  // end of stream: get_next() returns null
   mbx_ctx* c = k->ctx;
   int rc = set_device(c);
   if (rc) return rc;
   const mbx_table* t = k->t;
-  if (host_ids)
-    HIPCHK(hipMemcpyAsync(host_ids, k->ids + k->next, (size_t)take * sizeof(int64_t), hipMemcpyDeviceToHost,
-                          c->stream));
-  std::vector<std::vector<uint8_t>> imgs(k->outs.size());
+  // pinned batch buffers, sized to the largest batch asked for so far
+  const int64_t rows = max_rows < k->count ? max_rows : k->count;
+  if (k->batch_rows < rows) {
+    if ((rc = cursor_drain(k))) return rc;
+    cursor_release_pinned(k);
+    int64_t row_bytes = (int64_t)sizeof(int64_t);
+    for (size_t j = 0; j < k->outs.size(); j++) row_bytes += col_bytes(t, k->proj[j]);
+    for (int b = 0; b < 2; b++) {
+      HIPCHK(hipHostMalloc((void**)&k->pin[b], (size_t)(rows * row_bytes), hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&k->ev[b], hipEventDisableTiming));
+    }
+    k->batch_rows = rows;
+  }
+  int b;
+  if (k->pf_start == k->next && k->pf_n >= take) {
+    b = k->pf_buf;  // this batch is already on its way
+    k->pf_start = -1;
+  } else {
+    if ((rc = cursor_drain(k))) return rc;
+    b = k->pf_buf ^ 1;
+    if ((rc = cursor_fetch(k, b, k->next, take))) return rc;
+  }
+  // the following batch into the other buffer, before this one is consumed
+  const int64_t nxt = k->next + take;
+  const int64_t m = k->count - nxt < max_rows ? k->count - nxt : max_rows;
+  HIPCHK(hipEventSynchronize(k->ev[b]));
+  if (m > 0) {
+    if ((rc = cursor_fetch(k, b ^ 1, nxt, m))) return rc;
+    k->pf_start = nxt;
+    k->pf_n = m;
+    k->pf_buf = b ^ 1;
+  }
+  const uint8_t* src = k->pin[b];
+  if (host_ids) memcpy(host_ids, src, (size_t)take * sizeof(int64_t));
+  src += (size_t)k->batch_rows * sizeof(int64_t);
   for (size_t j = 0; j < k->outs.size(); j++) {
-    if (!host_out || !host_out[j]) continue;
     const TCol& tc = t->cols[(size_t)k->proj[j]];
     const int64_t w = (int64_t)tc.stride_w * 4;
-    if (tc.attr_type == MBX_ATTR_STRING) {
-      imgs[j].resize((size_t)(take * w));
-      HIPCHK(hipMemcpyAsync(imgs[j].data(), (uint8_t*)k->outs[j] + k->next * w, (size_t)(take * w),
-                            hipMemcpyDeviceToHost, c->stream));
-    } else {
-      HIPCHK(hipMemcpyAsync(host_out[j], (uint8_t*)k->outs[j] + k->next * w, (size_t)(take * w),
-                            hipMemcpyDeviceToHost, c->stream));
+    if (host_out && host_out[j]) {
+      if (tc.attr_type == MBX_ATTR_STRING)
+        unpack_rows(tc, src, take, host_out[j]);
+      else
+        memcpy(host_out[j], src, (size_t)(take * w));
     }
-  }
-  HIPCHK(hipStreamSynchronize(c->stream));
-  for (size_t j = 0; j < k->outs.size(); j++) {
-    if (!host_out || !host_out[j]) continue;
-    const TCol& tc = t->cols[(size_t)k->proj[j]];
-    if (tc.attr_type == MBX_ATTR_STRING) unpack_rows(tc, imgs[j].data(), take, host_out[j]);
+    src += (size_t)(k->batch_rows * w);
   }
   k->next += take;
   *n = take;
@@ -1565,18 +1647,111 @@ extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_id
 
 extern "C" int mbx_cursor_restart(mbx_cursor* k) {
   NOTNULL(k);
+  int rc = cursor_drain(k);
   k->next = 0;
-  return MBX_OK;
+  return rc;
 }
 
 extern "C" int mbx_cursor_close(mbx_cursor* k) {
   if (!k) return MBX_OK;
   hipSetDevice(k->ctx->device);
   hipStreamSynchronize(k->ctx->stream);
+  cursor_release_pinned(k);
+  hipFree(k->dcount);
   hipFree(k->ids);
   for (void* d : k->outs) hipFree(d);
   delete k;
   return MBX_OK;
+}
+
+extern "C" int mbx_cursor_stats(const mbx_cursor* k, int64_t* delivered, int64_t* d2h_bytes) {
+  NOTNULL(k);
+  if (delivered) *delivered = k->next;
+  if (d2h_bytes) *d2h_bytes = k->d2h_bytes;
+  return MBX_OK;
+}
+
+// ColumnarIndexScan end to end into a cursor: one k_cnf_select launch writes
+// the positions and projected rows of the CNF's selection into the cursor's
+// device buffers (no BitSet stored, no second launch), then get_next()
+// batches come out of mbx_cursor_next.  The buffers are sized by an upper
+// bound of the count: min over conjuncts of the sum of their bitmaps'
+// cardinalities (OR <= sum, AND <= min), at most the table's rows.
+extern "C" int mbx_cnf_cursor_launch(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* const* bms,
+                                     const int32_t* conj_offsets, int32_t nconj, const mbx_bitmap* deleted,
+                                     const int32_t* proj, int32_t nproj, mbx_cursor** out, int64_t** dev_count) {
+  NOTNULL(c);
+  NOTNULL(t);
+  NOTNULL(out);
+  *out = nullptr;
+  if (dev_count) *dev_count = nullptr;
+  if (c->capturing) return fail(MBX_E_INVALID, "cnf_cursor: inside a graph capture (it allocates)");
+  BitmapCnf C;
+  int rc = cnf_args(t->nrows, bms, conj_offsets, nconj, deleted, &C);
+  if (rc) return rc;
+  if (nproj < 0 || nproj > kMaxProj) return fail(MBX_E_UNSUPPORTED, "cnf_cursor: %d columns (max %d)", nproj, kMaxProj);
+  if (nproj > 0) NOTNULL(proj);
+  for (int32_t j = 0; j < nproj; j++)
+    if (proj[j] < 0 || proj[j] >= (int32_t)t->cols.size())
+      return fail(MBX_E_RANGE, "cnf_cursor: column %d outside 0..%zu", proj[j], t->cols.size() - 1);
+  if ((rc = set_device(c))) return rc;
+  int64_t bound = t->nrows;
+  for (int32_t cj = 0; cj < nconj; cj++) {
+    int64_t s = 0;
+    for (int32_t k = conj_offsets[cj]; k < conj_offsets[cj + 1] && s < bound; k++) {
+      mbx_bitmap* b = const_cast<mbx_bitmap*>(bms[k]);
+      if ((rc = ensure_count(c, b))) return rc;
+      s += b->count;
+    }
+    if (s < bound) bound = s;
+  }
+  mbx_cursor* k = new (std::nothrow) mbx_cursor();
+  if (!k) return fail(MBX_E_NOMEM, "cnf_cursor: host allocation");
+  k->ctx = c;
+  k->t = t;
+  k->bound = bound;
+  const size_t cap = (size_t)(bound > 0 ? bound : 1);
+  hipError_t e = hipMalloc(&k->dcount, sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc(&k->ids, cap * sizeof(int64_t));
+  for (int32_t j = 0; j < nproj && e == hipSuccess; j++) {
+    void* d = nullptr;
+    e = hipMalloc(&d, cap * (size_t)col_bytes(t, proj[j]));
+    k->outs.push_back(d);
+    k->proj.push_back(proj[j]);
+  }
+  if (e != hipSuccess) {
+    mbx_cursor_close(k);
+    return fail(MBX_E_NOMEM, "cnf_cursor: %s", hipGetErrorString(e));
+  }
+  ProjCol pc[kMaxProj];
+  for (int32_t j = 0; j < nproj; j++) {
+    pc[j].base = t->cols[(size_t)proj[j]].dev;
+    pc[j].stride_w = t->cols[(size_t)proj[j]].stride_w;
+    pc[j].pad_ = 0;
+  }
+  e = launch_cnf_materialize(C, deleted ? deleted->words : nullptr, (t->nrows + 63) >> 6, t->nrows, c->lookback,
+                             t->row_offset, k->ids, pc, k->outs.data(), nproj, k->dcount, c->stream, nullptr,
+                             c->tune.select_dbg >> 4);
+  if (e != hipSuccess) {
+    mbx_cursor_close(k);
+    return fail(MBX_E_DEVICE, "cnf_cursor: %s", hipGetErrorString(e));
+  }
+  k->count_pending = true;
+  if (dev_count) *dev_count = k->dcount;
+  *out = k;
+  return MBX_OK;
+}
+
+extern "C" int mbx_cnf_cursor_open(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* const* bms,
+                                   const int32_t* conj_offsets, int32_t nconj, const mbx_bitmap* deleted,
+                                   const int32_t* proj, int32_t nproj, mbx_cursor** out) {
+  int rc = mbx_cnf_cursor_launch(c, t, bms, conj_offsets, nconj, deleted, proj, nproj, out, nullptr);
+  if (rc) return rc;
+  if ((rc = cursor_resolve(*out))) {
+    mbx_cursor_close(*out);
+    *out = nullptr;
+  }
+  return rc;
 }
 
 extern "C" int mbx_bitmap_select(mbx_ctx* c, const mbx_bitmap* b, int64_t row_offset, int64_t* host_ids, int64_t cap,

@@ -961,7 +961,7 @@ extern "C" int mbx_db_stage(mbx_ctx* c, mbx_db* db, const char* name, mbx_table*
   for (int32_t i = 0; i < n && e == hipSuccess; ++i) {
     const ColumnPages& cp = cps[(size_t)i];
     const TCol& tc = t->cols[(size_t)i];
-    PageDecodeArgs A;
+    PageDecodeArgs A{};
     A.image = dimg;
     A.image_pages = image_pages;
     A.page_of = dpage_of + pofs;
@@ -1010,6 +1010,258 @@ extern "C" int mbx_db_stage(mbx_ctx* c, mbx_db* db, const char* name, mbx_table*
   }
   *out = t;
   return MBX_OK;
+}
+
+// ------------------------------------------------- row-range staging (shards)
+
+namespace {
+
+// the column's highest position + 1 from its directory and the slot counts
+// of its last non-empty data pages only (column_pages reads every data
+// page's header; a shard must not touch the other shards' pages)
+int column_pages_lazy(mbx_db* db, const std::string& file, int32_t rec_len, ColumnPages* cp) {
+  const int32_t first = get_file_entry(db, file);
+  if (first == kInvalidPage) return fail(MBX_E_INVALID, "heapfile %s is missing", file.c_str());
+  int rc = heap_pages(db, first, &cp->pages);
+  if (rc) return rc;
+  cp->rec_len = rec_len;
+  cp->recs_per_page = recs_per_data_page(rec_len);
+  int64_t npi = 0;
+  for (const DataPage& d : cp->pages) npi = std::max(npi, d.index + 1);
+  cp->page_of.assign((size_t)npi, kInvalidPage);
+  for (const DataPage& d : cp->pages) {
+    cp->page_of[(size_t)d.index] = d.pid;
+    cp->records += d.recct;
+  }
+  for (int64_t pi = npi - 1; pi >= 0; --pi) {
+    const int32_t pid = cp->page_of[(size_t)pi];
+    if (pid == kInvalidPage) continue;
+    const int32_t cnt = get16(db->page(pid) + kSlotCnt);
+    if (cnt < 0 || cnt > cp->recs_per_page)
+      return fail(MBX_E_INVALID, "%s: data page %d holds %d slots (max %d)", file.c_str(), pid, cnt,
+                  cp->recs_per_page);
+    if (cnt > 0) {
+      cp->nrows = pi * cp->recs_per_page + cnt;
+      break;
+    }
+  }
+  return MBX_OK;
+}
+
+}  // namespace
+
+extern "C" int mbx_db_stage_range(mbx_ctx* c, mbx_db* db, const char* name, int64_t row_begin, int64_t row_end,
+                                  mbx_table** out) {
+  NOTNULL(c);
+  NOTNULL(db);
+  NOTNULL(name);
+  NOTNULL(out);
+  *out = nullptr;
+  if (row_begin < 0 || (row_begin & 63) || row_end < row_begin)
+    return fail(MBX_E_INVALID, "db_stage_range: rows [%lld, %lld) (begin must be a multiple of 64)",
+                (long long)row_begin, (long long)row_end);
+  Schema sc;
+  int rc = read_schema(db, name, &sc);
+  if (rc) return rc;
+  const int32_t n = sc.ncols;
+  std::vector<ColumnPages> cps((size_t)n);
+  int64_t total = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if ((rc = column_pages_lazy(db, std::string(name) + "." + std::to_string(i), record_len(sc.cols[(size_t)i]),
+                                &cps[(size_t)i])))
+      return rc;
+    total = std::max(total, cps[(size_t)i].nrows);
+  }
+  const int64_t r0 = std::min(row_begin, total), r1 = std::min(row_end, total);
+  const int64_t nrows = r1 - r0;
+  const int64_t nwords = words_for(nrows);
+  // per column: the page indices covering [r0, r1) and their pages, packed
+  // into one compact image in page-index order (runs of consecutive pids
+  // copied together)
+  std::vector<int64_t> pi0((size_t)n, 0);
+  std::vector<std::vector<int32_t>> local_of((size_t)n);  // page index - pi0 -> image page (-1: none)
+  std::vector<int32_t> image_pids;
+  for (int32_t i = 0; i < n && nrows > 0; ++i) {
+    const ColumnPages& cp = cps[(size_t)i];
+    const int64_t a = r0 / cp.recs_per_page, b = (r1 - 1) / cp.recs_per_page;
+    pi0[(size_t)i] = a;
+    local_of[(size_t)i].assign((size_t)(b - a + 1), -1);
+    for (int64_t pi = a; pi <= b && pi < (int64_t)cp.page_of.size(); ++pi) {
+      const int32_t pid = cp.page_of[(size_t)pi];
+      if (pid == kInvalidPage) continue;
+      local_of[(size_t)i][(size_t)(pi - a)] = (int32_t)image_pids.size();
+      image_pids.push_back(pid);
+    }
+  }
+  // cf.md bits [r0, r1) (r0 is a multiple of 64: whole words)
+  std::vector<uint8_t> md_bytes;
+  const int32_t md = get_file_entry(db, std::string(name) + ".md");
+  if (md != kInvalidPage && (rc = bm_read_bytes(db, md, &md_bytes))) return rc;
+  std::vector<uint64_t> mdw;
+  {
+    const int64_t have = ((int64_t)md_bytes.size() + 7) / 8;
+    const int64_t w0 = r0 / 64, nw = std::max<int64_t>(0, std::min(have - w0, nwords));
+    mdw.assign((size_t)(nw > 0 ? nw : 0), 0ull);
+    for (int64_t w = 0; w < nw; ++w) {
+      const size_t byte0 = (size_t)(w0 + w) * 8;
+      const size_t len = std::min<size_t>(8, md_bytes.size() - byte0);
+      memcpy(&mdw[(size_t)w], md_bytes.data() + byte0, len);
+    }
+  }
+  const int64_t md_words = (int64_t)mdw.size();
+
+  mbx_table* t = nullptr;
+  if ((rc = table_alloc(c, sc.cols.data(), n, nrows, r0, true, &t))) return rc;
+  const int64_t image_pages = (int64_t)image_pids.size();
+  uint8_t* dimg = nullptr;
+  int32_t* dpage_of = nullptr;
+  uint64_t* dpresent = nullptr;
+  uint64_t* dmd = nullptr;
+  int32_t* dflags = nullptr;
+  int64_t npi_total = 0;
+  for (const auto& l : local_of) npi_total += (int64_t)l.size();
+  const int64_t pw = nwords > 0 ? nwords : 1;
+  void* pinned = nullptr;
+  const size_t chunk = (size_t)32 << 20;
+  hipStream_t s = c->stream;
+  hipError_t e = hipMalloc(&dimg, (size_t)(image_pages > 0 ? image_pages : 1) * kPage);
+  if (e == hipSuccess) e = hipMalloc(&dpage_of, sizeof(int32_t) * (size_t)(npi_total > 0 ? npi_total : 1));
+  if (e == hipSuccess) e = hipMalloc(&dpresent, sizeof(uint64_t) * (size_t)pw * (size_t)n);
+  if (e == hipSuccess) e = hipMalloc(&dmd, sizeof(uint64_t) * (size_t)(md_words > 0 ? md_words : 1));
+  if (e == hipSuccess) e = hipMalloc(&dflags, sizeof(int32_t) * 2);
+  if (e == hipSuccess) e = hipHostMalloc(&pinned, 2 * chunk, hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMemsetAsync(dpresent, 0, sizeof(uint64_t) * (size_t)pw * (size_t)n, s);
+  if (e == hipSuccess) e = hipMemsetAsync(dflags, 0, sizeof(int32_t) * 2, s);
+  for (int32_t i = 0; i < n && e == hipSuccess; ++i) {
+    const TCol& tc = t->cols[(size_t)i];
+    e = hipMemsetAsync(tc.dev, 0, (size_t)(nrows > 0 ? nrows : 1) * (size_t)tc.stride_w * 4, s);
+  }
+  // this shard's pages only, through two pinned chunks
+  {
+    hipEvent_t done[2] = {nullptr, nullptr};
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&done[0], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&done[1], hipEventDisableTiming);
+    const int64_t per_chunk = (int64_t)(chunk / kPage);
+    int k = 0;
+    for (int64_t p0 = 0; p0 < image_pages && e == hipSuccess; p0 += per_chunk, k ^= 1) {
+      const int64_t np = std::min(per_chunk, image_pages - p0);
+      e = hipEventSynchronize(done[k]);
+      uint8_t* buf = (uint8_t*)pinned + (size_t)k * chunk;
+      for (int64_t j = 0; j < np && e == hipSuccess;) {
+        int64_t run = 1;
+        while (j + run < np && image_pids[(size_t)(p0 + j + run)] == image_pids[(size_t)(p0 + j)] + run) ++run;
+        memcpy(buf + (size_t)j * kPage, db->page(image_pids[(size_t)(p0 + j)]), (size_t)run * kPage);
+        j += run;
+      }
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(dimg + (size_t)p0 * kPage, buf, (size_t)np * kPage, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipEventRecord(done[k], s);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (done[0]) hipEventDestroy(done[0]);
+    if (done[1]) hipEventDestroy(done[1]);
+  }
+  std::vector<int32_t> page_of;
+  page_of.reserve((size_t)npi_total);
+  for (const auto& l : local_of) page_of.insert(page_of.end(), l.begin(), l.end());
+  if (e == hipSuccess && npi_total > 0)
+    e = hipMemcpy(dpage_of, page_of.data(), sizeof(int32_t) * page_of.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && md_words > 0)
+    e = hipMemcpy(dmd, mdw.data(), sizeof(uint64_t) * (size_t)md_words, hipMemcpyHostToDevice);
+  int64_t pofs = 0;
+  for (int32_t i = 0; i < n && e == hipSuccess && nrows > 0; ++i) {
+    const ColumnPages& cp = cps[(size_t)i];
+    const TCol& tc = t->cols[(size_t)i];
+    PageDecodeArgs A{};
+    A.image = dimg;
+    A.image_pages = image_pages;
+    A.page_of = dpage_of + pofs;
+    A.npages = (int64_t)local_of[(size_t)i].size();
+    A.rec_len = cp.rec_len;
+    A.recs_per_page = cp.recs_per_page;
+    A.kind = tc.attr_type == MBX_ATTR_STRING ? kStr : (tc.attr_type == MBX_ATTR_REAL ? kReal : kInt);
+    A.size = tc.size;
+    A.stride = tc.stride_w * 4;
+    A.out = (uint8_t*)tc.dev;
+    A.present = dpresent + (size_t)pw * (size_t)i;
+    A.nrows = nrows;
+    A.err = dflags;
+    A.page_index0 = pi0[(size_t)i];
+    A.pos_begin = r0;
+    A.range = 1;
+    e = launch_page_decode(A, s);
+    pofs += A.npages;
+  }
+  if (e == hipSuccess && nrows > 0)
+    e = launch_present_merge(dpresent, dpresent + pw, n - 1, pw, dmd, md_words, nrows, t->deleted, dflags + 1, s);
+  int32_t flags[2] = {0, 0};
+  if (e == hipSuccess) e = hipMemcpyAsync(flags, dflags, sizeof(flags), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  hipFree(dimg);
+  hipFree(dpage_of);
+  hipFree(dpresent);
+  hipFree(dmd);
+  hipFree(dflags);
+  if (pinned) hipHostFree(pinned);
+  if (e != hipSuccess) {
+    mbx_table_free(t);
+    return fail(MBX_E_DEVICE, "db_stage_range %s: %s", name, hipGetErrorString(e));
+  }
+  if (flags[0]) {
+    mbx_table_free(t);
+    return fail(MBX_E_INVALID, "db_stage_range %s: malformed data pages (flags 0x%x)", name, flags[0]);
+  }
+  if (flags[1] & 1) {
+    mbx_table_free(t);
+    return fail(MBX_E_INVALID, "Invalid position calculations: the column heapfiles of %s disagree", name);
+  }
+  if (!(flags[1] & 2) && t->deleted) {
+    hipFree(t->deleted);
+    t->deleted = nullptr;
+    t->owns_deleted = false;
+  }
+  *out = t;
+  return MBX_OK;
+}
+
+extern "C" int mbx_db_bitmap_stage_range(mbx_ctx* c, mbx_db* db, const char* filename, int64_t bit_begin,
+                                         int64_t nbits, mbx_bitmap** out) {
+  NOTNULL(c);
+  NOTNULL(db);
+  NOTNULL(filename);
+  NOTNULL(out);
+  *out = nullptr;
+  if (nbits < 0 || bit_begin < 0 || (bit_begin & 63))
+    return fail(MBX_E_INVALID, "bitmap_stage_range: bits [%lld, +%lld) (begin must be a multiple of 64)",
+                (long long)bit_begin, (long long)nbits);
+  const int32_t head = get_file_entry(db, filename);
+  if (head == kInvalidPage) return fail(MBX_E_INVALID, "The file %s does not exist.", filename);
+  const int64_t nw = words_for(nbits);
+  std::vector<uint64_t> words((size_t)(nw > 0 ? nw : 1), 0ull);
+  uint8_t* wb = reinterpret_cast<uint8_t*>(words.data());
+  // BM.readBitSet's concatenation of the chain's records, keeping only the
+  // bytes of [bit_begin / 8, bit_begin / 8 + 8 * nw)
+  const int64_t b0 = bit_begin / 8, b1 = b0 + nw * 8;
+  int64_t at = 0;  // byte offset of the current record in the concatenation
+  int32_t p = head;
+  int guard = 0;
+  while (p != kInvalidPage && at < b1) {
+    if (p < 0 || p >= db->num_pages || guard++ > db->num_pages)
+      return fail(MBX_E_INVALID, "BitMapFile chain leaves the DB at page %d", p);
+    const uint8_t* pg = db->page(p);
+    const int32_t cnt = get16(pg + kSlotCnt);
+    int32_t sl = 0;
+    while (sl < cnt && hf_slot_len(pg, sl) == -1) ++sl;
+    if (sl == cnt) return fail(MBX_E_INVALID, "InvalidSlotNumberException: BitMapFile page %d holds no record", p);
+    const int32_t len = hf_slot_len(pg, sl), off = hf_slot_off(pg, sl);
+    if (len < 0 || off + len > kPage) return fail(MBX_E_INVALID, "corrupt BitMapFile page %d", p);
+    const int64_t lo = std::max(at, b0), hi = std::min(at + len, b1);
+    if (lo < hi) memcpy(wb + (lo - b0), pg + off + (lo - at), (size_t)(hi - lo));
+    at += len;
+    p = get32(pg + kNext);
+  }
+  if (nbits & 63) words[(size_t)nw - 1] &= (1ull << (nbits & 63)) - 1ull;
+  return mbx_bitmap_upload(c, nbits, words.data(), out);
 }
 
 // ------------------------------------------------- bitmap-index persistence

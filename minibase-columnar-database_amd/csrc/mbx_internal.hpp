@@ -187,6 +187,14 @@ struct PageDecodeArgs {
   uint64_t* present;         // BitSet of positions that hold a record
   int64_t nrows;
   int32_t* err;              // bit flags of malformed pages
+  // row-range staging (mbx_db_stage_range): page_of[i] is page index
+  // page_index0 + i, output row r is position pos_begin + r; positions
+  // outside [pos_begin, pos_begin + nrows) are another shard's (range = 1:
+  // skipped, not an error)
+  int64_t page_index0;
+  int64_t pos_begin;
+  int32_t range;
+  int32_t pad2_;
 };
 
 hipError_t launch_page_decode(const PageDecodeArgs& A, hipStream_t s);

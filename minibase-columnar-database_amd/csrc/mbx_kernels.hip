@@ -499,10 +499,43 @@ struct Gather4 {
   int32_t n;  // projected columns (0: positions only)
 };
 
-template <int G4>
+// Any projection (ColumnarIndexScan's out_indexes with char(n) columns, or
+// more than 4 columns): template argument G4 == kWide.  Column g's rows are
+// sw[g] 32-bit words (the device row image: 1 for int / float, stride_w for
+// char(n)); a lane copies its row's words, all loads before the stores.
+constexpr int kWide = -1;
+struct GatherW {
+  const uint32_t* col[kMaxProj];
+  uint32_t* out[kMaxProj];
+  int32_t sw[kMaxProj];
+  int32_t n;
+};
+
+__device__ __forceinline__ void wide_row(const GatherW& G, int64_t p, int64_t o) {
+  for (int g = 0; g < G.n; ++g) {
+    const int sw = G.sw[g];
+    const uint32_t* __restrict__ s = G.col[g] + p * sw;
+    uint32_t* __restrict__ d = G.out[g] + o * sw;
+    if (sw == 1) {
+      d[0] = s[0];
+      continue;
+    }
+    int k = 0;
+    for (; k + 4 <= sw; k += 4) {
+      const uint32_t a = s[k], b = s[k + 1], c = s[k + 2], e = s[k + 3];
+      d[k] = a;
+      d[k + 1] = b;
+      d[k + 2] = c;
+      d[k + 3] = e;
+    }
+    for (; k < sw; ++k) d[k] = s[k];
+  }
+}
+
+template <int G4, class GT = Gather4>
 __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const StepScan& r, int64_t& off,
                                            int64_t row_offset, int64_t* __restrict__ ids, const uint16_t* st,
-                                           int lane, const Gather4& G, uint32_t first = 0) {
+                                           int lane, const GT& G, uint32_t first = 0) {
   if (r.total == 0) return;
   const int64_t lbase = base * 64;  // table-local row of bit 0 of word `base`
   if (r.total <= kStageIds) {
@@ -512,23 +545,32 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
       const bool two = i1 < r.total;
       const int64_t p0 = lbase + st[i0];
       const int64_t p1 = two ? lbase + st[i1] : p0;
-      uint32_t v0[G4 > 0 ? G4 : 1], v1[G4 > 0 ? G4 : 1];
-#pragma unroll
-      for (int g = 0; g < G4; ++g)
-        if (g < G.n) {
-          v0[g] = (uint32_t)G.col[g][p0];
-          v1[g] = (uint32_t)G.col[g][p1];
+      if constexpr (G4 == kWide) {
+        if (ids) {
+          ids[off + i0] = row_offset + p0;
+          if (two) ids[off + i1] = row_offset + p1;
         }
-      if (ids) {
-        ids[off + i0] = row_offset + p0;
-        if (two) ids[off + i1] = row_offset + p1;
+        wide_row(G, p0, off + i0);
+        if (two) wide_row(G, p1, off + i1);
+      } else {
+        uint32_t v0[G4 > 0 ? G4 : 1], v1[G4 > 0 ? G4 : 1];
+#pragma unroll
+        for (int g = 0; g < G4; ++g)
+          if (g < G.n) {
+            v0[g] = (uint32_t)G.col[g][p0];
+            v1[g] = (uint32_t)G.col[g][p1];
+          }
+        if (ids) {
+          ids[off + i0] = row_offset + p0;
+          if (two) ids[off + i1] = row_offset + p1;
+        }
+#pragma unroll
+        for (int g = 0; g < G4; ++g)
+          if (g < G.n) {
+            G.out[g][off + i0] = v0[g];
+            if (two) G.out[g][off + i1] = v1[g];
+          }
       }
-#pragma unroll
-      for (int g = 0; g < G4; ++g)
-        if (g < G.n) {
-          G.out[g][off + i0] = v0[g];
-          if (two) G.out[g][off + i1] = v1[g];
-        }
     }
     __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next step
   } else {
@@ -543,20 +585,24 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
         const int64_t p = lbase + j * 64 + lane;
         const int64_t o = off + slot + below;
         if (ids) ids[o] = row_offset + p;
+        if constexpr (G4 == kWide) {
+          wide_row(G, p, o);
+        } else {
 #pragma unroll
-        for (int g = 0; g < G4; ++g)
-          if (g < G.n) G.out[g][o] = (uint32_t)G.col[g][p];
+          for (int g = 0; g < G4; ++g)
+            if (g < G.n) G.out[g][o] = (uint32_t)G.col[g][p];
+        }
       }
     }
   }
   off += r.total;
 }
 
-template <int G4 = 0>
+template <int G4 = 0, class GT = Gather4>
 __device__ __forceinline__ void emit_step(int64_t base, uint64_t mw, int64_t& off, int64_t row_offset,
-                                          int64_t* __restrict__ ids, uint16_t* st, int lane, const Gather4& G) {
+                                          int64_t* __restrict__ ids, uint16_t* st, int lane, const GT& G) {
   const StepScan r = stage_step(mw, st, lane);
-  store_step<G4>(base, mw, r, off, row_offset, ids, st, lane, G);
+  store_step<G4, GT>(base, mw, r, off, row_offset, ids, st, lane, G);
 }
 
 // ------------------------------------------------------------- fast scan
@@ -1330,12 +1376,14 @@ __device__ __forceinline__ uint64_t cnf_word(const BitmapCnf& C, int64_t w) {
   return r;
 }
 
-template <int G4, int NB>  // G4: projected columns the registers hold; NB: 1..4 operands batched, 0: any
+// G4: projected 4-byte columns the registers hold (kWide: any projection,
+// GT = GatherW); NB: 1..4 operands batched, 0: any
+template <int G4, int NB, class GT = Gather4>
 __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
                                                        int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
                                                        int64_t* __restrict__ lb, int64_t row_offset,
                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                       Gather4 G, int64_t* __restrict__ stamps, int32_t dbg) {
+                                                       GT G, int64_t* __restrict__ stamps, int32_t dbg) {
   // dbg bit 3: the chained look-back -- each block also publishes its
   // inclusive prefix, and wave 0 walks back 64 predecessors per round to the
   // nearest published one (~4 flag lines per block instead of every
@@ -1443,14 +1491,16 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
       tot += q.total;
       nst = r + 1;
     }
+    if constexpr (G4 != kWide) {
 #pragma unroll
-    for (int k = 0; k < kPrefetch; ++k) {
-      const uint32_t i = (uint32_t)lane + 64u * k;
-      if (i < tot) {
-        const int64_t p = a0 * 64 + st[i];
+      for (int k = 0; k < kPrefetch; ++k) {
+        const uint32_t i = (uint32_t)lane + 64u * k;
+        if (i < tot) {
+          const int64_t p = a0 * 64 + st[i];
 #pragma unroll
-        for (int g = 0; g < G4; ++g)
-          if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p];
+          for (int g = 0; g < G4; ++g)
+            if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p];
+        }
       }
     }
   }
@@ -1532,23 +1582,27 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
       const uint32_t i = (uint32_t)lane + 64u * k;
       if (i < tot) {
         if (ids) ids[off + i] = row_offset + a0 * 64 + st[i];
+        if constexpr (G4 == kWide) {
+          wide_row(G, a0 * 64 + st[i], off + i);
+        } else {
 #pragma unroll
-        for (int g = 0; g < G4; ++g)
-          if (g < G.n) G.out[g][off + i] = pv[k][g];
+          for (int g = 0; g < G4; ++g)
+            if (g < G.n) G.out[g][off + i] = pv[k][g];
+        }
       }
     }
     const StepScan all{0u, tot};
-    store_step<G4>(a0, 0ull, all, off, row_offset, ids, st, lane, G, 64u * kPrefetch);
+    store_step<G4, GT>(a0, 0ull, all, off, row_offset, ids, st, lane, G, 64u * kPrefetch);
 #pragma unroll
     for (int r = 0; r < kSelRegs; ++r) {
       const int64_t base = a0 + r * 64;
       if (r < nst) continue;
       if (base >= a1) break;
-      emit_step<G4>(base, wr[r], off, row_offset, ids, st, lane, G);
+      emit_step<G4, GT>(base, wr[r], off, row_offset, ids, st, lane, G);
     }
   } else {
     for (int64_t base = a0; base < a1; base += 64)
-      emit_step<G4>(base, base + lane < a1 ? word_at(base + lane) : 0ull, off, row_offset, ids, st, lane, G);
+      emit_step<G4, GT>(base, base + lane < a1 ? word_at(base + lane) : 0ull, off, row_offset, ids, st, lane, G);
   }
   if (stamps) {
     __syncthreads();
@@ -1966,14 +2020,25 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
                                   int64_t* stamps, int32_t dbg) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
-  if (nproj < 0 || nproj > 4) return hipErrorInvalidValue;
+  if (nproj < 0 || nproj > kMaxProj) return hipErrorInvalidValue;
+  // <= 4 four-byte columns: values prefetched in registers (Gather4); any
+  // other projection (char(n) rows, more columns): row copies (GatherW)
+  bool narrow = nproj <= 4;
+  for (int j = 0; j < nproj; ++j) narrow = narrow && proj[j].stride_w == 1;
   Gather4 G{};
+  GatherW W{};
   for (int j = 0; j < nproj; ++j) {
-    if (proj[j].stride_w != 1) return hipErrorInvalidValue;
-    G.col[j] = (const int32_t*)proj[j].base;
-    G.out[j] = (uint32_t*)out[j];
+    if (proj[j].stride_w < 1) return hipErrorInvalidValue;
+    if (narrow) {
+      G.col[j] = (const int32_t*)proj[j].base;
+      G.out[j] = (uint32_t*)out[j];
+    }
+    W.col[j] = (const uint32_t*)proj[j].base;
+    W.out[j] = (uint32_t*)out[j];
+    W.sw[j] = proj[j].stride_w;
   }
-  G.n = nproj;
+  G.n = narrow ? nproj : 0;
+  W.n = nproj;
   // <= kLookbackBlocks blocks: one poll load per thread per 256 predecessors
   const int64_t wpb = (nwords + kLookbackBlocks - 1) / kLookbackBlocks;
   const int64_t g = (nwords + wpb - 1) / wpb;
@@ -1984,7 +2049,10 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   dbg = (dbg & ~8) | ((!(dbg & 8) && nbits < (int64_t(1) << 32)) ? 8 : 0);
   // the prefetch registers sized to the projection: <= 2 columns or <= 4
 #define MBX_CNF_SELECT(NB)                                                                                  \
-  if (nproj <= 2)                                                                                           \
+  if (!narrow)                                                                                              \
+    hipLaunchKernelGGL((k_cnf_select<kWide, NB, GatherW>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, \
+                       nwords, tail_mask_of(nbits), wpb, lb, row_offset, ids, total, W, stamps, dbg);            \
+  else if (nproj <= 2)                                                                                      \
     hipLaunchKernelGGL((k_cnf_select<2, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
                        tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg);                    \
   else                                                                                                      \

@@ -134,6 +134,21 @@ struct mbx_cursor {
   int64_t* ids = nullptr;  // device
   std::vector<void*> outs; // device, one per projected column
   std::vector<int32_t> proj;
+  // double-buffered delivery (mbx_cursor_next): while the caller consumes
+  // batch k, batch k+1 is already on its way into the other pinned buffer.
+  // A pinned batch = ids (batch_rows x 8 B), then each column's device rows.
+  uint8_t* pin[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  int64_t batch_rows = 0;   // rows a pinned buffer holds
+  int64_t pf_start = -1;    // first row of the batch in flight into pin[pf_buf] (-1: none)
+  int64_t pf_n = 0;
+  int pf_buf = 0;
+  int64_t d2h_bytes = 0;    // statistics: bytes copied device -> pinned
+  // mbx_cnf_cursor_launch: the count is still on the device (in dcount)
+  // until the first mbx_cursor_count / mbx_cursor_next reads it
+  int64_t* dcount = nullptr;
+  int64_t bound = 0;        // capacity of ids / outs (rows)
+  bool count_pending = false;
 };
 
 namespace mbx {

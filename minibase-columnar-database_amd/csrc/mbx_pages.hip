@@ -55,13 +55,13 @@ __global__ __launch_bounds__(kBlock) void k_page_decode(PageDecodeArgs A) {
         const uint32_t se = ld_be32a(pg + kDbSlotBase + 4 * k);
         const int32_t len = (int32_t)(int16_t)(se >> 16);
         const int32_t off = (int32_t)(se & 0xFFFFu);
-        const int64_t pos = pi * A.recs_per_page + k;
+        const int64_t pos = (A.page_index0 + pi) * A.recs_per_page + k - A.pos_begin;  // output row
         if (len == -1) {
           // EMPTY_SLOT: no record at this position
         } else if (len != A.rec_len || off < kDbSlotBase || off + len > kDbPage) {
           err |= 4;
-        } else if (pos >= A.nrows) {
-          err |= 8;
+        } else if (pos < 0 || pos >= A.nrows) {
+          if (!A.range) err |= 8;  // range staging: another shard's position
         } else {
           const uint8_t* rec = pg + off;
           ok = true;
@@ -107,11 +107,18 @@ __global__ __launch_bounds__(kBlock) void k_page_decode(PageDecodeArgs A) {
       }
       const uint64_t m = __ballot(ok);
       if (lane == 0 && m) {
-        const int64_t base = pi * A.recs_per_page + k0;
-        const int sh = (int)(base & 63);
-        unsigned long long* w = reinterpret_cast<unsigned long long*>(A.present) + (base >> 6);
-        atomicOr(w, (unsigned long long)(m << sh));
-        if (sh && (m >> (64 - sh))) atomicOr(w + 1, (unsigned long long)(m >> (64 - sh)));
+        const int64_t base = (A.page_index0 + pi) * A.recs_per_page + k0 - A.pos_begin;
+        unsigned long long* w0 = reinterpret_cast<unsigned long long*>(A.present);
+        if (base >= 0) {
+          const int sh = (int)(base & 63);
+          unsigned long long* w = w0 + (base >> 6);
+          atomicOr(w, (unsigned long long)(m << sh));
+          if (sh && (m >> (64 - sh))) atomicOr(w + 1, (unsigned long long)(m >> (64 - sh)));
+        } else if (base > -64) {
+          // the page starts before this shard (range staging): lanes below
+          // -base hold another shard's positions and are not in m
+          atomicOr(w0, (unsigned long long)(m >> (-base)));
+        }
       }
     }
   }

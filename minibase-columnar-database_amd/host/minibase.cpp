@@ -601,6 +601,51 @@ static void fill_row(heap::Tuple& J, const std::vector<AttrType>& types, const s
   }
 }
 
+void CursorBatches::reset(mbx_cursor* c, const std::vector<AttrType>& types, const std::vector<short>& sizes,
+                          const std::vector<int32_t>& cols) {
+  close();
+  cur_ = c;
+  types_ = types;
+  sizes_ = sizes;
+  cols_ = cols;
+  batch_.assign(cols.size(), {});
+  for (size_t j = 0; j < cols.size(); j++) batch_[j].resize((size_t)(kRows * col_width(types, sizes, cols[j])));
+  ids_.assign((size_t)kRows, 0);
+  n_ = i_ = 0;
+}
+
+int64_t CursorBatches::count() const {
+  int64_t n = 0;
+  if (cur_) chk<FileScanException>(mbx_cursor_count(cur_, &n), "cursor count");
+  return n;
+}
+
+bool CursorBatches::next() {
+  if (!cur_) return false;
+  if (i_ >= n_) {
+    std::vector<void*> ptrs(cols_.size());
+    for (size_t j = 0; j < cols_.size(); j++) ptrs[j] = batch_[j].data();
+    chk<FileScanException>(mbx_cursor_next(cur_, kRows, ids_.data(), ptrs.data(), &n_), "get_next");
+    i_ = 0;
+    if (n_ == 0) return false;
+  }
+  i_++;
+  return true;
+}
+
+void CursorBatches::fill(heap::Tuple& J) const { fill_row(J, types_, sizes_, cols_, batch_, i_ - 1); }
+
+void CursorBatches::restart() {
+  if (cur_) chk<FileScanException>(mbx_cursor_restart(cur_), "restart");
+  n_ = i_ = 0;
+}
+
+void CursorBatches::close() {
+  if (cur_) mbx_cursor_close(cur_);
+  cur_ = nullptr;
+  n_ = i_ = 0;
+}
+
 ColumnarFileScan::ColumnarFileScan(const std::string& file_name, const std::vector<AttrType>& in1,
                                    const std::vector<short>& s1_sizes, short len_in1, int n_out_flds,
                                    const std::vector<FldSpec>& proj_list, CondExpr* const* outFilter)
@@ -865,24 +910,48 @@ static BitSetPtr or_bitmaps(const columnar::Columnarfile& cf, const std::vector<
   return std::make_shared<columnar::DeviceBitSet>(out);
 }
 
-static void materialize_all(const columnar::Columnarfile& cf, const BitSetPtr& sel, const std::vector<int>& cols,
-                            std::vector<int64_t>& ids, std::vector<std::vector<uint8_t>>& vals) {
-  const auto types = cf.getAttributeTypes();
-  const auto sizes = cf.getAttrSizes();
-  const int64_t n = sel->cardinality();
-  ids.assign((size_t)(n > 0 ? n : 1), 0);
-  vals.assign(cols.size(), {});
-  std::vector<void*> ptrs(cols.size());
-  std::vector<int32_t> pc(cols.begin(), cols.end());
-  for (size_t j = 0; j < cols.size(); j++) {
-    vals[j].resize((size_t)((n > 0 ? n : 1) * iterator::col_width(types, sizes, cols[j])));
-    ptrs[j] = vals[j].data();
+static bool trace_on() {
+  static const bool on = getenv("MBX_TRACE") && atoi(getenv("MBX_TRACE")) != 0;
+  return on;
+}
+
+// ColumnarIndexScan / ColumnIndexScan get_next() in ONE kernel launch: the
+// CNF over the conjuncts' bitmaps (minus cf.md), the positions and the
+// projected rows straight into a cursor (mbx_cnf_cursor_open, k_cnf_select)
+static mbx_cursor* cnf_cursor(const columnar::Columnarfile& cf, const std::vector<std::vector<BitSetPtr>>& conjuncts,
+                              const std::vector<int>& cols, const char* who) {
+  std::vector<mbx_bitmap*> bms;
+  std::vector<int32_t> offs{0};
+  for (const auto& conj : conjuncts) {
+    for (const auto& b : conj) bms.push_back(b->get());
+    offs.push_back((int32_t)bms.size());
   }
-  int64_t got = 0;
-  chk<IndexException>(mbx_materialize(global::SystemDefs::ctx(), cf.table(), sel->get(), pc.data(), (int32_t)pc.size(),
-                                      ids.data(), ptrs.data(), (int64_t)ids.size(), &got),
-                      "late materialisation");
-  ids.resize((size_t)got);
+  std::vector<int32_t> pc(cols.begin(), cols.end());
+  BitSetPtr del = cf.getMarkedDeleted();
+  mbx_cursor* c = nullptr;
+  chk<IndexException>(mbx_cnf_cursor_open(global::SystemDefs::ctx(), cf.table(), bms.data(), offs.data(),
+                                          (int32_t)conjuncts.size(), del ? del->get() : nullptr, pc.data(),
+                                          (int32_t)pc.size(), &c),
+                      std::string(who) + ": one-launch CNF + projection");
+  if (trace_on()) {
+    int64_t n = 0;
+    mbx_cursor_count(c, &n);
+    fprintf(stderr, "trace: %s: one launch (k_cnf_select), %zu conjuncts, %zu bitmaps, %lld rows\n", who,
+            conjuncts.size(), bms.size(), (long long)n);
+  }
+  return c;
+}
+
+// a cursor over a BitSet the reference's step-wise objects produced
+static mbx_cursor* bitset_cursor(const columnar::Columnarfile& cf, const BitSetPtr& sel, const std::vector<int>& cols,
+                                 const char* who) {
+  std::vector<int32_t> pc(cols.begin(), cols.end());
+  mbx_cursor* c = nullptr;
+  chk<IndexException>(mbx_cursor_open(global::SystemDefs::ctx(), cf.table(), sel->get(), pc.data(), (int32_t)pc.size(),
+                                      &c),
+                      std::string(who) + ": late materialisation");
+  if (trace_on()) fprintf(stderr, "trace: %s: step-wise BitSets + materialise\n", who);
+  return c;
 }
 
 ColumnIndexScan::ColumnIndexScan(IndexType index, columnar::Columnarfile* cf, const std::string& indName,
@@ -908,7 +977,7 @@ ColumnIndexScan::ColumnIndexScan(IndexType index, columnar::Columnarfile* cf, co
   }
   (void)str_sizes;
   Jtuple_.setHdr(otypes, osizes);
-  positions_ = or_bitmaps(*cf, {valueBitmaps(*cf, colNo_, sel_)});
+  values_ = valueBitmaps(*cf, colNo_, sel_);
 }
 
 ColumnIndexScan::ColumnIndexScan(IndexType index, columnar::Columnarfile* cf, const std::string& indName,
@@ -916,17 +985,21 @@ ColumnIndexScan::ColumnIndexScan(IndexType index, columnar::Columnarfile* cf, co
                                  CondExpr* const* selects, int fldNum)
     : ColumnIndexScan(index, cf, indName, types, str_sizes, noInFlds, 0, {}, {}, selects, fldNum, false) {}
 
-BitSetPtr ColumnIndexScan::getPositionsOfIndexScan() { return positions_; }
+BitSetPtr ColumnIndexScan::getPositionsOfIndexScan() {
+  if (!positions_) positions_ = or_bitmaps(*f_, {values_});
+  return positions_;
+}
 
-void ColumnIndexScan::materialize() {
-  if (ready_) return;
-  materialize_all(*f_, positions_, outIndexes_, ids_, vals_);
-  ready_ = true;
+void ColumnIndexScan::open_cursor() {
+  if (rows_.open()) return;
+  const std::vector<int> cols = index_only_ ? std::vector<int>{} : outIndexes_;
+  std::vector<int32_t> pc(cols.begin(), cols.end());
+  rows_.reset(cnf_cursor(*f_, {values_}, cols, "ColumnIndexScan"), f_->getAttributeTypes(), f_->getAttrSizes(), pc);
 }
 
 heap::Tuple* ColumnIndexScan::get_next() {
-  materialize();
-  if (next_ >= (int64_t)ids_.size()) return nullptr;
+  open_cursor();
+  if (!rows_.next()) return nullptr;
   if (index_only_) {
     // only the key is returned (R/index/ColumnIndexScan.java:512-565)
     std::vector<AttrType> t{types_.at((size_t)colNo_)};
@@ -935,25 +1008,25 @@ heap::Tuple* ColumnIndexScan::get_next() {
     Jtuple_.setHdr(t, s);
     if (t[0].attrType == AttrType::attrString) Jtuple_.setStrFld(1, sel_.operand2.string);
     else Jtuple_.setIntFld(1, sel_.operand2.integer);
-    next_++;
     return &Jtuple_;
   }
-  std::vector<int32_t> cols(outIndexes_.begin(), outIndexes_.end());
-  iterator::fill_row(Jtuple_, f_->getAttributeTypes(), f_->getAttrSizes(), cols, vals_, next_);
-  next_++;
+  rows_.fill(Jtuple_);
   return &Jtuple_;
 }
 
 global::TID ColumnIndexScan::get_next_tid() {
-  materialize();
+  open_cursor();
   global::TID tid;
   tid.numRIDs = f_->getFieldCount();
-  if (next_ < (int64_t)ids_.size()) tid.position = ids_[(size_t)next_++];
+  if (rows_.next()) tid.position = rows_.position();
   return tid;
 }
 
-void ColumnIndexScan::close() { closeFlag = true; }
-void ColumnIndexScan::restart() { next_ = 0; }
+void ColumnIndexScan::close() {
+  rows_.close();
+  closeFlag = true;
+}
+void ColumnIndexScan::restart() { rows_.restart(); }
 int ColumnIndexScan::getTupleSize() { return Jtuple_.size(); }
 
 ColumnarIndexScan::ColumnarIndexScan(columnar::Columnarfile* cf, const std::vector<int>& fldNums,
@@ -1046,8 +1119,10 @@ ColumnarIndexScan::ColumnarIndexScan(columnar::Columnarfile* cf, const std::vect
     }
   }
   if (!dup && total <= 64) {
-    // one k_bitmap_cnf launch: AND_c OR_k bitmaps AND NOT deleted
-    output_ = or_bitmaps(*cf, lists);
+    // one k_cnf_select launch at the first get_next: AND_c OR_k bitmaps AND
+    // NOT deleted, the positions and the projected rows; the BitSet itself is
+    // formed only if getOutputPositions() asks for it
+    lists_ = lists;
     fused_ = true;
     return;
   }
@@ -1082,20 +1157,39 @@ ColumnarIndexScan::ColumnarIndexScan(columnar::Columnarfile* cf, const std::vect
   output_ = objs[0];
 }
 
+BitSetPtr ColumnarIndexScan::getOutputPositions() {
+  if (!output_) output_ = or_bitmaps(*f_, lists_);
+  return output_;
+}
+
+void ColumnarIndexScan::open_cursor() {
+  if (rows_.open()) return;
+  std::vector<int32_t> pc(outIndexes_.begin(), outIndexes_.end());
+  mbx_cursor* c = fused_ ? cnf_cursor(*f_, lists_, outIndexes_, "ColumnarIndexScan")
+                         : bitset_cursor(*f_, output_, outIndexes_, "ColumnarIndexScan");
+  rows_.reset(c, f_->getAttributeTypes(), f_->getAttrSizes(), pc);
+}
+
 heap::Tuple* ColumnarIndexScan::get_next() {
-  if (!ready_) {
-    materialize_all(*f_, output_, outIndexes_, ids_, vals_);
-    ready_ = true;
-  }
-  if (next_ >= (int64_t)ids_.size()) return nullptr;
-  std::vector<int32_t> cols(outIndexes_.begin(), outIndexes_.end());
-  iterator::fill_row(Jtuple_, f_->getAttributeTypes(), f_->getAttrSizes(), cols, vals_, next_);
-  next_++;
+  open_cursor();
+  if (!rows_.next()) return nullptr;
+  rows_.fill(Jtuple_);
   return &Jtuple_;
 }
 
-void ColumnarIndexScan::close() { closeFlag = true; }
-void ColumnarIndexScan::restart() { next_ = 0; }
+global::TID ColumnarIndexScan::get_next_tid() {
+  open_cursor();
+  global::TID tid;
+  tid.numRIDs = f_->getFieldCount();
+  if (rows_.next()) tid.position = rows_.position();
+  return tid;
+}
+
+void ColumnarIndexScan::close() {
+  rows_.close();
+  closeFlag = true;
+}
+void ColumnarIndexScan::restart() { rows_.restart(); }
 int ColumnarIndexScan::getTupleSize() { return Jtuple_.size(); }
 
 }  // namespace index

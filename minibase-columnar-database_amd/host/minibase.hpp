@@ -247,6 +247,37 @@ std::string int_key(int v);
 
 namespace iterator {
 
+// get_next() over an mbx_cursor (Iterator.get_next, R/iterator/Iterator.java:12-141):
+// batches of kRows positions + projected rows come out of the cursor's
+// double-buffered delivery; fill() writes the current row into Jtuple.
+class CursorBatches {
+ public:
+  static constexpr int64_t kRows = 8192;
+  CursorBatches() = default;
+  ~CursorBatches() { close(); }
+  CursorBatches(const CursorBatches&) = delete;
+  CursorBatches& operator=(const CursorBatches&) = delete;
+  // takes ownership of c; cols = the projected file columns
+  void reset(mbx_cursor* c, const std::vector<AttrType>& types, const std::vector<short>& sizes,
+             const std::vector<int32_t>& cols);
+  bool open() const { return cur_ != nullptr; }
+  int64_t count() const;
+  bool next();                  // the next row; false at the end of the stream
+  int64_t position() const { return ids_[(size_t)i_ - 1]; }
+  void fill(heap::Tuple& J) const;
+  void restart();
+  void close();
+
+ private:
+  mbx_cursor* cur_ = nullptr;
+  std::vector<AttrType> types_;
+  std::vector<short> sizes_;
+  std::vector<int32_t> cols_;
+  std::vector<std::vector<uint8_t>> batch_;
+  std::vector<int64_t> ids_;
+  int64_t n_ = 0, i_ = 0;
+};
+
 // R/iterator/ColumnarFileScan.java:51-99 (+ get_next :156-172, get_next_tid :174-188)
 class ColumnarFileScan : public Iterator {
  public:
@@ -371,19 +402,17 @@ class ColumnIndexScan : public iterator::Iterator {
                                                        const CondExpr& e);
 
  private:
-  void materialize();
+  void open_cursor();
   columnar::Columnarfile* f_;
   int colNo_;
   std::vector<int> outIndexes_;
   std::vector<AttrType> types_;
   bool index_only_ = false;
   CondExpr sel_{};
-  columnar::BitSetPtr positions_;
+  std::vector<columnar::BitSetPtr> values_;  // the value bitmaps OR-ed by getBitSet
+  columnar::BitSetPtr positions_;            // their OR minus deleted, built on first use
   heap::Tuple Jtuple_;
-  std::vector<int64_t> ids_;
-  std::vector<std::vector<uint8_t>> vals_;
-  int64_t next_ = 0;
-  bool ready_ = false;
+  iterator::CursorBatches rows_;             // get_next: one k_cnf_select launch
 };
 
 // R/index/ColumnarIndexScan.java:79-182 (+ getOutputPositions :270, get_next :287-308)
@@ -394,23 +423,27 @@ class ColumnarIndexScan : public iterator::Iterator {
                     const std::vector<AttrType>& types, const std::vector<short>& str_sizes, int noInFlds,
                     int noOutFlds, const std::vector<int>& out_indexes, const std::vector<FldSpec>& outFlds,
                     CondExpr* const* selects, bool indexOnly);
-  columnar::BitSetPtr getOutputPositions() const { return output_; }
+  // the CNF's BitSet (on the one-launch path it is formed on first request)
+  columnar::BitSetPtr getOutputPositions();
   heap::Tuple* get_next() override;
+  global::TID get_next_tid();
   void close() override;
   void restart() override;
   int getTupleSize() override;
+  // true: no repeated constraint -- CNF, positions and projection in ONE
+  // kernel launch (mbx_cnf_cursor_open / k_cnf_select); false: the
+  // reference's step-wise BitSet objects (its duplicate-constraint cache)
   bool usedFusedCnf() const { return fused_; }
 
  private:
+  void open_cursor();
   columnar::Columnarfile* f_;
   std::vector<int> outIndexes_;
   std::vector<AttrType> types_;
+  std::vector<std::vector<columnar::BitSetPtr>> lists_;  // fused: bitmaps per conjunct
   columnar::BitSetPtr output_;
   heap::Tuple Jtuple_;
-  std::vector<int64_t> ids_;
-  std::vector<std::vector<uint8_t>> vals_;
-  int64_t next_ = 0;
-  bool ready_ = false;
+  iterator::CursorBatches rows_;
   bool fused_ = false;
 };
 }  // namespace index

@@ -86,7 +86,8 @@ EXPORTS = [
     "mbx_scan_aggregate_async", "mbx_bitmap_alloc", "mbx_bitmap_upload", "mbx_bitmap_download", "mbx_bitmap_info",
     "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_cnf_materialize_async", "mbx_bitmap_index_build",
     "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
-    "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close", "mbx_probe_read", "mbx_set_tuning",
+    "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close", "mbx_cursor_stats", "mbx_cnf_cursor_open", "mbx_cnf_cursor_launch",
+    "mbx_probe_read", "mbx_set_tuning",
     "mbx_diag_select_stamps", "mbx_dev_alloc", "mbx_dev_free", "mbx_dev_download", "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
     "mbx_comm_info", "mbx_comm_wait", "mbx_comm_allreduce_count_async", "mbx_comm_allreduce_agg_async",
     "mbx_comm_allgather_count_async", "mbx_comm_allreduce_count_all", "mbx_comm_allreduce_agg_all",
@@ -96,7 +97,7 @@ EXPORTS = [
     "mbx_db_columnar_insert", "mbx_db_columnar_info", "mbx_db_mark_deleted", "mbx_db_bitmap_write",
     "mbx_db_bitmap_read", "mbx_db_stage", "mbx_db_allocate_pages", "mbx_db_add_file_entry",
     "mbx_db_create_bitmap_index", "mbx_db_bitmap_values", "mbx_db_bitmap_stage", "mbx_db_mark_deleted_many",
-    "mbx_db_purge",
+    "mbx_db_purge", "mbx_db_stage_range", "mbx_db_bitmap_stage_range",
     # include/mbx_join.h
     "mbx_join", "mbx_join_info", "mbx_join_fetch", "mbx_join_free", "mbx_gather",
 ]
@@ -165,6 +166,9 @@ def lib():
         "mbx_cursor_next": ([V, I64, V, P(V), P(I64)], ctypes.c_int),
         "mbx_cursor_restart": ([V], ctypes.c_int),
         "mbx_cursor_close": ([V], ctypes.c_int),
+        "mbx_cursor_stats": ([V, P(I64), P(I64)], ctypes.c_int),
+        "mbx_cnf_cursor_open": ([V, V, P(V), P(I32), I32, V, P(I32), I32, P(V)], ctypes.c_int),
+        "mbx_cnf_cursor_launch": ([V, V, P(V), P(I32), I32, V, P(I32), I32, P(V), P(V)], ctypes.c_int),
         "mbx_probe_read": ([V, V, P(I32), I32, I64, I32, I64], ctypes.c_int),
         "mbx_set_tuning": ([V, ctypes.c_char_p, I64], ctypes.c_int),
         "mbx_diag_select_stamps": ([V, V, I64], ctypes.c_int),
@@ -206,6 +210,8 @@ def lib():
         "mbx_db_bitmap_stage": ([V, V, ctypes.c_char_p, I64, P(V)], ctypes.c_int),
         "mbx_db_mark_deleted_many": ([V, ctypes.c_char_p, V, I64], ctypes.c_int),
         "mbx_db_purge": ([V, ctypes.c_char_p], ctypes.c_int),
+        "mbx_db_stage_range": ([V, V, ctypes.c_char_p, I64, I64, P(V)], ctypes.c_int),
+        "mbx_db_bitmap_stage_range": ([V, V, ctypes.c_char_p, I64, I64, P(V)], ctypes.c_int),
         "mbx_join": ([V, V, V, V, V, P(JoinCnf), I32, I64, P(V)], ctypes.c_int),
         "mbx_join_info": ([V, P(I64), P(I64)], ctypes.c_int),
         "mbx_join_fetch": ([V, V, I64, I64, V, V, V], ctypes.c_int),
@@ -425,6 +431,21 @@ class Context:
         _chk(lib().mbx_db_stage(self.h, db.h, name.encode(), ctypes.byref(h)))
         return Table(self, h, info["nrows"], [(t, s) for t, s in info["cols"]], 0)
 
+    def stage_db_range(self, db, name, row_begin, row_end):
+        """mbx_db_stage_range: positions [row_begin, row_end) of a Columnarfile
+        (one shard; row_offset = row_begin), only that range's pages read."""
+        info = db.columnar_info(name)
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_db_stage_range(self.h, db.h, name.encode(), row_begin, row_end, ctypes.byref(h)))
+        n, off, nc = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32()
+        _chk(lib().mbx_table_info(h, ctypes.byref(n), ctypes.byref(off), ctypes.byref(nc)))
+        return Table(self, h, n.value, [(t, s) for t, s in info["cols"]], off.value)
+
+    def stage_db_bitmap_range(self, db, filename, bit_begin, nbits):
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_db_bitmap_stage_range(self.h, db.h, filename.encode(), bit_begin, nbits, ctypes.byref(h)))
+        return Bitmap(self, h, nbits)
+
     # -- plans / scans ---------------------------------------------------
     def compile(self, table, cnf):
         keep = []
@@ -517,10 +538,8 @@ class Context:
         _chk(lib().mbx_bitmap_cnf_async(self.h, bms, offs, len(conjuncts),
                                         None if deleted is None else deleted.h, out.h))
 
-    def cnf_materialize_async(self, table, conjuncts, proj, dev_ids, dev_outs, dev_count, deleted=None):
-        """mbx_cnf_materialize_async: CNF of index BitSets + positions + <= 4
-        projected 4-byte columns in one launch (device pointers as ints;
-        dev_ids may be None)."""
+    @staticmethod
+    def _cnf_arrays(conjuncts):
         flat = [b for conj in conjuncts for b in conj]
         bms = (ctypes.c_void_p * max(1, len(flat)))(*[b.h.value for b in flat])
         offs = (ctypes.c_int32 * (len(conjuncts) + 1))()
@@ -529,6 +548,34 @@ class Context:
             offs[i] = k
             k += len(conj)
         offs[len(conjuncts)] = k
+        return bms, offs
+
+    def cnf_cursor(self, table, conjuncts, proj, deleted=None):
+        """mbx_cnf_cursor_open: ColumnarIndexScan (CNF of index BitSets) +
+        positions + projected rows (any columns) in one launch, as a cursor."""
+        bms, offs = self._cnf_arrays(conjuncts)
+        pj = (ctypes.c_int32 * max(1, len(proj)))(*proj)
+        h = ctypes.c_void_p()
+        _chk(lib().mbx_cnf_cursor_open(self.h, table.h, bms, offs, len(conjuncts),
+                                       None if deleted is None else deleted.h, pj, len(proj), ctypes.byref(h)))
+        return Cursor(self, h, table, list(proj))
+
+    def cnf_cursor_launch(self, table, conjuncts, proj, deleted=None):
+        """mbx_cnf_cursor_launch: as cnf_cursor, launch only -> (Cursor, device
+        pointer of its count)."""
+        bms, offs = self._cnf_arrays(conjuncts)
+        pj = (ctypes.c_int32 * max(1, len(proj)))(*proj)
+        h, dc = ctypes.c_void_p(), ctypes.c_void_p()
+        _chk(lib().mbx_cnf_cursor_launch(self.h, table.h, bms, offs, len(conjuncts),
+                                         None if deleted is None else deleted.h, pj, len(proj), ctypes.byref(h),
+                                         ctypes.byref(dc)))
+        return Cursor(self, h, table, list(proj)), dc.value
+
+    def cnf_materialize_async(self, table, conjuncts, proj, dev_ids, dev_outs, dev_count, deleted=None):
+        """mbx_cnf_materialize_async: CNF of index BitSets + positions +
+        projected rows in one launch (device pointers as ints; dev_ids may be
+        None; dev_outs[j] in the device row layout of column proj[j])."""
+        bms, offs = self._cnf_arrays(conjuncts)
         pj = (ctypes.c_int32 * max(1, len(proj)))(*proj)
         outs = (ctypes.c_void_p * max(1, len(proj)))(*dev_outs)
         _chk(lib().mbx_cnf_materialize_async(self.h, table.h, bms, offs, len(conjuncts),
@@ -754,6 +801,12 @@ class Cursor(_Handle):
 
     def restart(self):
         _chk(lib().mbx_cursor_restart(self.h))
+
+    def stats(self):
+        """(rows handed out so far, bytes copied device -> host)"""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        _chk(lib().mbx_cursor_stats(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
 
 class Db:

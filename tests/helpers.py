@@ -114,3 +114,50 @@ def device_dictionary_column(dic, idx, chunk=1 << 23):
     for s in range(0, n, chunk):
         out[s:s + chunk].copy_(dic[idx[s:s + chunk].long()])
     return out
+
+
+def index_registry(ctx, ocols, t, col):
+    """`index db cf <col> bitmap`: one BitMapFile per distinct value, built on
+    the GPU in one pass; the registry maps value -> device bitmap."""
+    typ, size, arr = ocols[col]
+    if typ == oracle.STRING:
+        vals = sorted({bytes(r).rstrip(b"\0") for r in arr})
+        specs = [("str", v) for v in vals]
+    else:
+        vals = sorted(set(int(x) for x in arr))
+        specs = [("int", v) for v in vals]
+    bms = ctx.index_build(t, col, specs)
+    return dict(zip(vals, bms))
+
+
+def value_set(reg, typ, op, lit):
+    """ColumnIndexScan.getBitSet value selection (R/index/ColumnIndexScan.java:656-740)."""
+    if typ == oracle.STRING:
+        key = lambda v: oracle.java_mutf8(v).decode("utf-8", "surrogatepass").encode("utf-16-be", "surrogatepass")
+        litb = oracle.java_mutf8(lit)
+        cmp = lambda other: (key(litb) > key(other)) - (key(litb) < key(other))
+        lit_key = litb
+    else:
+        cmp = lambda other: (lit > other) - (lit < other)
+        lit_key = lit
+    out = []
+    if op in (oracle.EQ, oracle.LE, oracle.GE) and lit_key in reg:
+        out.append(reg[lit_key])
+    for v, bm in reg.items():
+        c = cmp(v)
+        if (op in (oracle.LT, oracle.LE) and c > 0) or (op in (oracle.GT, oracle.GE) and c < 0) or \
+                (op == oracle.NE and c != 0):
+            out.append(bm)
+    return out
+
+
+def index_conjuncts(regs, cnf, types):
+    """ColumnarIndexScan's bitmap lists (R/index/ColumnarIndexScan.java:130-181):
+    per conjunct the value bitmaps of every term, in term order."""
+    out = []
+    for conj in cnf:
+        lst = []
+        for op, (_, fld), (_, lit), *_ in conj:
+            lst += value_set(regs[fld - 1], types[fld - 1], op, lit)
+        out.append(lst)
+    return out

@@ -5,7 +5,8 @@ against numpy's CNF / nonzero / fancy indexing of the same host data and
 against the two-call form (mbx_bitmap_cnf_async + mbx_materialize_async):
 operand counts on both sides of the batched-load branch (<= 4 / > 4
 bitmaps), deleted rows, ragged sizes, densities 0..1, 0-4 int/float
-columns, positions on or off, a shard's row_offset, a table past the
+columns (char(n) and wider projections: test_cnf_cursor.py and the limits
+test here), positions on or off, a shard's row_offset, a table past the
 register-cached range (> 134 M rows: the words are re-formed for the write
 pass), many launches in a row (the epoch advances) and graph replays (the
 epoch is read from device memory, not baked into the graph)."""
@@ -218,18 +219,38 @@ def test_cnf_materialize_past_the_register_range(ctx):
     assert bool((ids[:k_want] == want).all()) and bool((out[:k_want] == col[want]).all())
 
 
-def test_cnf_materialize_rejects_what_it_cannot_fuse(ctx, m):
+def test_cnf_materialize_any_projection_and_limits(ctx, m):
+    """char(n) rows and more than 4 columns go through the same launch (the
+    wide row gather); more than 16 columns, a null output and a bitmap of
+    another size are rejected."""
     n = 1000
+    words = ["x", "South_Dakota", "", "zzzzzzzzzzzzzzzz"]
+    svals = [words[i % 4] for i in range(n)]
     cols = [(oracle.INTEGER, 4, np.arange(n, dtype=np.int32)),
-            (oracle.STRING, 16, helpers.encode_strings(["x"], 16)[np.zeros(n, dtype=np.int64)])]
+            (oracle.STRING, 16, helpers.encode_strings(svals, 16))]
     t = ctx.stage(cols)
-    A = ctx.bitmap_upload(n, words_of(np.ones(n, dtype=bool)))
+    sel = np.arange(n) % 3 == 1
+    A = ctx.bitmap_upload(n, words_of(sel))
+    want = np.nonzero(sel)[0]
+    torch.cuda.synchronize()
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-    buf = torch.zeros(n, dtype=torch.int32, device="cuda")
-    with pytest.raises(m.MbxError):  # a string column
-        ctx.cnf_materialize_async(t, [[A]], [1], None, [buf.data_ptr()], cnt.data_ptr())
-    with pytest.raises(m.MbxError):  # five columns
-        ctx.cnf_materialize_async(t, [[A]], [0] * 5, None, [buf.data_ptr()] * 5, cnt.data_ptr())
+    srow = torch.zeros(n * 4, dtype=torch.int32, device="cuda")  # 16-byte device rows
+    outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(5)]
+    torch.cuda.synchronize()
+    ctx.cnf_materialize_async(t, [[A]], [1], None, [srow.data_ptr()], cnt.data_ptr())
+    ctx.sync()
+    assert int(cnt.item()) == len(want)
+    rows = srow.cpu().numpy().view(np.uint8).reshape(n, 16)[:len(want)]
+    assert [bytes(r).rstrip(b"\0").decode() for r in rows] == [svals[i] for i in want]
+    ctx.cnf_materialize_async(t, [[A]], [0] * 5, None, [o.data_ptr() for o in outs], cnt.data_ptr())
+    ctx.sync()
+    for o in outs:
+        assert np.array_equal(o[:len(want)].cpu().numpy(), want)
+    buf = outs[0]
+    with pytest.raises(m.MbxError):  # seventeen columns
+        ctx.cnf_materialize_async(t, [[A]], [0] * 17, None, [buf.data_ptr()] * 17, cnt.data_ptr())
+    with pytest.raises(m.MbxError):  # a null output buffer
+        ctx.cnf_materialize_async(t, [[A]], [0, 1], None, [buf.data_ptr(), 0], cnt.data_ptr())
     B = ctx.bitmap_upload(n + 1, words_of(np.ones(n + 1, dtype=bool)))
     with pytest.raises(m.MbxError):  # bitmap / table size mismatch
         ctx.cnf_materialize_async(t, [[B]], [0], None, [buf.data_ptr()], cnt.data_ptr())

@@ -55,39 +55,8 @@ def test_golden_counts(ctx, mini, g):
     assert ctx.scan_count(ctx.compile(t, helpers.golden_cnf(g["cnf"]))) == g["count"]
 
 
-def index_registry(ctx, ocols, t, col):
-    """`index db cf <col> bitmap`: one BitMapFile per distinct value, built on
-    the GPU in one pass; the registry maps value -> device bitmap."""
-    typ, size, arr = ocols[col]
-    if typ == oracle.STRING:
-        vals = sorted({bytes(r).rstrip(b"\0") for r in arr})
-        specs = [("str", v) for v in vals]
-    else:
-        vals = sorted(set(int(x) for x in arr))
-        specs = [("int", v) for v in vals]
-    bms = ctx.index_build(t, col, specs)
-    return dict(zip(vals, bms))
-
-
-def value_set(reg, typ, op, lit):
-    """ColumnIndexScan.getBitSet value selection (R/index/ColumnIndexScan.java:656-740)."""
-    if typ == oracle.STRING:
-        key = lambda v: oracle.java_mutf8(v).decode("utf-8", "surrogatepass").encode("utf-16-be", "surrogatepass")
-        litb = oracle.java_mutf8(lit)
-        cmp = lambda other: (key(litb) > key(other)) - (key(litb) < key(other))
-        lit_key = litb
-    else:
-        cmp = lambda other: (lit > other) - (lit < other)
-        lit_key = lit
-    out = []
-    if op in (oracle.EQ, oracle.LE, oracle.GE) and lit_key in reg:
-        out.append(reg[lit_key])
-    for v, bm in reg.items():
-        c = cmp(v)
-        if (op in (oracle.LT, oracle.LE) and c > 0) or (op in (oracle.GT, oracle.GE) and c < 0) or \
-                (op == oracle.NE and c != 0):
-            out.append(bm)
-    return out
+index_registry = helpers.index_registry
+value_set = helpers.value_set
 
 
 @pytest.mark.parametrize("g", GOLD["bitsets"] + GOLD["indexes_query"],
