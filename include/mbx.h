@@ -332,6 +332,9 @@ int mbx_comm_allgather_count_async(mbx_comm *comm, const int64_t *dev_count, int
 /* one process, n communicators of one mbx_comm_init_all clique (rank order) */
 int mbx_comm_allreduce_count_all(mbx_comm *const *comms, int32_t n, int64_t *const *dev_counts, int64_t count);
 int mbx_comm_allreduce_agg_all(mbx_comm *const *comms, int32_t n, mbx_agg *const *dev_recs);
+/* dev_alls[i][r] = rank r's *dev_counts[r], for every rank i (one grouped all-gather) */
+int mbx_comm_allgather_count_all(mbx_comm *const *comms, int32_t n, const int64_t *const *dev_counts,
+                                 int64_t *const *dev_alls);
 
 /* ---- HIP graphs: a repeated query (scan + exchange) captured once and
  * replayed with one launch.  Between begin and end the context's *_async

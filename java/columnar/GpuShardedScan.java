@@ -1,67 +1,89 @@
 package columnar;
 
-import java.nio.ByteBuffer;
-
 import global.GpuContext;
 import global.Native;
 import iterator.CondExpr;
 
 /**
- * One JVM driving every GPU of the node (SURVEY.md 8(e), DESIGN.md section 6):
- * the table's rows are split into 64-aligned row ranges (Native.shardBounds),
- * each staged on its own GPU with row_offset = the range's first position;
- * a query runs one scan per GPU and ONE RCCL exchange over xGMI combines the
- * per-shard results on the devices (COUNT: int64 all-reduce; COUNT/SUM/MIN/MAX:
- * all-gather of the 48-byte records folded in rank order, so the double SUM
- * is reproducible for a given GPU count).  The reference engine is one
- * process (R/global/SystemDefs.java:6-9); so is this.
+ * One JVM driving every GPU of the node (SURVEY.md 8(e), DESIGN.md section 6).
+ * A Columnarfile of the DB file is split into one 64-aligned row range per
+ * GPU (Native.shardBounds, positions as long), and each range is staged
+ * straight from the DB file onto its GPU (Native.dbStageRange ->
+ * mbx_db_stage_range: only that range's pages are read; no column passes
+ * through the JVM, so no 2 GB ByteBuffer limit -- C5's 16 GB char(16)
+ * column included).  A query runs one scan per GPU and ONE RCCL exchange
+ * over xGMI combines the per-shard results on the devices (COUNT: int64
+ * all-reduce; COUNT/SUM/MIN/MAX: all-gather of the 48-byte records folded in
+ * rank order, so the double SUM is reproducible for a given GPU count).  The
+ * clique is GpuContext's, shared by every sharded scan of the JVM.  The
+ * reference engine is one process (R/global/SystemDefs.java:6-9); so is
+ * this.  Sharded index scans: {@link #indexScan}.
  */
 public final class GpuShardedScan implements AutoCloseable {
-  private final long[] ctxs, comms, tables, slots;
-  private final long nrows;
+  final long[] ctxs, tables, begins, ends;
+  private final long[] slots, comms;
+  final long db, nrows;
+  final String name;
+  private boolean closed;
 
-  /**
-   * cols: one direct ByteBuffer per column in host order (char(n): n bytes of
-   * zero-padded modified UTF-8 per row); deleted: cf.md's BitSet.toLongArray()
-   * or null.
-   */
-  public GpuShardedScan(int[] attrTypes, short[] sizes, long nrows, ByteBuffer[] cols, long[] deleted)
-      throws Exception {
+  /** the Columnarfile `columnarFile` of the DB file GpuTables.open(...) named */
+  public GpuShardedScan(String columnarFile) throws Exception {
     final int n = GpuContext.devices();
-    this.nrows = nrows;
+    name = columnarFile;
+    db = GpuTables.dbHandle();                    // the buffer pool is flushed first
+    nrows = Native.dbColumnarRows(db, columnarFile);
     ctxs = new long[n];
     tables = new long[n];
     slots = new long[n];
-    for (int g = 0; g < n; g++) {
-      ctxs[g] = GpuContext.ctx(g);
-      long[] be = Native.shardBounds(nrows, n, g);
-      ByteBuffer[] part = new ByteBuffer[cols.length];
-      for (int j = 0; j < cols.length; j++) {
-        int w = attrTypes[j] == global.AttrType.attrString ? sizes[j] : 4;
-        ByteBuffer d = cols[j].duplicate();
-        d.position((int) (be[0] * w)).limit((int) (be[1] * w));
-        part[j] = d.slice().order(cols[j].order());
+    begins = new long[n];
+    ends = new long[n];
+    try {
+      for (int g = 0; g < n; g++) {
+        ctxs[g] = GpuContext.ctx(g);
+        long[] be = Native.shardBounds(nrows, n, g);
+        begins[g] = be[0];
+        ends[g] = be[1];
+        tables[g] = Native.dbStageRange(ctxs[g], db, columnarFile, be[0], be[1]);
+        slots[g] = Native.devAlloc(ctxs[g], Native.AGG_RECORD_BYTES);
       }
-      long[] del = null;
-      if (deleted != null) {                         // be[0] is a multiple of 64: whole words
-        int w0 = (int) (be[0] / 64), w1 = (int) Math.min(deleted.length, (be[1] + 63) / 64);
-        del = new long[Math.max(0, w1 - w0)];
-        if (w1 > w0) System.arraycopy(deleted, w0, del, 0, w1 - w0);
-      }
-      tables[g] = Native.tableStage(ctxs[g], attrTypes, sizes, be[1] - be[0], part, del, be[0]);
-      slots[g] = Native.devAlloc(ctxs[g], Native.AGG_RECORD_BYTES);
+      comms = GpuContext.comms();                  // one RCCL clique, rank g = GPU g
+    } catch (Exception e) {
+      release();
+      throw e;
     }
-    comms = Native.commInitAll(ctxs);                 // one RCCL clique, rank g = GPU g
   }
 
   private long[] compile(CondExpr[] filter) throws Exception {
     long[] plans = new long[ctxs.length];
-    for (int g = 0; g < ctxs.length; g++) plans[g] = Native.planCompile(ctxs[g], tables[g], filter);
+    try {
+      for (int g = 0; g < ctxs.length; g++) plans[g] = Native.planCompile(ctxs[g], tables[g], filter);
+    } catch (Exception e) {
+      free(plans);
+      throw e;
+    }
     return plans;
   }
 
-  private void free(long[] plans) {
+  private static void free(long[] plans) {
     for (long p : plans) if (p != 0) Native.planFree(p);
+  }
+
+  /**
+   * Waits for every GPU.  Every context is synced even when one raises (a NaN
+   * an async scan reached raises at the sync, PredEval's exception): each
+   * context's sticky flag is read and cleared and its exchange stream
+   * drained; the first exception is rethrown after the loop.
+   */
+  static void syncAll(long[] ctxs) throws Exception {
+    Exception first = null;
+    for (long c : ctxs) {
+      try {
+        Native.sync(c);
+      } catch (Exception e) {
+        if (first == null) first = e;
+      }
+    }
+    if (first != null) throw first;
   }
 
   /** Query.executeFileScan's resultCount over all shards: one scan per GPU + one all-reduce */
@@ -70,7 +92,7 @@ public final class GpuShardedScan implements AutoCloseable {
     try {
       for (int g = 0; g < ctxs.length; g++) Native.scanCountAsync(ctxs[g], plans[g], slots[g]);
       Native.commAllreduceCountAll(comms, slots);
-      for (long c : ctxs) Native.sync(c);             // a NaN reached by a float compare raises here
+      syncAll(ctxs);
       return Native.countDownload(ctxs[0], slots[0]);
     } finally {
       free(plans);
@@ -83,22 +105,75 @@ public final class GpuShardedScan implements AutoCloseable {
     try {
       for (int g = 0; g < ctxs.length; g++) Native.scanAggregateAsync(ctxs[g], plans[g], col, slots[g]);
       Native.commAllreduceAggAll(comms, slots);
-      for (long c : ctxs) Native.sync(c);
+      syncAll(ctxs);
       return Native.aggDownload(ctxs[0], slots[0]);
     } finally {
       free(plans);
     }
   }
 
+  /**
+   * ColumnarIndexScan over the shards (index.GpuShardedColumnarIndexScan):
+   * same arguments as the reference constructor minus the Columnarfile.
+   */
+  public index.GpuShardedColumnarIndexScan indexScan(Columnarfile cf, global.AttrType[] types, short[] str_sizes,
+                                                    int noInFlds, int noOutFlds, int[] out_indexes,
+                                                    iterator.FldSpec[] outFlds, CondExpr[] selects)
+      throws Exception {
+    return new index.GpuShardedColumnarIndexScan(this, cf, types, str_sizes, noInFlds, noOutFlds, out_indexes,
+                                                 outFlds, selects);
+  }
+
   public long rows() {
     return nrows;
   }
 
-  public void close() {
-    for (long c : comms) Native.commFree(c);
+  public int shards() {
+    return ctxs.length;
+  }
+
+  public long context(int g) {
+    return ctxs[g];
+  }
+
+  public long table(int g) {
+    return tables[g];
+  }
+
+  public long rowBegin(int g) {
+    return begins[g];
+  }
+
+  public long rowEnd(int g) {
+    return ends[g];
+  }
+
+  /** the DB file the shards were staged from (their BitMapFile slices come from it too) */
+  public long db() {
+    return db;
+  }
+
+  /** the clique over the shards' GPUs (rank g = shard g) */
+  public long[] comms() {
+    return comms;
+  }
+
+  public String fileName() {
+    return name;
+  }
+
+  private void release() {
     for (int g = 0; g < ctxs.length; g++) {
-      Native.devFree(ctxs[g], slots[g]);
-      Native.tableFree(tables[g]);
+      if (slots[g] != 0) Native.devFree(ctxs[g], slots[g]);
+      if (tables[g] != 0) Native.tableFree(tables[g]);
+      slots[g] = tables[g] = 0;
     }
+  }
+
+  /** frees the shards; the clique stays with GpuContext */
+  public void close() {
+    if (closed) return;
+    release();
+    closed = true;
   }
 }

@@ -41,6 +41,11 @@ public final class GpuTables {
     return db;
   }
 
+  /** the DB file handle (buffer pool flushed first): sharded scans stage their row ranges from it */
+  public static synchronized long dbHandle() throws Exception {
+    return db();
+  }
+
   public static synchronized long get(String columnarFile) throws Exception {
     Long t = tables.get(columnarFile);
     if (t == null) {

@@ -7,6 +7,7 @@ package global;
  */
 public final class GpuContext {
   private static long[] ctxs;
+  private static long[] comms;   // one RCCL clique over the contexts of GPUs 0..n-1, shared
 
   private GpuContext() {}
 
@@ -26,8 +27,24 @@ public final class GpuContext {
     return Math.max(1, Native.deviceCount());
   }
 
-  /** releases every context (SystemDefs shutdown) */
+  /**
+   * The communicators of one RCCL clique over every GPU (rank g = GPU g),
+   * created once and shared by every sharded scan of the JVM: a context
+   * carries at most one communicator (mbx_comm_init_all refuses a second).
+   */
+  public static synchronized long[] comms() throws Exception {
+    if (comms == null) {
+      long[] cs = new long[devices()];
+      for (int g = 0; g < cs.length; g++) cs[g] = ctx(g);
+      comms = Native.commInitAll(cs);
+    }
+    return comms;
+  }
+
+  /** releases the clique and every context (SystemDefs shutdown) */
   public static synchronized void shutdown() {
+    if (comms != null) for (long m : comms) if (m != 0) Native.commFree(m);
+    comms = null;
     if (ctxs == null) return;
     for (long c : ctxs) if (c != 0) Native.free(c);
     ctxs = null;

@@ -27,19 +27,27 @@ final class GpuBitmapValues {
   private GpuBitmapValues() {}
 
   static List<Long> of(Columnarfile f, int colNo, CondExpr e, long nbits) throws Exception {
+    final boolean str = f.getAttributeType(colNo).attrType == AttrType.attrString;
+    final List<Long> out = new ArrayList<>();
+    for (Object v : values(f, colNo, e)) out.add(handle(f, colNo, v, str, nbits));
+    return out;
+  }
+
+  /** the registered values v with `v op literal` (String or Integer), in getBitSet's order */
+  static List<Object> values(Columnarfile f, int colNo, CondExpr e) throws Exception {
     final int op = e.op.attrOperator;
     final boolean str = f.getAttributeType(colNo).attrType == AttrType.attrString;
     final Set<?> all = f.getBitmapValues(colNo);
-    final List<Long> out = new ArrayList<>();
+    final List<Object> out = new ArrayList<>();
     final Object lit = str ? (Object) e.operand2.string : (Object) Integer.valueOf(e.operand2.integer);
     if ((op == AttrOperator.aopEQ || op == AttrOperator.aopLE || op == AttrOperator.aopGE) && all.contains(lit))
-      out.add(handle(f, colNo, lit, str, nbits));
+      out.add(lit);
     for (Object v : all) {
       final int c = str ? ((String) lit).compareTo((String) v) : Integer.compare((Integer) lit, (Integer) v);
       final boolean take = ((op == AttrOperator.aopLT || op == AttrOperator.aopLE) && c > 0)
           || ((op == AttrOperator.aopGT || op == AttrOperator.aopGE) && c < 0)
           || (op == AttrOperator.aopNE && c != 0);
-      if (take) out.add(handle(f, colNo, v, str, nbits));
+      if (take) out.add(v);
     }
     return out;
   }

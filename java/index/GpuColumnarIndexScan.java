@@ -21,17 +21,22 @@ import iterator.TupleUtils;
 /**
  * Drop-in for ColumnarIndexScan (R/index/ColumnarIndexScan.java:79-330): same
  * constructor, getOutputPositions(), get_next() in nextSetBit order.
- * Bitmap-index CNFs run as ONE k_bitmap_cnf launch over the value BitSets of
- * every term (OR within a conjunct, AND across, AND NOT cf.md).  Two cases
- * keep the reference's own ColumnarIndexScan for the positions, so its
+ * Bitmap-index CNFs run as ONE kernel launch (Native.cnfCursorOpen,
+ * k_cnf_select) over the value BitSets of every term -- OR within a
+ * conjunct, AND across, AND NOT cf.md -- that also writes the positions and
+ * the projected out_indexes rows (char(n) included) for get_next(); the
+ * CNF's BitSet is formed only if getOutputPositions() asks for it.  Two
+ * cases keep the reference's own ColumnarIndexScan for the positions, so its
  * results stay identical: a B-tree term (B-tree access is out of scope for
  * the GPU path) and a repeated identical constraint (its duplicateConstraints
- * cache ORs in a BitSet that a later AND mutates, :147-172).  Either way the
- * projection of out_indexes is materialised on the GPU.
+ * cache ORs in a BitSet that a later AND mutates, :147-172); their
+ * projection is still materialised on the GPU.
  */
-public class GpuColumnarIndexScan extends Iterator {
-  private final long ctx, table;
-  private long output, cursor;
+public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelection {
+  private final long ctx, table, nbits;
+  private long output, cursor, deleted;
+  private long[] cnfBitmaps;
+  private int[] cnfOffsets;
   private final Tuple Jtuple = new Tuple();
   private final AttrType[] outTypes;
   private final int[] outIdx, projTypes;
@@ -49,7 +54,7 @@ public class GpuColumnarIndexScan extends Iterator {
     TupleUtils.setup_op_tuple(Jtuple, outTypes, types, noInFlds, str_sizes, outFlds, noOutFlds);
     ctx = GpuContext.ctx();
     table = GpuTables.get(columnarFile.get_fileName());
-    final long nbits = tableRows(table);
+    nbits = tableRows(table);
     outIdx = out_indexes == null ? new int[0] : out_indexes.clone();
     projTypes = new int[outIdx.length];
     projSizes = new short[outIdx.length];
@@ -67,23 +72,25 @@ public class GpuColumnarIndexScan extends Iterator {
           bms.addAll(GpuBitmapValues.of(columnarFile, fieldOf(e) - 1, e, nbits));
         offs.add(bms.size());
       }
-      long[] h = new long[bms.size()];
-      for (int k = 0; k < h.length; k++) h[k] = bms.get(k);
-      int[] o = new int[offs.size()];
-      for (int k = 0; k < o.length; k++) o[k] = offs.get(k);
-      long deleted = Native.bitmapUpload(ctx, nbits, columnarFile.getMarkedDeleted().getBitSet().toLongArray());
+      cnfBitmaps = new long[bms.size()];
+      for (int k = 0; k < cnfBitmaps.length; k++) cnfBitmaps[k] = bms.get(k);
+      cnfOffsets = new int[offs.size()];
+      for (int k = 0; k < cnfOffsets.length; k++) cnfOffsets[k] = offs.get(k);
+      deleted = Native.bitmapUpload(ctx, nbits, columnarFile.getMarkedDeleted().getBitSet().toLongArray());
       try {
-        output = Native.bitmapCnf(ctx, nbits, h, o, deleted);       // one kernel, any CNF shape
-      } finally {
-        Native.bitmapFree(deleted);
+        // CNF + positions + projected rows: one kernel, any CNF shape
+        cursor = Native.cnfCursorOpen(ctx, table, cnfBitmaps, cnfOffsets, deleted, outIdx);
+      } catch (Exception e) {
+        close();
+        throw e;
       }
     } else {
       ColumnarIndexScan ref = new ColumnarIndexScan(columnarFile, fldNums, indexTypes, indNames, types, str_sizes,
                                                     noInFlds, noOutFlds, out_indexes, outFlds, selects, indexOnly);
       output = Native.bitmapUpload(ctx, nbits, ref.getOutputPositions().toLongArray());
       ref.close();
+      cursor = Native.cursorOpen(ctx, table, output, outIdx);
     }
-    cursor = Native.cursorOpen(ctx, table, output, outIdx);
   }
 
   private static long tableRows(long table) throws Exception {
@@ -114,7 +121,20 @@ public class GpuColumnarIndexScan extends Iterator {
   }
 
   public BitSet getOutputPositions() throws Exception {
-    return BitSet.valueOf(Native.bitmapDownload(ctx, output));
+    return BitSet.valueOf(Native.bitmapDownload(ctx, gpuSelection()));                       // (:270)
+  }
+
+  public long gpuSelection() throws Exception {
+    if (output == 0) output = Native.bitmapCnf(ctx, nbits, cnfBitmaps, cnfOffsets, deleted);
+    return output;
+  }
+
+  public long gpuTable() {
+    return table;
+  }
+
+  public int[] fileColumns() {
+    return outIdx.clone();
   }
 
   public Tuple get_next() throws Exception {
@@ -138,7 +158,7 @@ public class GpuColumnarIndexScan extends Iterator {
     return Jtuple;
   }
 
-  /** true where the CNF ran as one GPU launch (false: the reference's positions) */
+  /** true where the CNF, positions and projection ran as one GPU launch (false: the reference's positions) */
   public boolean usedFusedCnf() {
     return fused;
   }
@@ -147,7 +167,8 @@ public class GpuColumnarIndexScan extends Iterator {
     if (!closeFlag) {
       if (cursor != 0) Native.cursorClose(cursor);
       if (output != 0) Native.bitmapFree(output);
-      cursor = output = 0;
+      if (deleted != 0) Native.bitmapFree(deleted);
+      cursor = output = deleted = 0;
       closeFlag = true;
     }
   }

@@ -17,7 +17,7 @@ import heap.Tuple;
  * are left unset -- the reference's callers (DeleteQuery -> markTupleDeleted,
  * R/columnar/Columnarfile.java:812-830) read only the position.
  */
-public class GpuColumnarFileScan extends Iterator {
+public class GpuColumnarFileScan extends Iterator implements GpuSelection {
   static final int BATCH = 8192;
 
   private final long ctx, table, plan;
@@ -88,6 +88,18 @@ public class GpuColumnarFileScan extends Iterator {
   public TID get_next_tid() throws Exception {
     if (!fill()) return null;
     return new TID(len_in1, (int) ids[i++]);
+  }
+
+  public long gpuTable() {
+    return table;
+  }
+
+  public long gpuSelection() {
+    return selection;
+  }
+
+  public int[] fileColumns() {
+    return proj.clone();
   }
 
   /** the whole selection's size (Query's resultCount) without materialising it */

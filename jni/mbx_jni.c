@@ -28,6 +28,7 @@
 
 #include "../include/mbx.h"
 #include "../include/mbx_db.h"
+#include "../include/mbx_join.h"
 
 #define H(p) ((jlong)(intptr_t)(p))
 #define P(T, j) ((T *)(intptr_t)(j))
@@ -313,6 +314,49 @@ JNIEXPORT jlong JNICALL Java_global_Native_dbBitmapStage(JNIEnv *env, jclass cls
   return H(b);
 }
 
+/* one shard of a Columnarfile: positions [row_begin, row_end), only its pages read */
+JNIEXPORT jlong JNICALL Java_global_Native_dbStageRange(JNIEnv *env, jclass cls, jlong ctx, jlong db, jstring name,
+                                                        jlong row_begin, jlong row_end) {
+  (void)cls;
+  const char *n = (*env)->GetStringUTFChars(env, name, NULL);
+  mbx_table *t = NULL;
+  const int rc = n ? mbx_db_stage_range(P(mbx_ctx, ctx), P(mbx_db, db), n, row_begin, row_end, &t) : MBX_E_INVALID;
+  if (n) (*env)->ReleaseStringUTFChars(env, name, n);
+  check(env, rc, kFileScan);
+  return H(t);
+}
+
+/* a shard's slice of a BitMapFile */
+JNIEXPORT jlong JNICALL Java_global_Native_dbBitmapStageRange(JNIEnv *env, jclass cls, jlong ctx, jlong db,
+                                                              jstring file, jlong bit_begin, jlong nbits) {
+  (void)cls;
+  const char *n = (*env)->GetStringUTFChars(env, file, NULL);
+  mbx_bitmap *b = NULL;
+  const int rc =
+      n ? mbx_db_bitmap_stage_range(P(mbx_ctx, ctx), P(mbx_db, db), n, bit_begin, nbits, &b) : MBX_E_INVALID;
+  if (n) (*env)->ReleaseStringUTFChars(env, file, n);
+  check(env, rc, kIndex);
+  return H(b);
+}
+
+JNIEXPORT jlong JNICALL Java_global_Native_dbColumnarRows(JNIEnv *env, jclass cls, jlong db, jstring name) {
+  (void)cls;
+  const char *n = (*env)->GetStringUTFChars(env, name, NULL);
+  int64_t nrows = 0;
+  const int rc = n ? mbx_db_columnar_info(P(mbx_db, db), n, 0, NULL, NULL, NULL, &nrows, NULL) : MBX_E_INVALID;
+  if (n) (*env)->ReleaseStringUTFChars(env, name, n);
+  check(env, rc, kFileScan);
+  return nrows;
+}
+
+JNIEXPORT jlong JNICALL Java_global_Native_tableRowOffset(JNIEnv *env, jclass cls, jlong t) {
+  (void)cls;
+  int64_t nrows = 0, row_offset = 0;
+  int32_t ncols = 0;
+  check(env, mbx_table_info(P(mbx_table, t), &nrows, &row_offset, &ncols), kFileScan);
+  return row_offset;
+}
+
 /* ---- plans and scans ----------------------------------------------------- */
 
 JNIEXPORT jlong JNICALL Java_global_Native_planCompile(JNIEnv *env, jclass cls, jlong ctx, jlong table,
@@ -355,6 +399,10 @@ JNIEXPORT jlong JNICALL Java_global_Native_scanBitmap(JNIEnv *env, jclass cls, j
 /* the get_next_tid stream as positions (DeleteQuery; R/iterator/ColumnarFileScan.java:174-188) */
 JNIEXPORT jlongArray JNICALL Java_global_Native_scanSelect(JNIEnv *env, jclass cls, jlong ctx, jlong plan, jlong cap) {
   (void)cls;
+  /* a Java long[] holds at most Integer.MAX_VALUE - 8 elements: a larger
+   * selection raises (mbx_scan_select's capacity check) instead of wrapping */
+  const jlong max_java = 0x7ffffff7;
+  if (cap > max_java) cap = max_java;
   int64_t *ids = (int64_t *)malloc(sizeof(int64_t) * (size_t)(cap > 0 ? cap : 1));
   if (!ids) {
     throw_chain(env, kChain, "scanSelect: host allocation");
@@ -477,8 +525,8 @@ JNIEXPORT jlong JNICALL Java_global_Native_bitmapCnf(JNIEnv *env, jclass cls, jl
   return H(out);
 }
 
-/* ColumnarIndexScan in one launch: the CNF of index BitSets + positions (devIds 0: none) + up to 4 int /
- * float projected columns into device slots (devAlloc); waits, returns the selected row count */
+/* ColumnarIndexScan in one launch: the CNF of index BitSets + positions (devIds 0: none) + the projected
+ * columns' rows into device slots (devAlloc); waits, returns the selected row count */
 JNIEXPORT jlong JNICALL Java_global_Native_cnfMaterialize(JNIEnv *env, jclass cls, jlong ctx, jlong table,
                                                           jlongArray bms, jintArray conj_offsets, jlong deleted,
                                                           jintArray proj, jlong dev_ids, jlongArray dev_out,
@@ -501,12 +549,14 @@ JNIEXPORT jlong JNICALL Java_global_Native_cnfMaterialize(JNIEnv *env, jclass cl
   if (v && outs && o && (nb == 0 || h) && (np == 0 || (pj && d))) {
     for (jsize i = 0; i < nb; i++) v[i] = P(const mbx_bitmap, h[i]);
     for (jsize j = 0; j < np; j++) outs[j] = P(void, d[j]);
+    /* the download waits for this launch on the context stream; it does not
+     * consume the sticky NaN word an earlier async scan may have left (that
+     * one is raised by the next Native.sync, where it belongs) */
     if (!check(env, mbx_cnf_materialize_async(P(mbx_ctx, ctx), P(const mbx_table, table), v, (const int32_t *)o,
                                               (int32_t)(no - 1), P(const mbx_bitmap, deleted),
                                               (const int32_t *)pj, (int32_t)np, P(int64_t, dev_ids), outs,
                                               P(int64_t, dev_count)),
-               kIndex) &&
-        !check(env, mbx_sync(P(mbx_ctx, ctx)), kIndex))
+               kIndex))
       check(env, mbx_dev_download(P(mbx_ctx, ctx), P(void, dev_count), &count, sizeof(count)), kChain);
   } else {
     throw_chain(env, kChain, "cnfMaterialize: host allocation");
@@ -550,11 +600,116 @@ JNIEXPORT jlong JNICALL Java_global_Native_cursorOpen(JNIEnv *env, jclass cls, j
   return H(c);
 }
 
+/* bitmap handles + conjunct offsets of a CNF, borrowed for one call */
+typedef struct {
+  const mbx_bitmap **v;
+  jlong *h;
+  jint *o;
+  jint *pj;
+  jsize nb, no, np;
+} CnfArgs;
+
+static int cnf_args_get(JNIEnv *env, jlongArray bms, jintArray conj_offsets, jintArray proj, CnfArgs *a) {
+  memset(a, 0, sizeof(*a));
+  a->nb = (*env)->GetArrayLength(env, bms);
+  a->no = (*env)->GetArrayLength(env, conj_offsets);
+  a->np = proj ? (*env)->GetArrayLength(env, proj) : 0;
+  if (a->no < 1) {
+    throw_chain(env, kIndex, "CNF: conj_offsets needs nconj + 1 entries");
+    return -1;
+  }
+  a->v = (const mbx_bitmap **)calloc((size_t)(a->nb > 0 ? a->nb : 1), sizeof(void *));
+  a->h = a->nb > 0 ? (*env)->GetLongArrayElements(env, bms, NULL) : NULL;
+  a->o = (*env)->GetIntArrayElements(env, conj_offsets, NULL);
+  a->pj = a->np > 0 ? (*env)->GetIntArrayElements(env, proj, NULL) : NULL;
+  if (!a->v || !a->o || (a->nb > 0 && !a->h) || (a->np > 0 && !a->pj)) {
+    throw_chain(env, kChain, "CNF: host allocation");
+    return -1;
+  }
+  for (jsize i = 0; i < a->nb; i++) a->v[i] = P(const mbx_bitmap, a->h[i]);
+  return 0;
+}
+
+static void cnf_args_release(JNIEnv *env, jlongArray bms, jintArray conj_offsets, jintArray proj, CnfArgs *a) {
+  if (a->h) (*env)->ReleaseLongArrayElements(env, bms, a->h, JNI_ABORT);
+  if (a->o) (*env)->ReleaseIntArrayElements(env, conj_offsets, a->o, JNI_ABORT);
+  if (a->pj) (*env)->ReleaseIntArrayElements(env, proj, a->pj, JNI_ABORT);
+  free(a->v);
+}
+
+/* ColumnarIndexScan (R/index/ColumnarIndexScan.java:79-182, get_next :287-308) in one launch, as a cursor */
+JNIEXPORT jlong JNICALL Java_global_Native_cnfCursorOpen(JNIEnv *env, jclass cls, jlong ctx, jlong table,
+                                                         jlongArray bms, jintArray conj_offsets, jlong deleted,
+                                                         jintArray proj) {
+  (void)cls;
+  CnfArgs a;
+  mbx_cursor *c = NULL;
+  if (cnf_args_get(env, bms, conj_offsets, proj, &a) == 0)
+    check(env,
+          mbx_cnf_cursor_open(P(mbx_ctx, ctx), P(const mbx_table, table), a.v, (const int32_t *)a.o,
+                              (int32_t)(a.no - 1), P(const mbx_bitmap, deleted), (const int32_t *)a.pj,
+                              (int32_t)a.np, &c),
+          kIndex);
+  cnf_args_release(env, bms, conj_offsets, proj, &a);
+  return H(c);
+}
+
+/* launch only: {cursor, device pointer of its count} (the count feeds the shards' exchange) */
+JNIEXPORT jlongArray JNICALL Java_global_Native_cnfCursorLaunch(JNIEnv *env, jclass cls, jlong ctx, jlong table,
+                                                               jlongArray bms, jintArray conj_offsets, jlong deleted,
+                                                               jintArray proj) {
+  (void)cls;
+  CnfArgs a;
+  mbx_cursor *c = NULL;
+  int64_t *dcount = NULL;
+  jlongArray out = NULL;
+  if (cnf_args_get(env, bms, conj_offsets, proj, &a) == 0 &&
+      !check(env,
+             mbx_cnf_cursor_launch(P(mbx_ctx, ctx), P(const mbx_table, table), a.v, (const int32_t *)a.o,
+                                   (int32_t)(a.no - 1), P(const mbx_bitmap, deleted), (const int32_t *)a.pj,
+                                   (int32_t)a.np, &c, &dcount),
+             kIndex)) {
+    jlong v[2] = {H(c), H(dcount)};
+    out = (*env)->NewLongArray(env, 2);
+    if (out) (*env)->SetLongArrayRegion(env, out, 0, 2, v);
+    else mbx_cursor_close(c);
+  }
+  cnf_args_release(env, bms, conj_offsets, proj, &a);
+  return out;
+}
+
 JNIEXPORT jlong JNICALL Java_global_Native_cursorCount(JNIEnv *env, jclass cls, jlong cur) {
   (void)cls;
   int64_t n = 0;
   check(env, mbx_cursor_count(P(mbx_cursor, cur), &n), kFileScan);
   return n;
+}
+
+/* n values of one projected column in the mbx_materialize host layout ->
+ * int[] / float[] / String[] (char(n): zero-padded modified UTF-8,
+ * NUL-terminated for NewStringUTF) */
+static jobject column_array(JNIEnv *env, jint type, jshort size, const void *buf, int64_t n, jclass strc) {
+  jobject col = NULL;
+  if (type == MBX_ATTR_INTEGER) {
+    col = (*env)->NewIntArray(env, (jsize)n);
+    if (col) (*env)->SetIntArrayRegion(env, (jintArray)col, 0, (jsize)n, (const jint *)buf);
+  } else if (type == MBX_ATTR_REAL) {
+    col = (*env)->NewFloatArray(env, (jsize)n);
+    if (col) (*env)->SetFloatArrayRegion(env, (jfloatArray)col, 0, (jsize)n, (const jfloat *)buf);
+  } else {
+    jobjectArray sa = (*env)->NewObjectArray(env, (jsize)n, strc, NULL);
+    char *tmp = (char *)malloc((size_t)size + 1);
+    for (int64_t r = 0; sa && tmp && r < n; r++) {
+      memcpy(tmp, (const char *)buf + r * size, (size_t)size);
+      tmp[size] = 0;
+      jstring js = (*env)->NewStringUTF(env, tmp);
+      (*env)->SetObjectArrayElement(env, sa, (jsize)r, js);
+      (*env)->DeleteLocalRef(env, js);
+    }
+    free(tmp);
+    col = sa;
+  }
+  return col;
 }
 
 /* The next <= max_rows rows: {long[] positions, Object[] columns}, a column
@@ -590,26 +745,7 @@ JNIEXPORT jobjectArray JNICALL Java_global_Native_cursorNext(JNIEnv *env, jclass
     jlongArray jids = (*env)->NewLongArray(env, (jsize)n);
     if (jids) (*env)->SetLongArrayRegion(env, jids, 0, (jsize)n, (const jlong *)ids);
     for (jsize j = 0; cols && j < np; j++) {
-      jobject col = NULL;
-      if (t[j] == MBX_ATTR_INTEGER) {
-        col = (*env)->NewIntArray(env, (jsize)n);
-        if (col) (*env)->SetIntArrayRegion(env, (jintArray)col, 0, (jsize)n, (const jint *)bufs[j]);
-      } else if (t[j] == MBX_ATTR_REAL) {
-        col = (*env)->NewFloatArray(env, (jsize)n);
-        if (col) (*env)->SetFloatArrayRegion(env, (jfloatArray)col, 0, (jsize)n, (const jfloat *)bufs[j]);
-      } else { /* char(n): zero-padded modified UTF-8, NUL-terminated for NewStringUTF */
-        jobjectArray sa = (*env)->NewObjectArray(env, (jsize)n, strc, NULL);
-        char *tmp = (char *)malloc((size_t)s[j] + 1);
-        for (int64_t r = 0; sa && tmp && r < n; r++) {
-          memcpy(tmp, (const char *)bufs[j] + r * s[j], (size_t)s[j]);
-          tmp[s[j]] = 0;
-          jstring js = (*env)->NewStringUTF(env, tmp);
-          (*env)->SetObjectArrayElement(env, sa, (jsize)r, js);
-          (*env)->DeleteLocalRef(env, js);
-        }
-        free(tmp);
-        col = sa;
-      }
+      jobject col = column_array(env, t[j], s[j], bufs[j], n, strc);
       (*env)->SetObjectArrayElement(env, cols, j, col);
       (*env)->DeleteLocalRef(env, col);
     }
@@ -785,4 +921,182 @@ JNIEXPORT void JNICALL Java_global_Native_commAllreduceAggAll(JNIEnv *env, jclas
     check(env, mbx_comm_allreduce_agg_all(cv, (int32_t)n, (mbx_agg *const *)pv), kChain);
   free(cv);
   free(pv);
+}
+
+JNIEXPORT void JNICALL Java_global_Native_commAllgatherCountAll(JNIEnv *env, jclass cls, jlongArray comms,
+                                                                jlongArray dev_counts, jlongArray dev_alls) {
+  (void)cls;
+  mbx_comm **cv = NULL, **cv2 = NULL;
+  void **pv = NULL, **av = NULL;
+  jsize n = 0, n2 = 0;
+  if (ptrs_of(env, comms, dev_counts, &cv, &pv, &n) || ptrs_of(env, comms, dev_alls, &cv2, &av, &n2))
+    throw_chain(env, kChain, "commAllgatherCountAll: one device count and one result slot per communicator");
+  else
+    check(env, mbx_comm_allgather_count_all(cv, (int32_t)n, (const int64_t *const *)pv, (int64_t *const *)av),
+          kChain);
+  free(cv);
+  free(pv);
+  free(cv2);
+  free(av);
+}
+
+/* the context stream waits (on the device) for the collectives enqueued so far */
+JNIEXPORT void JNICALL Java_global_Native_commWait(JNIEnv *env, jclass cls, jlong comm) {
+  (void)cls;
+  check(env, mbx_comm_wait(P(mbx_comm, comm)), kChain);
+}
+
+JNIEXPORT jlongArray JNICALL Java_global_Native_longsDownload(JNIEnv *env, jclass cls, jlong ctx, jlong dev, jint n) {
+  (void)cls;
+  if (n < 0) {
+    throw_chain(env, kChain, "longsDownload: n < 0");
+    return NULL;
+  }
+  jlong *v = (jlong *)calloc((size_t)(n > 0 ? n : 1), sizeof(jlong));
+  jlongArray out = NULL;
+  if (!v) {
+    throw_chain(env, kChain, "longsDownload: host allocation");
+    return NULL;
+  }
+  if (!check(env, mbx_dev_download(P(mbx_ctx, ctx), P(void, dev), v, (int64_t)n * (int64_t)sizeof(jlong)), kChain)) {
+    out = (*env)->NewLongArray(env, n);
+    if (out) (*env)->SetLongArrayRegion(env, out, 0, n, v);
+  }
+  free(v);
+  return out;
+}
+
+/* ---- joins (include/mbx_join.h): ColumnarNestedLoopJoins / BitMapQuery pairs -- */
+
+JNIEXPORT jlong JNICALL Java_global_Native_join(JNIEnv *env, jclass cls, jlong ctx, jlong outer, jlong outer_sel,
+                                                jlong inner, jlong inner_sel, jintArray terms, jintArray conj_offsets,
+                                                jint order, jlong outer_block) {
+  (void)cls;
+  const jsize nt3 = (*env)->GetArrayLength(env, terms);
+  const jsize no = (*env)->GetArrayLength(env, conj_offsets);
+  if (nt3 % 3 != 0 || no < 1 || nt3 / 3 > MBX_MAX_JOIN_TERMS) {
+    throw_chain(env, kChain, "join: terms are {op, outerCol, innerCol} triples, conj_offsets nconj + 1 entries");
+    return 0;
+  }
+  mbx_join_term jt[MBX_MAX_JOIN_TERMS];
+  jint *t = nt3 > 0 ? (*env)->GetIntArrayElements(env, terms, NULL) : NULL;
+  jint *o = (*env)->GetIntArrayElements(env, conj_offsets, NULL);
+  mbx_join_result *r = NULL;
+  if ((nt3 > 0 && !t) || !o) {
+    throw_chain(env, kChain, "join: host allocation");
+  } else {
+    for (jsize k = 0; k < nt3 / 3; k++) {
+      jt[k].op = t[3 * k];
+      jt[k].outer_col = t[3 * k + 1];
+      jt[k].inner_col = t[3 * k + 2];
+      jt[k].pad_ = 0;
+    }
+    mbx_join_cnf cnf;
+    cnf.terms = jt;
+    cnf.conj_offsets = (const int32_t *)o;
+    cnf.nconj = (int32_t)(no - 1);
+    check(env,
+          mbx_join(P(mbx_ctx, ctx), P(const mbx_table, outer), P(const mbx_bitmap, outer_sel),
+                   P(const mbx_table, inner), P(const mbx_bitmap, inner_sel), &cnf, order, outer_block, &r),
+          kChain);
+  }
+  if (t) (*env)->ReleaseIntArrayElements(env, terms, t, JNI_ABORT);
+  if (o) (*env)->ReleaseIntArrayElements(env, conj_offsets, o, JNI_ABORT);
+  return H(r);
+}
+
+JNIEXPORT jlongArray JNICALL Java_global_Native_joinInfo(JNIEnv *env, jclass cls, jlong res) {
+  (void)cls;
+  int64_t count = 0, passes = 0;
+  if (check(env, mbx_join_info(P(const mbx_join_result, res), &count, &passes), kChain)) return NULL;
+  jlong v[2] = {count, passes};
+  jlongArray out = (*env)->NewLongArray(env, 2);
+  if (out) (*env)->SetLongArrayRegion(env, out, 0, 2, v);
+  return out;
+}
+
+/* pairs [start, start + n): {long[] outer positions, long[] inner positions, int[] pass} */
+JNIEXPORT jobjectArray JNICALL Java_global_Native_joinFetch(JNIEnv *env, jclass cls, jlong ctx, jlong res, jlong start,
+                                                            jint n) {
+  (void)cls;
+  if (n < 0 || start < 0) {
+    throw_chain(env, kChain, "joinFetch: bad range");
+    return NULL;
+  }
+  int64_t *op = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int64_t *ip = (int64_t *)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int32_t *ps = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n > 0 ? n : 1));
+  jobjectArray out = NULL;
+  if (!op || !ip || !ps) {
+    throw_chain(env, kChain, "joinFetch: host allocation");
+  } else if (!check(env, mbx_join_fetch(P(mbx_ctx, ctx), P(const mbx_join_result, res), start, n, op, ip, ps),
+                    kChain)) {
+    jclass objc = (*env)->FindClass(env, "java/lang/Object");
+    jlongArray jo = (*env)->NewLongArray(env, n);
+    jlongArray ji = (*env)->NewLongArray(env, n);
+    jintArray jp = (*env)->NewIntArray(env, n);
+    if (jo) (*env)->SetLongArrayRegion(env, jo, 0, n, (const jlong *)op);
+    if (ji) (*env)->SetLongArrayRegion(env, ji, 0, n, (const jlong *)ip);
+    if (jp) (*env)->SetIntArrayRegion(env, jp, 0, n, (const jint *)ps);
+    out = objc ? (*env)->NewObjectArray(env, 3, objc, NULL) : NULL;
+    if (out) {
+      (*env)->SetObjectArrayElement(env, out, 0, jo);
+      (*env)->SetObjectArrayElement(env, out, 1, ji);
+      (*env)->SetObjectArrayElement(env, out, 2, jp);
+    }
+  }
+  free(op);
+  free(ip);
+  free(ps);
+  return out;
+}
+
+JNIEXPORT void JNICALL Java_global_Native_joinFree(JNIEnv *env, jclass cls, jlong res) {
+  (void)env, (void)cls;
+  mbx_join_free(P(mbx_join_result, res));
+}
+
+/* late materialisation by explicit positions (Heapfile.findRID + getRecord per value) */
+JNIEXPORT jobjectArray JNICALL Java_global_Native_gather(JNIEnv *env, jclass cls, jlong ctx, jlong table,
+                                                         jlongArray positions, jintArray proj, jintArray types,
+                                                         jshortArray sizes) {
+  (void)cls;
+  const jsize n = (*env)->GetArrayLength(env, positions);
+  const jsize np = (*env)->GetArrayLength(env, proj);
+  if ((*env)->GetArrayLength(env, types) != np || (*env)->GetArrayLength(env, sizes) != np) {
+    throw_chain(env, kChain, "gather: proj / types / sizes disagree");
+    return NULL;
+  }
+  jlong *pos = n > 0 ? (*env)->GetLongArrayElements(env, positions, NULL) : NULL;
+  jint *pj = np > 0 ? (*env)->GetIntArrayElements(env, proj, NULL) : NULL;
+  jint *t = np > 0 ? (*env)->GetIntArrayElements(env, types, NULL) : NULL;
+  jshort *s = np > 0 ? (*env)->GetShortArrayElements(env, sizes, NULL) : NULL;
+  void **bufs = (void **)calloc((size_t)(np > 0 ? np : 1), sizeof(void *));
+  int bad = !bufs || (n > 0 && !pos) || (np > 0 && (!pj || !t || !s));
+  for (jsize j = 0; !bad && j < np; j++) {
+    bufs[j] = malloc((t[j] == MBX_ATTR_STRING ? (size_t)s[j] : 4) * (size_t)(n > 0 ? n : 1));
+    bad = !bufs[j];
+  }
+  jobjectArray out = NULL;
+  if (bad) {
+    throw_chain(env, kChain, "gather: host allocation");
+  } else if (!check(env, mbx_gather(P(mbx_ctx, ctx), P(const mbx_table, table), (const int64_t *)pos, n,
+                                    (const int32_t *)pj, (int32_t)np, bufs),
+                    kFileScan)) {
+    jclass objc = (*env)->FindClass(env, "java/lang/Object");
+    jclass strc = (*env)->FindClass(env, "java/lang/String");
+    out = objc ? (*env)->NewObjectArray(env, np, objc, NULL) : NULL;
+    for (jsize j = 0; out && j < np; j++) {
+      jobject col = column_array(env, t[j], s[j], bufs[j], n, strc);
+      (*env)->SetObjectArrayElement(env, out, j, col);
+      (*env)->DeleteLocalRef(env, col);
+    }
+  }
+  for (jsize j = 0; bufs && j < np; j++) free(bufs[j]);
+  free(bufs);
+  if (pos) (*env)->ReleaseLongArrayElements(env, positions, pos, JNI_ABORT);
+  if (pj) (*env)->ReleaseIntArrayElements(env, proj, pj, JNI_ABORT);
+  if (t) (*env)->ReleaseIntArrayElements(env, types, t, JNI_ABORT);
+  if (s) (*env)->ReleaseShortArrayElements(env, sizes, s, JNI_ABORT);
+  return out;
 }

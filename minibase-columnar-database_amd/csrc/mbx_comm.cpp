@@ -294,6 +294,29 @@ extern "C" int mbx_comm_allreduce_count_all(mbx_comm* const* comms, int32_t n, i
   return MBX_OK;
 }
 
+extern "C" int mbx_comm_allgather_count_all(mbx_comm* const* comms, int32_t n, const int64_t* const* dev_counts,
+                                            int64_t* const* dev_alls) {
+  if (int rc = check_all(comms, n)) return rc;
+  NOTNULL(dev_counts);
+  NOTNULL(dev_alls);
+  for (int32_t i = 0; i < n; ++i) {
+    NOTNULL(dev_counts[i]);
+    NOTNULL(dev_alls[i]);
+    HIPCHK(hipSetDevice(comms[i]->ctx->device));
+    if (int rc = fork_after_main(comms[i])) return rc;
+  }
+  NCCLCHK(ncclGroupStart());
+  for (int32_t i = 0; i < n; ++i) {
+    const ncclResult_t r = ncclAllGather(dev_counts[i], dev_alls[i], 1, ncclInt64, comms[i]->nc, comms[i]->xs);
+    if (r != ncclSuccess) {
+      ncclGroupEnd();
+      return fail(MBX_E_DEVICE, "ncclAllGather (rank %d): %s", i, ncclGetErrorString(r));
+    }
+  }
+  NCCLCHK(ncclGroupEnd());
+  return MBX_OK;
+}
+
 extern "C" int mbx_comm_allreduce_agg_all(mbx_comm* const* comms, int32_t n, mbx_agg* const* dev_recs) {
   if (int rc = check_all(comms, n)) return rc;
   NOTNULL(dev_recs);

@@ -750,6 +750,8 @@ struct ColumnPages {
   int32_t max_pid = -1;
 };
 
+int column_pages_lazy(mbx_db* db, const std::string& file, int32_t rec_len, ColumnPages* cp);
+
 int column_pages(mbx_db* db, const std::string& file, int32_t rec_len, ColumnPages* cp) {
   const int32_t first = get_file_entry(db, file);
   if (first == kInvalidPage) return fail(MBX_E_INVALID, "heapfile %s is missing", file.c_str());
@@ -792,8 +794,9 @@ extern "C" int mbx_db_columnar_info(mbx_db* db, const char* name, int32_t max_co
     }
   }
   if (nrows || live) {
+    // the directory + the last data pages' headers (not every data page)
     ColumnPages cp;
-    if ((rc = column_pages(db, std::string(name) + ".0", record_len(sc.cols[0]), &cp))) return rc;
+    if ((rc = column_pages_lazy(db, std::string(name) + ".0", record_len(sc.cols[0]), &cp))) return rc;
     if (nrows) *nrows = cp.nrows;
     if (live) {
       int64_t del = 0;

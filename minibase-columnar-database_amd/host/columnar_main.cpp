@@ -251,17 +251,42 @@ void query(const std::vector<std::string>& a) {
   }
 }
 
+struct IndexCnf {
+  std::vector<std::unique_ptr<CondExpr>> pool;
+  std::vector<CondExpr*> heads;
+  std::vector<IndexType> itypes;
+  std::vector<std::string> inames;
+};
+IndexCnf index_cnf(columnar::Columnarfile& cf, const std::string& spec);
+
 void indexes_query(const std::vector<std::string>& a) {
   if (a.size() < 6) throw std::runtime_error("Invalid number of attributes.");
   columnar::Columnarfile cf = open_cf(a[1], a[2]);
   Target t = targets(cf, a[3]);
   if (std::stoi(a[5]) < 1) throw std::runtime_error("NUMBUF is not more than 1.");
-  // MultiIndexQuery.buildCNFQueryCondExpr (R/input/MultiIndexQuery.java:159-230)
-  std::vector<std::unique_ptr<CondExpr>> pool;
-  std::vector<CondExpr*> heads;
-  std::vector<IndexType> itypes;
-  std::vector<std::string> inames;
-  for (const std::string& conj : split(a[4], '^')) {
+  IndexCnf q = index_cnf(cf, a[4]);
+  if (a[0] == "indexes_query_sharded") {
+    // test / bench hook (no reference command): the same query over row-range
+    // shards, one per GPU (index::ShardedColumnarIndexScan)
+    if (a.size() < 7) throw std::runtime_error("indexes_query_sharded: SHARDS missing");
+    global::GpuSet& gpus = global::GpuSet::get(std::stoi(a[6]));
+    index::ShardedColumnarIndexScan scan(&cf, gpus, (int)t.proj.size(), t.out_indexes, t.proj, q.heads.data());
+    print_rows(scan, cf, t);
+    return;
+  }
+  index::ColumnarIndexScan scan(&cf, {}, q.itypes, q.inames, cf.getAttributeTypes(), cf.getStringSizes(),
+                                cf.getFieldCount(), (int)t.proj.size(), t.out_indexes, t.proj, q.heads.data(), true);
+  print_rows(scan, cf, t);
+}
+
+// MultiIndexQuery.buildCNFQueryCondExpr (R/input/MultiIndexQuery.java:159-230)
+IndexCnf index_cnf(columnar::Columnarfile& cf, const std::string& spec) {
+  IndexCnf q;
+  auto& pool = q.pool;
+  auto& heads = q.heads;
+  auto& itypes = q.itypes;
+  auto& inames = q.inames;
+  for (const std::string& conj : split(spec, '^')) {
     if (conj.size() < 2 || conj.front() != '{' || conj.back() != '}') throw std::runtime_error("Invalid query format");
     CondExpr* head = nullptr;
     CondExpr* tail = nullptr;
@@ -293,9 +318,7 @@ void indexes_query(const std::vector<std::string>& a) {
     heads.push_back(head);
   }
   heads.push_back(nullptr);
-  index::ColumnarIndexScan scan(&cf, {}, itypes, inames, cf.getAttributeTypes(), cf.getStringSizes(),
-                                cf.getFieldCount(), (int)t.proj.size(), t.out_indexes, t.proj, heads.data(), true);
-  print_rows(scan, cf, t);
+  return q;
 }
 
 // ------------------------------------------------------------------ joins
@@ -708,7 +731,7 @@ int run() {
       if (a[0] == "batchinsert") batchinsert(a);
       else if (a[0] == "index") index_cmd(a);
       else if (a[0] == "query") query(a);
-      else if (a[0] == "indexes_query") indexes_query(a);
+      else if (a[0] == "indexes_query" || a[0] == "indexes_query_sharded") indexes_query(a);
       else if (a[0] == "nlj") nlj_cmd(a);
       else if (a[0] == "delete_query") delete_query(a);
       else if (a[0] == "bmj") bmj_cmd(a);

@@ -66,6 +66,40 @@ mbx_ctx* SystemDefs::ctx() {
   return g_ctx;
 }
 
+static std::map<int, std::unique_ptr<GpuSet>>& gpu_sets() {
+  static std::map<int, std::unique_ptr<GpuSet>>* sets = new std::map<int, std::unique_ptr<GpuSet>>();
+  return *sets;  // released by SystemDefs::shutdown, never at static destruction
+}
+
+GpuSet& GpuSet::get(int nshards) {
+  auto& sets = gpu_sets();
+  if (nshards < 1) throw chainexception::ChainException("GpuSet: " + std::to_string(nshards) + " shards");
+  auto it = sets.find(nshards);
+  if (it != sets.end()) return *it->second;
+  std::unique_ptr<GpuSet> g(new GpuSet());
+  int32_t nd = 0;
+  chk<chainexception::ChainException>(mbx_device_count(&nd), "GpuSet: device count");
+  if (nd < 1) throw chainexception::ChainException("GpuSet: no GPU visible");
+  for (int i = 0; i < nshards; i++) {
+    mbx_ctx* c = nullptr;
+    chk<chainexception::ChainException>(mbx_init(i % nd, &c), "GpuSet: context for shard " + std::to_string(i));
+    g->ctxs_.push_back(c);
+  }
+  if (nshards <= nd) {  // a device per shard: one RCCL clique
+    g->comms_.assign((size_t)nshards, nullptr);
+    chk<chainexception::ChainException>(mbx_comm_init_all(g->ctxs_.data(), nshards, g->comms_.data()),
+                                        "GpuSet: RCCL clique");
+  }
+  GpuSet& ref = *g;
+  sets[nshards] = std::move(g);
+  return ref;
+}
+
+GpuSet::~GpuSet() {
+  for (mbx_comm* m : comms_) mbx_comm_free(m);
+  for (mbx_ctx* c : ctxs_) mbx_free(c);
+}
+
 }  // namespace global
 namespace columnar {
 void close_all_files();
@@ -100,11 +134,14 @@ mbx_db* SystemDefs::open(const std::string& dbname, int num_pgs) {
 mbx_db* SystemDefs::db() { return g_db; }
 
 // flushAllPages + close: every device object goes before the context
+static std::map<int, std::unique_ptr<GpuSet>>& gpu_sets();
+
 void SystemDefs::shutdown() {
   columnar::close_all_files();
   for (auto& kv : open_dbs()) mbx_db_close(kv.second);
   open_dbs().clear();
   g_db = nullptr;
+  gpu_sets().clear();
   if (g_ctx) mbx_free(g_ctx);
   g_ctx = nullptr;
 }
@@ -398,6 +435,8 @@ int Columnarfile::colNameToIndex(const std::string& name) const {
 std::string Columnarfile::indexToColName(int idx) const { return impl_->names.at((size_t)idx); }
 
 // the DB file's pages -> HBM, records decoded by the GPU (mbx_db_stage)
+mbx_db* Columnarfile::db() const { return impl_->db; }
+
 mbx_table* Columnarfile::table() const {
   Impl& I = *impl_;
   if (I.table && !I.dirty) return I.table;
@@ -867,14 +906,20 @@ namespace index {
 using columnar::BitSetPtr;
 
 std::vector<BitSetPtr> ColumnIndexScan::valueBitmaps(const columnar::Columnarfile& cf, int colNo, const CondExpr& e) {
+  std::vector<BitSetPtr> out;
+  for (const std::string& k : valueKeys(cf, colNo, e)) out.push_back(cf.getBitmapIndex(colNo, k));
+  return out;
+}
+
+std::vector<std::string> ColumnIndexScan::valueKeys(const columnar::Columnarfile& cf, int colNo, const CondExpr& e) {
   const auto types = cf.getAttributeTypes();
   const bool str = types.at((size_t)colNo).attrType == AttrType::attrString;
   const std::string lit = str ? e.operand2.string : columnar::int_key(e.operand2.integer);
   const int op = e.op.attrOperator;
-  std::vector<BitSetPtr> out;
+  std::vector<std::string> out;
   using O = global::AttrOperator;
   // symbol = value (R/index/ColumnIndexScan.java:660-668)
-  if (op == O::aopEQ || op == O::aopLE || op == O::aopGE) out.push_back(cf.getBitmapIndex(colNo, lit));
+  if (op == O::aopEQ || op == O::aopLE || op == O::aopGE) out.push_back(lit);
   if (op == O::aopLT || op == O::aopLE || op == O::aopGT || op == O::aopGE || op == O::aopNE) {
     for (const std::string& other : cf.getBitmapValues(colNo)) {
       int c;  // sign(value.compareTo(other))
@@ -887,7 +932,7 @@ std::vector<BitSetPtr> ColumnIndexScan::valueBitmaps(const columnar::Columnarfil
       if ((op == O::aopLT || op == O::aopLE) && c > 0) take = true;   // :671-688
       if ((op == O::aopGT || op == O::aopGE) && c < 0) take = true;   // :691-709
       if (op == O::aopNE && c != 0) take = true;                      // :712-730
-      if (take) out.push_back(cf.getBitmapIndex(colNo, other));
+      if (take) out.push_back(other);
     }
   }
   return out;  // aopNOT / aopNOP / opRANGE: no value, an empty BitSet
@@ -1191,6 +1236,189 @@ void ColumnarIndexScan::close() {
 }
 void ColumnarIndexScan::restart() { rows_.restart(); }
 int ColumnarIndexScan::getTupleSize() { return Jtuple_.size(); }
+
+ShardedColumnarIndexScan::ShardedColumnarIndexScan(columnar::Columnarfile* cf, global::GpuSet& gpus, int noOutFlds,
+                                                   const std::vector<int>& out_indexes,
+                                                   const std::vector<FldSpec>& outFlds, CondExpr* const* selects)
+    : f_(cf), outIndexes_(out_indexes) {
+  if ((int)outFlds.size() != noOutFlds) throw IndexException("ShardedColumnarIndexScan: noOutFlds");
+  if (!selects || !selects[0]) throw IndexException("ShardedColumnarIndexScan: no selection");
+  const auto types = cf->getAttributeTypes();
+  const auto sizes = cf->getAttrSizes();
+  std::vector<AttrType> otypes;
+  std::vector<short> osizes;
+  for (int c : out_indexes) {
+    otypes.push_back(types.at((size_t)c));
+    if (types[(size_t)c].attrType == AttrType::attrString) osizes.push_back(sizes[(size_t)c]);
+  }
+  Jtuple_.setHdr(otypes, osizes);
+  // the conjuncts' terms and their constraint keys (:137-146)
+  struct Term {
+    const CondExpr* e;
+    int col;
+  };
+  std::vector<std::vector<Term>> conj;
+  std::set<std::string> keys;
+  for (int i = 0; selects[i]; i++) {
+    std::vector<Term> ts;
+    for (const CondExpr* e = selects[i]; e; e = e->next) {
+      if (e->type1.attrType != AttrType::attrSymbol || e->type2.attrType == AttrType::attrSymbol)
+        throw IndexException("IndexScan.java: invalid constraint");
+      const int col = e->operand1.symbol.offset - 1;
+      const std::string lit = e->type2.attrType == AttrType::attrInteger ? std::to_string(e->operand2.integer)
+                                                                          : e->operand2.string;
+      if (!keys.insert(cf->indexToColName(col) + e->op.toString() + lit + e->indexType.toString()).second)
+        throw IndexException("ShardedColumnarIndexScan: a repeated constraint (use ColumnarIndexScan)");
+      if (e->indexType.indexType != IndexType::B_Index && !cf->bitmapIndexExists(col))
+        throw IndexException("Bitmap index does not exist on column " + cf->indexToColName(col));
+      ts.push_back({e, col});
+    }
+    conj.push_back(ts);
+  }
+  mbx_db* db = cf->db();
+  const std::string& name = cf->get_fileName();
+  int64_t N = 0;
+  chk<IndexException>(mbx_db_columnar_info(db, name.c_str(), 0, nullptr, nullptr, nullptr, &N, nullptr),
+                      "ShardedColumnarIndexScan: positions");
+  const auto& ctxs = gpus.ctxs();
+  const int n = (int)ctxs.size();
+  std::vector<int32_t> proj(out_indexes.begin(), out_indexes.end());
+  std::vector<int64_t*> dcounts((size_t)n, nullptr);
+  tables_.assign((size_t)n, nullptr);
+  bitmaps_.assign((size_t)n, {});
+  for (int g = 0; g < n; g++) {
+    mbx_ctx* c = ctxs[(size_t)g];
+    int64_t b = 0, e = 0;
+    chk<IndexException>(mbx_shard_bounds(N, n, g, &b, &e), "shard bounds");
+    chk<IndexException>(mbx_db_stage_range(c, db, name.c_str(), b, e, &tables_[(size_t)g]),
+                        "shard " + std::to_string(g) + ": staging rows [" + std::to_string(b) + ", " +
+                            std::to_string(e) + ")");
+    int64_t nb = 0;
+    mbx_table_info(tables_[(size_t)g], &nb, nullptr, nullptr);
+    auto& owned = bitmaps_[(size_t)g];
+    auto slice = [&](const std::string& file) -> mbx_bitmap* {
+      int32_t head = -1;
+      chk<IndexException>(mbx_db_file_entry(db, file.c_str(), &head), "get_file_entry");
+      mbx_bitmap* z = nullptr;
+      if (head >= 0) {
+        chk<IndexException>(mbx_db_bitmap_stage_range(c, db, file.c_str(), b, nb, &z), "BitMapFile " + file);
+      } else {  // no BitMapFile for the value: the empty BitSet (Columnarfile.java:1124)
+        int64_t cnt = 0;
+        int32_t offs[2] = {0, 0};
+        chk<IndexException>(mbx_bitmap_cnf(c, nb, nullptr, offs, 1, nullptr, &z, &cnt), "empty BitSet");
+      }
+      owned.push_back(z);
+      return z;
+    };
+    mbx_bitmap* del = slice(name + ".md");
+    int64_t ndel = 0;
+    mbx_bitmap_info(del, nullptr, nullptr, &ndel);
+    std::vector<mbx_bitmap*> bms;
+    std::vector<int32_t> offs{0};
+    for (const auto& ts : conj) {
+      for (const Term& t : ts) {
+        if (t.e->indexType.indexType == IndexType::B_Index) {
+          // the B-tree branch selects the term's own rows: the scan on the shard
+          CondExpr one = *t.e;
+          one.next = nullptr;
+          CondExpr* arr[2] = {&one, nullptr};
+          iterator::CnfImage img = iterator::flatten(arr);
+          mbx_cnf cnf = img.view();
+          mbx_plan* p = nullptr;
+          chk<IndexException>(mbx_plan_compile(c, tables_[(size_t)g], &cnf, &p), "B_Index term");
+          mbx_bitmap* z = nullptr;
+          int64_t cnt = 0;
+          const int rc = mbx_scan_bitmap(c, p, &z, &cnt);
+          mbx_plan_free(p);
+          chk<IndexException>(rc, "B_Index term scan");
+          owned.push_back(z);
+          bms.push_back(z);
+        } else {
+          for (const std::string& k : ColumnIndexScan::valueKeys(*cf, t.col, *t.e))
+            bms.push_back(slice(name + ".bm." + std::to_string(t.col) + "." + k));
+        }
+      }
+      offs.push_back((int32_t)bms.size());
+    }
+    mbx_cursor* cur = nullptr;
+    chk<IndexException>(mbx_cnf_cursor_launch(c, tables_[(size_t)g], bms.data(), offs.data(), (int32_t)conj.size(),
+                                              ndel > 0 ? del : nullptr, proj.data(), (int32_t)proj.size(), &cur,
+                                              &dcounts[(size_t)g]),
+                        "shard " + std::to_string(g) + ": one-launch CNF + projection");
+    rows_.emplace_back(new iterator::CursorBatches());
+    rows_.back()->reset(cur, types, sizes, proj);
+  }
+  // the exchange: every shard's count to every GPU (the concatenation offsets)
+  std::vector<int64_t> counts((size_t)n, 0);
+  const auto& comms = gpus.comms();
+  if (!comms.empty()) {
+    std::vector<int64_t*> alls((size_t)n, nullptr);
+    for (int g = 0; g < n; g++)
+      chk<IndexException>(mbx_dev_alloc(ctxs[(size_t)g], (int64_t)sizeof(int64_t) * n, (void**)&alls[(size_t)g]),
+                          "device slots");
+    std::vector<const int64_t*> src(dcounts.begin(), dcounts.end());
+    int rc = mbx_comm_allgather_count_all(comms.data(), n, src.data(), alls.data());
+    if (rc == MBX_OK) rc = mbx_comm_wait(comms[0]);
+    if (rc == MBX_OK) rc = mbx_dev_download(ctxs[0], alls[0], counts.data(), (int64_t)sizeof(int64_t) * n);
+    for (int g = 0; g < n; g++) mbx_dev_free(ctxs[(size_t)g], alls[(size_t)g]);
+    chk<IndexException>(rc, "shard counts all-gather (RCCL)");
+    rccl_ = true;
+    for (int g = 0; g < n; g++)
+      if (rows_[(size_t)g]->count() != counts[(size_t)g])
+        throw IndexException("ShardedColumnarIndexScan: exchanged count differs from shard " + std::to_string(g));
+  } else {
+    for (int g = 0; g < n; g++) counts[(size_t)g] = rows_[(size_t)g]->count();
+  }
+  offsets_.assign((size_t)n + 1, 0);
+  for (int g = 0; g < n; g++) offsets_[(size_t)g + 1] = offsets_[(size_t)g] + counts[(size_t)g];
+  total_ = offsets_[(size_t)n];
+  if (trace_on()) {
+    fprintf(stderr, "trace: ShardedColumnarIndexScan: %d shards, exchange %s, counts", n, rccl_ ? "rccl" : "host");
+    for (int64_t k : counts) fprintf(stderr, " %lld", (long long)k);
+    fprintf(stderr, ", %lld rows\n", (long long)total_);
+  }
+}
+
+ShardedColumnarIndexScan::~ShardedColumnarIndexScan() { close(); }
+
+bool ShardedColumnarIndexScan::advance() {
+  while (shard_ < rows_.size()) {
+    if (rows_[shard_]->next()) return true;
+    shard_++;
+  }
+  return false;
+}
+
+heap::Tuple* ShardedColumnarIndexScan::get_next() {
+  if (!advance()) return nullptr;
+  rows_[shard_]->fill(Jtuple_);
+  return &Jtuple_;
+}
+
+global::TID ShardedColumnarIndexScan::get_next_tid() {
+  global::TID tid;
+  tid.numRIDs = f_->getFieldCount();
+  if (advance()) tid.position = rows_[shard_]->position();
+  return tid;
+}
+
+void ShardedColumnarIndexScan::close() {
+  if (closeFlag) return;
+  rows_.clear();
+  for (auto& v : bitmaps_)
+    for (mbx_bitmap* b : v) mbx_bitmap_free(b);
+  bitmaps_.clear();
+  for (mbx_table* t : tables_) mbx_table_free(t);
+  tables_.clear();
+  closeFlag = true;
+}
+
+void ShardedColumnarIndexScan::restart() {
+  for (auto& r : rows_) r->restart();
+  shard_ = 0;
+}
+
+int ShardedColumnarIndexScan::getTupleSize() { return Jtuple_.size(); }
 
 }  // namespace index
 

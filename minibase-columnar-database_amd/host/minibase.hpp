@@ -78,6 +78,23 @@ class SystemDefs {
   static bool exists(const std::string& dbname);
   static void shutdown();
 };
+
+// The GPUs a sharded scan runs on: one context per
+// shard -- shard g on device g % (visible devices) -- and, when every shard
+// has a device of its own, one RCCL clique over them (mbx_comm_init_all),
+// owned here and shared by every sharded scan of the process (a context
+// holds at most one communicator).  Cached per shard count.
+class GpuSet {
+ public:
+  static GpuSet& get(int nshards);
+  const std::vector<mbx_ctx*>& ctxs() const { return ctxs_; }
+  const std::vector<mbx_comm*>& comms() const { return comms_; }  // empty: devices repeat
+  ~GpuSet();
+
+ private:
+  std::vector<mbx_ctx*> ctxs_;
+  std::vector<mbx_comm*> comms_;
+};
 }  // namespace global
 
 namespace heap {
@@ -224,6 +241,7 @@ class Columnarfile {
   std::string indexToColName(int idx) const;
   const std::string& get_fileName() const { return name_; }
   mbx_table* table() const;  // staged on first use
+  mbx_db* db() const;        // the DB file (shards stage their row ranges from it)
 
   // bitmap index registry (createBitMapIndex :698-753, getBitmapIndex :1103-1127,
   // getBitmapValues :1138)
@@ -400,6 +418,8 @@ class ColumnIndexScan : public iterator::Iterator {
   // satisfies `v op literal`
   static std::vector<columnar::BitSetPtr> valueBitmaps(const columnar::Columnarfile& cf, int colNo,
                                                        const CondExpr& e);
+  // the same selection as value keys (BitMapFile cf.bm.<col>.<key>)
+  static std::vector<std::string> valueKeys(const columnar::Columnarfile& cf, int colNo, const CondExpr& e);
 
  private:
   void open_cursor();
@@ -445,6 +465,48 @@ class ColumnarIndexScan : public iterator::Iterator {
   heap::Tuple Jtuple_;
   iterator::CursorBatches rows_;
   bool fused_ = false;
+};
+// ColumnarIndexScan over row-range shards of one Columnarfile, one shard per
+// GPU: shard g holds positions
+// [s_g, s_{g+1}) (mbx_shard_bounds: multiples of 64), staged straight from
+// the DB file by range (mbx_db_stage_range) with its slice of every BitMapFile
+// the CNF names and of cf.md (mbx_db_bitmap_stage_range).  Every shard runs
+// the one-launch CNF + projection (mbx_cnf_cursor_launch) -- all GPUs in
+// flight together -- then ONE grouped RCCL all-gather of the per-shard counts
+// (mbx_comm_allgather_count_all) gives every shard its offset in the output;
+// get_next() walks the shards in order, which is the reference's ascending
+// nextSetBit order (R/index/ColumnarIndexScan.java:130-181, 270, 287-308).
+// Without a clique (shards sharing a device) the counts are read per shard.
+// Terms: Bitmap (value-set OR, ColumnIndexScan.getBitSet) or B_Index (the
+// term's scan on the shard); a repeated constraint (the reference's mutable
+// cache, :147-172) throws -- use ColumnarIndexScan.
+class ShardedColumnarIndexScan : public iterator::Iterator {
+ public:
+  ShardedColumnarIndexScan(columnar::Columnarfile* cf, global::GpuSet& gpus, int noOutFlds,
+                           const std::vector<int>& out_indexes, const std::vector<FldSpec>& outFlds,
+                           CondExpr* const* selects);
+  ~ShardedColumnarIndexScan();
+  heap::Tuple* get_next() override;
+  global::TID get_next_tid();
+  void close() override;
+  void restart() override;
+  int getTupleSize() override;
+  int64_t count() const { return total_; }
+  const std::vector<int64_t>& shardOffsets() const { return offsets_; }  // nshards + 1
+  bool exchangedOverRccl() const { return rccl_; }
+
+ private:
+  bool advance();
+  columnar::Columnarfile* f_;
+  std::vector<int> outIndexes_;
+  heap::Tuple Jtuple_;
+  std::vector<mbx_table*> tables_;
+  std::vector<std::vector<mbx_bitmap*>> bitmaps_;  // per shard, all staged slices
+  std::vector<std::unique_ptr<iterator::CursorBatches>> rows_;
+  std::vector<int64_t> offsets_;
+  int64_t total_ = 0;
+  size_t shard_ = 0;
+  bool rccl_ = false;
 };
 }  // namespace index
 

@@ -91,6 +91,7 @@ EXPORTS = [
     "mbx_diag_select_stamps", "mbx_dev_alloc", "mbx_dev_free", "mbx_dev_download", "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
     "mbx_comm_info", "mbx_comm_wait", "mbx_comm_allreduce_count_async", "mbx_comm_allreduce_agg_async",
     "mbx_comm_allgather_count_async", "mbx_comm_allreduce_count_all", "mbx_comm_allreduce_agg_all",
+    "mbx_comm_allgather_count_all",
     "mbx_graph_begin", "mbx_graph_end", "mbx_graph_launch", "mbx_graph_free",
     # include/mbx_db.h
     "mbx_db_create", "mbx_db_open", "mbx_db_close", "mbx_db_info", "mbx_db_file_entry", "mbx_db_columnar_create",
@@ -187,6 +188,7 @@ def lib():
         "mbx_comm_allgather_count_async": ([V, V, V], ctypes.c_int),
         "mbx_comm_allreduce_count_all": ([P(V), I32, P(V), I64], ctypes.c_int),
         "mbx_comm_allreduce_agg_all": ([P(V), I32, P(V)], ctypes.c_int),
+        "mbx_comm_allgather_count_all": ([P(V), I32, P(V), P(V)], ctypes.c_int),
         "mbx_graph_begin": ([V], ctypes.c_int),
         "mbx_graph_end": ([V, P(V)], ctypes.c_int),
         "mbx_graph_launch": ([V], ctypes.c_int),
@@ -685,6 +687,14 @@ def comm_allreduce_agg_all(comms, dev_ptrs):
     n = len(comms)
     _chk(lib().mbx_comm_allreduce_agg_all((ctypes.c_void_p * n)(*[c.h for c in comms]), n,
                                           (ctypes.c_void_p * n)(*dev_ptrs)))
+
+
+def comm_allgather_count_all(comms, dev_counts, dev_alls):
+    """one grouped all-gather of every rank's device count into every rank's
+    dev_alls buffer (nranks int64)"""
+    n = len(comms)
+    _chk(lib().mbx_comm_allgather_count_all((ctypes.c_void_p * n)(*[c.h for c in comms]), n,
+                                            (ctypes.c_void_p * n)(*dev_counts), (ctypes.c_void_p * n)(*dev_alls)))
 
 
 class Comm:

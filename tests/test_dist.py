@@ -48,6 +48,38 @@ def test_three_rank_gloo_combine_cpu():
     _spawn("oracle", world=3)
 
 
+def _db_files(tmp_path, n4=200_003, n5=150_001):
+    m = mbx_pkg.load()
+    c4, c5 = str(tmp_path / "c4db"), str(tmp_path / "c5db")
+    dist_worker.write_db(m, c4, dist_worker.c4_columns(n4), ["c0", "c1", "c2", "c3"], deleted_every=101)
+    dist_worker.write_db(m, c5, dist_worker.c5_columns(n5), ["c0", "c1", "c2"], deleted_every=89)
+    return m, c4, c5
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_db_file_shards_gloo_cpu(tmp_path, world):
+    """C4- / C5-shaped DB files split into row ranges, one rank each: the
+    per-rank answers (read by the DB reader restatement) combined through
+    dist.py equal the whole-file answer."""
+    _, c4, c5 = _db_files(tmp_path)
+    mp.spawn(dist_worker.run_db, args=(world, _port(), "oracle", c4, c5), nprocs=world, join=True)
+
+
+@pytest.mark.gpu
+def test_db_file_shards_gloo_gpu(tmp_path):
+    """The same with every rank staging its range straight from the DB files
+    on cuda:0 (mbx_db_stage_range / mbx_db_bitmap_stage_range, the bitmap
+    indexes built on the GPU first) and running the one-launch CNF cursor."""
+    m, c4, c5 = _db_files(tmp_path)
+    ctx = m.Context(0)
+    with m.mbx.Db(c4) as db:
+        t = ctx.stage_db(db, "cf")
+        for c in (2, 3):
+            assert ctx.create_bitmap_index(db, "cf", t, c) == 10
+    ctx.close()
+    mp.spawn(dist_worker.run_db, args=(2, _port(), "mbx", c4, c5), nprocs=2, join=True)
+
+
 def test_fold_aggregates_rank_order_and_empty_shards():
     """The one-collective combine's fold (dist.fold_aggregates): int64 sums
     exact, the double SUM added in rank order, MIN/MAX with empty shards
