@@ -9,10 +9,11 @@ executed as ONE kernel launch per GPU (k_scan_fast<2, COUNT>; its last block
 folds the per-block counts), plus -- on N > 1 GPUs -- the path's one exchange
 step: an in-place RCCL all-reduce of the COUNTs over xGMI, issued by libmbx
 (mbx_comm_allreduce_count_async) on the communicator's exchange stream, so
-the next scans overlap it.  The exchange is bucketed (--exchange-bucket,
-default 10 = one captured graph): every step's COUNT is combined over all
-ranks, 10 steps per collective -- a tiny all-reduce costs its latency, not
-its bytes, so 10x fewer collectives (--exchange-bucket 1: one per step).
+the next scans overlap it.  Every step (= query) has its own collective
+(--exchange-bucket 1, the default: SURVEY 8(e)'s per-query
+N_total / (max_k t_kernel,k + t_reduce)); --exchange-bucket B > 1 lets the
+COUNTs of B consecutive steps share one all-reduce (a diagnostic: a tiny
+all-reduce costs its latency, not its bytes).
 Inputs are resident in HBM before the timed region.
 
 Scaling:
@@ -170,8 +171,8 @@ def main():
                     help="global rows (strong scaling) or rows per GPU (weak)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured HIP graph (0: eager launches)")
-    ap.add_argument("--exchange-bucket", type=int, default=10,
-                    help="steps whose COUNTs share one all-reduce (1: one collective per step)")
+    ap.add_argument("--exchange-bucket", type=int, default=1,
+                    help="steps whose COUNTs share one all-reduce (1, the default: one collective per query)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -339,7 +340,9 @@ def main():
         ms_per_step = t_max * 1e3 / steps
         algo_bytes = 2 * 4 * n  # c0 + c1 read once per launch (rank 0's shard)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        xchg = (f"RCCL all-reduce of the COUNTs of every {B} steps (libmbx mbx_comm, exchange stream)"
+        xchg = ((f"RCCL all-reduce of the COUNTs of every {B} steps (libmbx mbx_comm, exchange stream)" if B > 1
+                 else "RCCL all-reduce of every step's COUNT (one collective per query; libmbx mbx_comm, "
+                      "exchange stream)")
                 if comm is not None else None) or (
             "gloo all-reduce (same-device rehearsal)" if exchange else "none")
         out = {

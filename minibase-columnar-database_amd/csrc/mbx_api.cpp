@@ -90,6 +90,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
   t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
+  if (t.select_blocks < 1) t.select_blocks = 1024;  // as mbx_set_tuning: never a zero / negative grid divisor
 }
 
 static int ensure_partials(mbx_ctx* c, int64_t n) {

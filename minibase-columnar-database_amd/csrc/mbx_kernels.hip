@@ -1978,6 +1978,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
                               void* const* out, int32_t nproj, int64_t* total, hipStream_t s, int32_t dbg,
                               int64_t* stamps, bool fuse_gather, int64_t max_blocks) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
+  if (max_blocks < 1) max_blocks = 1024;
   // ~max_blocks (1024) compaction blocks whatever the segment size: S segments per block
   const int64_t nseg = (nwords + words_per_block - 1) / words_per_block;
   const int64_t S = (nseg + max_blocks - 1) / max_blocks;
