@@ -89,6 +89,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.distinct_lds_probes = (int32_t)env_knob("MBX_DISTINCT_LDS_PROBES", -1);
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
+  t.cursor_prefetch = (int32_t)env_knob("MBX_CURSOR_PREFETCH", 1);
   t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
   if (t.select_blocks < 1) t.select_blocks = 1024;  // as mbx_set_tuning: never a zero / negative grid divisor
 }
@@ -282,6 +283,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "select_dbg")) t.select_dbg = v;
   else if (!strcmp(knob, "gather_fused")) t.gather_fused = v;
   else if (!strcmp(knob, "select_blocks")) t.select_blocks = v < 1 ? 1024 : (int32_t)v;
+  else if (!strcmp(knob, "cursor_prefetch")) t.cursor_prefetch = v;
   else return fail(MBX_E_INVALID, "mbx_set_tuning: unknown knob `%s`", knob);
   return MBX_OK;
 }
@@ -1621,7 +1623,7 @@ extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_id
   const int64_t nxt = k->next + take;
   const int64_t m = k->count - nxt < max_rows ? k->count - nxt : max_rows;
   HIPCHK(hipEventSynchronize(k->ev[b]));
-  if (m > 0) {
+  if (m > 0 && c->tune.cursor_prefetch) {
     if ((rc = cursor_fetch(k, b ^ 1, nxt, m))) return rc;
     k->pf_start = nxt;
     k->pf_n = m;
