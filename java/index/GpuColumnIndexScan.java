@@ -72,7 +72,7 @@ public class GpuColumnIndexScan extends Iterator {
 
   private boolean fill() throws Exception {
     if (i < n) return true;
-    Object[] r = Native.cursorNext(cursor, 8192, projTypes, projSizes);
+    Object[] r = Native.cursorNext(cursor, 65536, projTypes, projSizes);
     if (r == null) return false;
     ids = (long[]) r[0];
     batch = (Object[]) r[1];

@@ -139,7 +139,7 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
 
   public Tuple get_next() throws Exception {
     if (i == n) {
-      Object[] r = Native.cursorNext(cursor, 8192, projTypes, projSizes);
+      Object[] r = Native.cursorNext(cursor, 65536, projTypes, projSizes);
       if (r == null) return null;
       ids = (long[]) r[0];
       batch = (Object[]) r[1];

@@ -30,7 +30,7 @@ import iterator.TupleUtils;
  * IndexException -- use GpuColumnarIndexScan.
  */
 public class GpuShardedColumnarIndexScan extends Iterator {
-  static final int BATCH = 8192;
+  static final int BATCH = 65536;   // rows per cursor batch (bench_delivery: 64 Ki keeps the copy calls small)
 
   private final GpuShardedScan s;
   private final Tuple Jtuple = new Tuple();

@@ -21,7 +21,7 @@ import heap.Tuple;
  * reference (:55-60, :166-171).
  */
 public class GpuColumnarColumnScan extends Iterator implements GpuSelection {
-  static final int BATCH = 8192;
+  static final int BATCH = 65536;   // rows per cursor batch (bench_delivery: 64 Ki keeps the copy calls small)
 
   private final long ctx, table, plan;
   private long selection, cursor;

@@ -18,7 +18,7 @@ import heap.Tuple;
  * R/columnar/Columnarfile.java:812-830) read only the position.
  */
 public class GpuColumnarFileScan extends Iterator implements GpuSelection {
-  static final int BATCH = 8192;
+  static final int BATCH = 65536;   // rows per cursor batch (bench_delivery: 64 Ki keeps the copy calls small)
 
   private final long ctx, table, plan;
   private long selection, cursor;

@@ -25,7 +25,7 @@ import heap.Tuple;
  * (GpuSelection): their rows stay on the device.
  */
 public class GpuColumnarNestedLoopJoins extends Iterator implements GlobalConst {
-  static final int BATCH = 8192;
+  static final int BATCH = 65536;   // rows per cursor batch (bench_delivery: 64 Ki keeps the copy calls small)
 
   private final long ctx, res, outerTable, innerTable;
   private final List<Long> owned = new ArrayList<>();    // bitmaps this operator made

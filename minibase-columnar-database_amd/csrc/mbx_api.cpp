@@ -90,6 +90,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
   t.cursor_prefetch = (int32_t)env_knob("MBX_CURSOR_PREFETCH", 1);
+  t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 0);
   t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
   if (t.select_blocks < 1) t.select_blocks = 1024;  // as mbx_set_tuning: never a zero / negative grid divisor
 }
@@ -284,6 +285,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "gather_fused")) t.gather_fused = v;
   else if (!strcmp(knob, "select_blocks")) t.select_blocks = v < 1 ? 1024 : (int32_t)v;
   else if (!strcmp(knob, "cursor_prefetch")) t.cursor_prefetch = v;
+  else if (!strcmp(knob, "scan_select_fused")) t.scan_select_fused = v;
   else return fail(MBX_E_INVALID, "mbx_set_tuning: unknown knob `%s`", knob);
   return MBX_OK;
 }
@@ -853,9 +855,15 @@ static int32_t ticket_groups_of(const mbx_ctx* c) {
   return g > kMaxTicketGroups ? kDefaultTicketGroups : g;
 }
 
+// k_scan_select's extra arguments (a BitSet scan that also writes the positions)
+struct FusedSelect {
+  int64_t* ids;
+  int64_t* total;
+};
+
 static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int32_t mode, uint64_t* out_words,
                         Partial* parts, int64_t tpb, int64_t* count_out, AggOut* agg_out, int32_t* nan_out,
-                        int64_t* seg_counts = nullptr) {
+                        int64_t* seg_counts = nullptr, const FusedSelect* fused = nullptr) {
   ScanLaunch L;
   L.plan = v.dev;
   L.nrows = p->t->nrows;
@@ -890,6 +898,16 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
     L.fin_mode = kFinWriteThrough;
   if (L.fin_mode == kFinPackedCount && mode == kModeAgg) L.fin_mode = kFinWriteThrough;
   if (L.fin_mode == kFinSeparate) L.ticket = nullptr;
+  if (fused) {
+    int64_t* stamps = nullptr;
+    if (c->tune.select_dbg & 8) {  // diagnostic stamps (mbx_diag_select_stamps)
+      if (!c->stamps) HIPCHK(hipMalloc(&c->stamps, sizeof(int64_t) * 4 * kMaxStampBlocks));
+      stamps = c->stamps;
+    }
+    HIPCHK(launch_scan_select(L, c->lookback, p->t->row_offset, fused->ids, fused->total, c->stream, stamps,
+                              c->tune.select_dbg >> 4));
+    return MBX_OK;
+  }
   HIPCHK(launch_scan(L, c->stream));
   if (L.fin_mode == kFinSeparate)
     HIPCHK(launch_finalize(parts, grid_blocks(L.nrows, tpb), L.agg_kind, agg_out, count_out, nan_out, c->stream));
@@ -983,6 +1001,19 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
 // dev_ids holds every row's position.
 static int scan_select_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int64_t* dev_ids, int64_t* dev_count,
                             int32_t* dev_nan) {
+  if (c->tune.scan_select_fused && b->nbits == p->t->nrows) {
+    // one launch (k_scan_select): int literal terms on <= 4 four-byte columns
+    PlanVariant* v = nullptr;
+    int rc = plan_variant(p, -1, &v);
+    if (rc) return rc;
+    const int64_t tpb = b->wpb / kWordsPerTile;
+    if (c->tune.scan_ri != 0 && p->all_literal &&
+        scan_select_fusable(p->t->nrows, tpb, v->fast_k, v->fast_ks, p->host.nterms, p->host.has_real) &&
+        grid_blocks(p->t->nrows, tpb) == b->nseg) {
+      const FusedSelect f{dev_ids, dev_count};
+      return enqueue_scan(c, p, *v, kModeBitmap, b->words, c->partials, tpb, dev_count, nullptr, dev_nan, b->segc, &f);
+    }
+  }
   int rc = scan_bitmap_into(c, p, b, dev_nan);
   if (rc) return rc;
   return materialize_dev(c, p->t, b, nullptr, 0, p->t->row_offset, dev_ids, nullptr, dev_count);

@@ -297,6 +297,14 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
                                   int64_t* stamps = nullptr, int32_t dbg = 0);
 constexpr int64_t kLookbackWords = 1 + 2 * 1024;  // epoch, per-block counts, per-block inclusive prefixes
+// BitSet + positions + COUNT of a plan in one launch (k_scan_select): plans of
+// 1..4 int literal terms on 4-byte columns, tables whose segments fit the
+// one-launch form (scan_select_fusable); L as for a kModeBitmap scan (its
+// out_words / seg_counts: the BitSet and its segment counts)
+bool scan_select_fusable(int64_t nrows, int64_t tiles_per_block, int32_t fast_k, int32_t fast_ks, int32_t nterms,
+                         int32_t has_real);
+hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offset, int64_t* ids, int64_t* total,
+                              hipStream_t s, int64_t* stamps = nullptr, int32_t dbg = 0);
 hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                              int64_t words_per_block, uint64_t* out, int64_t* segc, hipStream_t s);
 hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* b, int64_t nwords,

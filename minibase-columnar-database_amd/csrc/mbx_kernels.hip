@@ -1378,81 +1378,22 @@ __device__ __forceinline__ uint64_t cnf_word(const BitmapCnf& C, int64_t w) {
 
 // G4: projected 4-byte columns the registers hold (kWide: any projection,
 // GT = GatherW); NB: 1..4 operands batched, 0: any
-template <int G4, int NB, class GT = Gather4>
-__global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
-                                                       int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
-                                                       int64_t* __restrict__ lb, int64_t row_offset,
-                                                       int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                       GT G, int64_t* __restrict__ stamps, int32_t dbg) {
-  // dbg bit 3: the chained look-back -- each block also publishes its
-  // inclusive prefix, and wave 0 walks back 64 predecessors per round to the
-  // nearest published one (~4 flag lines per block instead of every
-  // predecessor's); without it, every thread polls its predecessors' counts
-  // (diagnostic A/B of that form, select_dbg >> 4: bit 0 polls with a
-  // 1024-clock back-off, bit 1 skips the look-back's wait (wrong output: its
-  // cost), bit 2 takes the first poll round as plain nontemporal loads)
-  // stamps (diagnostic, select_dbg bit 3): per block wall_clock64() at start /
-  // count published / offset known / end
-  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
-  __shared__ int64_t wcount[kWaves];
-  __shared__ int64_t wpre[kWaves];
-  __shared__ uint16_t stage[kWaves][32 * 64];
-  const int lane = threadIdx.x & 63;
-  const int wave = (int)uniform(threadIdx.x >> 6);
-  // epochs 1 .. 2^31 - 1: epoch << 32 stays a positive int64
+// The part of a one-launch selection after each wave has formed its words
+// (k_cnf_select from index BitSets, k_scan_select from a predicate scan):
+// the block count is published, the output offset taken from the
+// predecessors (decoupled look-back), the leading steps' positions staged and
+// their projected values loaded before the offset is known, then positions +
+// values written.  wr / cached: the wave's words (lane = word) when its range
+// fits kSelRegs x 64 words; word_at(w) re-forms word w otherwise.  segc (may
+// be null): the block's count is also stored there.
+template <int G4, class GT, class WordAt>
+__device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int64_t c, bool cached, int64_t a0,
+                                            int64_t a1, WordAt word_at, int lane, int wave, int64_t* __restrict__ lb,
+                                            int64_t epoch, int64_t row_offset, int64_t* __restrict__ ids,
+                                            int64_t* __restrict__ total, const GT& G, int64_t* __restrict__ stamps,
+                                            int32_t dbg, int64_t* __restrict__ segc, int64_t* wcount, int64_t* wpre,
+                                            uint16_t (*stage)[32 * 64]) {
   int64_t* const inc = lb + 1 + kLookbackBlocks;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
-  const uint32_t prev = (uint32_t)lb[0];
-  const int64_t epoch = prev >= 0x7fffffffu ? 1 : (int64_t)prev + 1;
-  const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
-  const int64_t s1 = min(s0 + words_per_block, nwords);
-  const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
-  const int64_t a0 = min(s0 + wave * per, s1);
-  const int64_t a1 = min(a0 + per, s1);
-  const bool cached = a1 - a0 <= 64 * kSelRegs;
-  auto word_at = [&](int64_t w) -> uint64_t {
-    uint64_t r = cnf_word(C, w);
-    if (del) r &= ~del[w];
-    if (w == nwords - 1) r &= tail_mask;
-    return r;
-  };
-  uint64_t wr[kSelRegs];
-  int64_t c = 0;
-  if (NB > 0 && cached) {
-    // every operand word of the wave's range in flight at once (NB x 8
-    // register pairs: sized to the operand count)
-    uint64_t q[kSelRegs][NB > 0 ? NB : 1];
-#pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
-      const int64_t w = a0 + r * 64 + lane;
-#pragma unroll
-      for (int k = 0; k < NB; ++k) q[r][k] = w < a1 ? C.bms[k][w] : 0ull;
-    }
-#pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
-      const int64_t w = a0 + r * 64 + lane;
-      uint64_t x = ~0ull;
-      for (int cj = 0; cj < C.nconj; ++cj) {
-        uint64_t o = 0;
-#pragma unroll
-        for (int k = 0; k < NB; ++k)
-          if (k >= C.conj_off[cj] && k < C.conj_off[cj + 1]) o |= q[r][k];
-        x &= o;
-      }
-      if (del && w < a1) x &= ~del[w];
-      if (w == nwords - 1) x &= tail_mask;
-      wr[r] = w < a1 ? x : 0ull;
-      c += __popcll(wr[r]);
-    }
-  } else if (cached) {
-#pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
-      const int64_t w = a0 + r * 64 + lane;
-      wr[r] = w < a1 ? word_at(w) : 0ull;
-      c += __popcll(wr[r]);
-    }
-  } else {
-    for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(word_at(w));
-  }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
   if (lane == 0) wcount[wave] = c;
@@ -1461,6 +1402,7 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   for (int k = 0; k < kWaves; ++k) bc += wcount[k];
   if (threadIdx.x == 0) {
     __hip_atomic_store(&lb[1 + blockIdx.x], (epoch << 32) | bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (segc) segc[blockIdx.x] = bc;  // the block's segment count of the BitSet it formed (k_scan_select)
     if (stamps) stamps[4 * blockIdx.x + 1] = wall_clock64();
   }
   // look-back: the predecessors' counts, all polls of a thread in flight together
@@ -1608,6 +1550,182 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
     __syncthreads();
     if (threadIdx.x == 0) stamps[4 * blockIdx.x + 3] = wall_clock64();
   }
+}
+
+template <int G4, int NB, class GT = Gather4>
+__global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
+                                                       int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
+                                                       int64_t* __restrict__ lb, int64_t row_offset,
+                                                       int64_t* __restrict__ ids, int64_t* __restrict__ total,
+                                                       GT G, int64_t* __restrict__ stamps, int32_t dbg) {
+  // dbg bit 3: the chained look-back -- each block also publishes its
+  // inclusive prefix, and wave 0 walks back 64 predecessors per round to the
+  // nearest published one (~4 flag lines per block instead of every
+  // predecessor's); without it, every thread polls its predecessors' counts
+  // (diagnostic A/B of that form, select_dbg >> 4: bit 0 polls with a
+  // 1024-clock back-off, bit 1 skips the look-back's wait (wrong output: its
+  // cost), bit 2 takes the first poll round as plain nontemporal loads)
+  // stamps (diagnostic, select_dbg bit 3): per block wall_clock64() at start /
+  // count published / offset known / end
+  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
+  __shared__ int64_t wcount[kWaves];
+  __shared__ int64_t wpre[kWaves];
+  __shared__ uint16_t stage[kWaves][32 * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  // epochs 1 .. 2^31 - 1: epoch << 32 stays a positive int64
+  const uint32_t prev = (uint32_t)lb[0];
+  const int64_t epoch = prev >= 0x7fffffffu ? 1 : (int64_t)prev + 1;
+  const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
+  const int64_t s1 = min(s0 + words_per_block, nwords);
+  const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
+  const int64_t a0 = min(s0 + wave * per, s1);
+  const int64_t a1 = min(a0 + per, s1);
+  const bool cached = a1 - a0 <= 64 * kSelRegs;
+  auto word_at = [&](int64_t w) -> uint64_t {
+    uint64_t r = cnf_word(C, w);
+    if (del) r &= ~del[w];
+    if (w == nwords - 1) r &= tail_mask;
+    return r;
+  };
+  uint64_t wr[kSelRegs];
+  int64_t c = 0;
+  if (NB > 0 && cached) {
+    // every operand word of the wave's range in flight at once (NB x 8
+    // register pairs: sized to the operand count)
+    uint64_t q[kSelRegs][NB > 0 ? NB : 1];
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t w = a0 + r * 64 + lane;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) q[r][k] = w < a1 ? C.bms[k][w] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t w = a0 + r * 64 + lane;
+      uint64_t x = ~0ull;
+      for (int cj = 0; cj < C.nconj; ++cj) {
+        uint64_t o = 0;
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+          if (k >= C.conj_off[cj] && k < C.conj_off[cj + 1]) o |= q[r][k];
+        x &= o;
+      }
+      if (del && w < a1) x &= ~del[w];
+      if (w == nwords - 1) x &= tail_mask;
+      wr[r] = w < a1 ? x : 0ull;
+      c += __popcll(wr[r]);
+    }
+  } else if (cached) {
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t w = a0 + r * 64 + lane;
+      wr[r] = w < a1 ? word_at(w) : 0ull;
+      c += __popcll(wr[r]);
+    }
+  } else {
+    for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(word_at(w));
+  }
+  select_tail<G4, GT>(wr, c, cached, a0, a1, word_at, lane, wave, lb, epoch, row_offset, ids, total, G, stamps, dbg,
+                      nullptr, wcount, wpre, stage);
+}
+
+constexpr int kDefaultU = 2;
+// measured on MI355X (profiles/r01/sweep3.log, C3 100M rows): U=2 tiles in
+// flight per wave with non-temporal loads, 4 blocks per CU, write-through
+// partials -> 135 us = 5.9 TB/s; plain loads +3 %, 8 blocks/CU +7 %,
+// 2 blocks/CU +56 %, release-fence partials +22 %.
+constexpr bool kDefaultNT = true;
+
+// ColumnarFileScan's get_next_tid stream as BitSet + ascending positions +
+// COUNT (R/iterator/ColumnarFileScan.java:174-188) in ONE launch
+// (mbx_scan_select_async, knob scan_select_fused): each wave scans a
+// contiguous run of its block's full tiles with the fast scan's tile body
+// (hoisted literal terms; row-interleaved loads, so each row group's ballot
+// is one BitSet word) and collects its words lane = word (the 4 words of its
+// i-th tile go to lanes 4i..4i+3 of register i / 16), stores them as the
+// BitSet (coalesced, after its loads) with the block's segment count, then
+// select_tail turns them into positions: count published, offset from the
+// predecessors (chained look-back), leading steps staged before the offset
+// is known -- no second launch, no re-read of the BitSet.  Plans of 1..4
+// 4-byte int literal terms (no float compare: no NaN reach), wave ranges of
+// <= kSelRegs x 16 tiles (tables up to ~134 M rows), <= kLookbackBlocks blocks.
+template <int K, bool DEL, int U, int TQ>
+__global__ __launch_bounds__(kBlock) void k_scan_select(ScanLaunch L, int64_t* __restrict__ lb, int64_t row_offset,
+                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
+                                                        int64_t* __restrict__ stamps, int32_t dbg) {
+  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
+  __shared__ int64_t wcount[kWaves];
+  __shared__ int64_t wpre[kWaves];
+  __shared__ uint16_t stage[kWaves][32 * 64];
+  const KPlan* __restrict__ P = L.plan;
+  const int lane = threadIdx.x & 63;
+  const int wave = (int)uniform(threadIdx.x >> 6);
+  const uint32_t prev = (uint32_t)lb[0];
+  const int64_t epoch = prev >= 0x7fffffffu ? 1 : (int64_t)prev + 1;
+  const int64_t nrows = L.nrows;
+  const int64_t nwords = (nrows + 63) >> 6;
+  const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+  const int64_t tb0 = (int64_t)blockIdx.x * L.tiles_per_block;
+  const int64_t tb1 = min(tb0 + L.tiles_per_block, ntiles);
+  const int64_t per = (tb1 - tb0 + kWaves - 1) / kWaves;  // tiles per wave (<= 16 * kSelRegs, host-checked)
+  const int64_t wt0 = min(tb0 + wave * per, tb1);
+  const int64_t wt1 = min(wt0 + per, tb1);
+  const int64_t a0 = wt0 * kWordsPerTile;
+  const int64_t a1 = min(wt1 * kWordsPerTile, nwords);
+  const int64_t tfull = min(wt1, nrows / kTileRows);  // this wave's full tiles end here
+  const int nterms = P->nterms;
+  const uint32_t all = P->all_conj;
+  const int32_t* colp[K];
+#pragma unroll
+  for (int s = 0; s < K; ++s) colp[s] = (const int32_t*)P->cols[s].base;
+  const int32_t* const strp[1] = {nullptr};
+  KTerm th[TQ];
+#pragma unroll
+  for (int ti = 0; ti < TQ; ++ti)
+    if (ti < nterms) th[ti] = P->terms[ti];
+  Acc acc;
+  acc_init(acc);
+  uint64_t wave_count = 0;
+  uint64_t wr[kSelRegs];
+  int64_t c = 0;
+#pragma unroll
+  for (int r = 0; r < kSelRegs; ++r) {
+    uint64_t cur = 0;
+    const int64_t g0 = wt0 + (int64_t)r * 16;  // first tile of register group r
+    for (int i = 0; i < 16; i += U) {
+      const int64_t base = g0 + i;
+      if (base >= wt1) break;
+      TileRegs<K, 0> D[U];
+      load_tiles<K, 0, U, kDefaultNT, true>(D, base, 1, tfull, colp, strp, lane);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t t = base + u;
+        uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
+        if (t < tfull) {
+          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, true>(L, P, D[u], t, lane, nterms, all, 0, false, acc,
+                                                           wave_count, th, w);
+        } else if (t < wt1) {  // the table's one partial tile
+          TileRegs<K, 0> Dp;
+          load_partial<K, 0, true>(Dp, t, nrows, colp, strp, lane);
+          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, false>(L, P, Dp, t, lane, nterms, all, 0, false, acc,
+                                                            wave_count, th, w);
+        }
+        if ((lane >> 2) == i + u) {
+          const int j = lane & 3;
+          cur = j == 0 ? w[0] : (j == 1 ? w[1] : (j == 2 ? w[2] : w[3]));
+        }
+      }
+    }
+    const int64_t wd = a0 + (int64_t)r * 64 + lane;
+    wr[r] = wd < a1 ? cur : 0ull;
+    c += __popcll(wr[r]);
+    if (L.out_words && wd < a1) L.out_words[wd] = wr[r];  // the BitSet output, after the loads
+  }
+  auto word_at = [&](int64_t) -> uint64_t { return 0ull; };  // never called: every range is cached
+  const Gather4 G{};
+  select_tail<0, Gather4>(wr, c, true, a0, a1, word_at, lane, wave, lb, epoch, row_offset, ids, total, G, stamps,
+                          dbg, L.seg_counts, wcount, wpre, stage);
 }
 
 // Late materialisation (Heapfile.findRID + getRecord per output column,
@@ -1829,13 +1947,6 @@ hipError_t launch_read_probe(const ProbeArgs& A, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- launchers
-
-constexpr int kDefaultU = 2;
-// measured on MI355X (profiles/r01/sweep3.log, C3 100M rows): U=2 tiles in
-// flight per wave with non-temporal loads, 4 blocks per CU, write-through
-// partials -> 135 us = 5.9 TB/s; plain loads +3 %, 8 blocks/CU +7 %,
-// 2 blocks/CU +56 %, release-fence partials +22 %.
-constexpr bool kDefaultNT = true;
 
 int64_t choose_tiles_per_block(int64_t nrows) {
   const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
@@ -2067,6 +2178,38 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
     default: MBX_CNF_SELECT(0); break;
   }
 #undef MBX_CNF_SELECT
+  return hipGetLastError();
+}
+
+bool scan_select_fusable(int64_t nrows, int64_t tiles_per_block, int32_t fast_k, int32_t fast_ks, int32_t nterms,
+                         int32_t has_real) {
+  const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
+  const int64_t nb = ntiles == 0 ? 1 : (ntiles + tiles_per_block - 1) / tiles_per_block;
+  return fast_k >= 1 && fast_k <= 4 && fast_ks == 0 && !has_real && nterms >= 1 && nterms <= kHoistTerms &&
+         nrows > 0 && nb <= kLookbackBlocks && (tiles_per_block + kWaves - 1) / kWaves <= 16 * kSelRegs &&
+         nrows < (int64_t(1) << 32);
+}
+
+hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offset, int64_t* ids, int64_t* total,
+                              hipStream_t s, int64_t* stamps, int32_t dbg) {
+  const int64_t g = grid_blocks(L.nrows, L.tiles_per_block);
+  // the chained look-back (32-bit inclusive prefixes: tables < 2^32 rows)
+  dbg = (dbg & ~8) | (!(dbg & 8) ? 8 : 0);
+  const bool del = L.deleted != nullptr;
+#define MBX_SCAN_SELECT(KK, UU)                                                                                  \
+  if (del)                                                                                                      \
+    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms>), dim3((unsigned)g), dim3(kBlock), 0, s, L, lb, \
+                       row_offset, ids, total, stamps, dbg);                                                    \
+  else                                                                                                          \
+    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms>), dim3((unsigned)g), dim3(kBlock), 0, s, L, lb, \
+                       row_offset, ids, total, stamps, dbg)
+  switch (L.fast_k) {
+    case 1: MBX_SCAN_SELECT(1, 4); break;
+    case 2: MBX_SCAN_SELECT(2, 2); break;
+    case 3: MBX_SCAN_SELECT(3, 2); break;
+    default: MBX_SCAN_SELECT(4, 2); break;
+  }
+#undef MBX_SCAN_SELECT
   return hipGetLastError();
 }
 

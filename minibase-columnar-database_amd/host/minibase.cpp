@@ -589,7 +589,7 @@ CnfImage flatten(CondExpr* const* filter, int remap_from, int remap_to) {
 // selection on the GPU, hand them out row by row
 
 struct Batch {
-  static constexpr int64_t kRows = 8192;
+  static constexpr int64_t kRows = CursorBatches::kRows;
 };
 
 static void setup_jtuple(heap::Tuple& J, const std::vector<AttrType>& in1, const std::vector<short>& s_sizes,
@@ -648,7 +648,13 @@ void CursorBatches::reset(mbx_cursor* c, const std::vector<AttrType>& types, con
   sizes_ = sizes;
   cols_ = cols;
   batch_.assign(cols.size(), {});
-  for (size_t j = 0; j < cols.size(); j++) batch_[j].resize((size_t)(kRows * col_width(types, sizes, cols[j])));
+  kind_.assign(cols.size(), 0);
+  width_.assign(cols.size(), 0);
+  for (size_t j = 0; j < cols.size(); j++) {
+    kind_[j] = types[(size_t)cols[j]].attrType;
+    width_[j] = col_width(types, sizes, cols[j]);
+    batch_[j].resize((size_t)(kRows * width_[j]));
+  }
   ids_.assign((size_t)kRows, 0);
   n_ = i_ = 0;
 }
@@ -672,7 +678,28 @@ bool CursorBatches::next() {
   return true;
 }
 
-void CursorBatches::fill(heap::Tuple& J) const { fill_row(J, types_, sizes_, cols_, batch_, i_ - 1); }
+void CursorBatches::fill(heap::Tuple& J) const {
+  const int64_t i = i_ - 1;
+  for (size_t j = 0; j < cols_.size(); j++) {
+    const uint8_t* p = batch_[j].data() + i * width_[j];
+    switch (kind_[j]) {
+      case AttrType::attrInteger: {
+        int32_t v;
+        memcpy(&v, p, 4);
+        J.setIntFld((int)j + 1, v);
+        break;
+      }
+      case AttrType::attrReal: {
+        float v;
+        memcpy(&v, p, 4);
+        J.setFloFld((int)j + 1, v);
+        break;
+      }
+      default:
+        J.setStrFld((int)j + 1, std::string((const char*)p, strnlen((const char*)p, (size_t)width_[j])));
+    }
+  }
+}
 
 void CursorBatches::restart() {
   if (cur_) chk<FileScanException>(mbx_cursor_restart(cur_), "restart");

@@ -270,7 +270,9 @@ namespace iterator {
 // double-buffered delivery; fill() writes the current row into Jtuple.
 class CursorBatches {
  public:
-  static constexpr int64_t kRows = 8192;
+  // rows per batch: 64 Ki rows keep the per-batch copy calls (one per column
+  // + the positions) well below the per-row Jtuple fill (bench_delivery)
+  static constexpr int64_t kRows = 65536;
   CursorBatches() = default;
   ~CursorBatches() { close(); }
   CursorBatches(const CursorBatches&) = delete;
@@ -291,6 +293,8 @@ class CursorBatches {
   std::vector<AttrType> types_;
   std::vector<short> sizes_;
   std::vector<int32_t> cols_;
+  std::vector<int> kind_;    // per projected column: its AttrType code
+  std::vector<int64_t> width_;  // per projected column: bytes per row in the batch
   std::vector<std::vector<uint8_t>> batch_;
   std::vector<int64_t> ids_;
   int64_t n_ = 0, i_ = 0;

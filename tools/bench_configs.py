@@ -164,11 +164,23 @@ def main():
         def step(k=0):  # BitSet + positions + COUNT: mbx_scan_select_async (BitSet scan, then the compaction)
             M._chk(L.mbx_scan_select_async(ctx.h, plan.h, bm.h, ids.data_ptr(), cnt.data_ptr()))
 
-        ms = kernel_ms(step, args.steps, args.warmup)
         want = int((cols[0] < 104858).sum().item())
-        got = int(cnt.item())
-        assert got == want, (got, want)
-        assert bool((ids[:got] == torch.nonzero(cols[0] < 104858).flatten()).all())
+        wpos = torch.nonzero(cols[0] < 104858).flatten()
+        # both forms, interleaved: the BitSet scan + compaction (two launches)
+        # and k_scan_select (one launch, knob scan_select_fused)
+        forms = {}
+        for rep in range(3):
+            for fused in (0, 1):
+                ctx.set_tuning("scan_select_fused", fused)
+                ids.zero_()
+                torch.cuda.synchronize()
+                forms.setdefault(fused, []).append(kernel_ms(step, args.steps, args.warmup))
+                got = int(cnt.item())
+                assert got == want, (fused, got, want)
+                assert bool((ids[:got] == wpos).all()), fused
+        fused_default = int(os.environ.get("MBX_SCAN_SELECT_FUSED", "0") or 0)
+        ctx.set_tuning("scan_select_fused", fused_default)
+        ms = min(forms[fused_default])
         # the same queries replayed from a HIP graph of 10 (mbx_graph_*: no host launches between them)
         ctx.sync()
         ctx.graph_begin()
@@ -181,6 +193,8 @@ def main():
         scan_ms = kernel_ms(lambda: ctx.scan_bitmap_async(plan, bm), args.steps, args.warmup)
         byts = n * 4 + n / 8 + got * 8
         emit({"config": "C2", "rows": n, "gpus": 1, "selected": got, "ms_per_query": ms, "rows_per_s": n / ms * 1e3,
+              "form": "one launch (k_scan_select)" if fused_default else "two launches (BitSet scan + k_select_ids)",
+              "ms_per_query_two_launch": forms[0], "ms_per_query_one_launch": forms[1],
               "graph_replay_ms_per_query": graph_ms,
               "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
               "scan_gbs": (n * 4 + n / 8) / scan_ms / 1e6})
