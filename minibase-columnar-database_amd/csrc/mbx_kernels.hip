@@ -343,6 +343,15 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
   }
   if (lane == 0) sh[wave] = a;
   __syncthreads();
+  if (!FULL && L.fin_mode == kFinSegOnly) {
+    if (threadIdx.x == 0 && L.seg_counts) {
+      int64_t cnt = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) cnt += sh[w].count;
+      __hip_atomic_store(L.seg_counts + blockIdx.x, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   if (!FULL && L.ticket && L.fin_mode == kFinPackedCount) {
     if (threadIdx.x == 0) {
       Acc r = sh[0];
@@ -448,24 +457,45 @@ struct StepScan {
 
 // sbase / pbase: stage from st[sbase] on, offsets + pbase; nothing is staged
 // unless the step's positions fit below kStageIds
+// Wave-wide inclusive prefix sum / max on the DPP paths (VALU only, no LDS
+// permute traffic): row_shr 1, 2, 4, 8 inside each 16-lane row, then
+// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry the rows'
+// totals upwards.  Lanes a DPP step does not write keep `old` = 0.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWS, 0xf, true);
+}
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += dpp0<0x111>(x);
+  x += dpp0<0x112>(x);
+  x += dpp0<0x114>(x);
+  x += dpp0<0x118>(x);
+  x += dpp0<0x142, 0xa>(x);
+  x += dpp0<0x143, 0xc>(x);
+  return x;
+}
+// lane 63 holds the maximum of every lane's (unsigned) value
+__device__ __forceinline__ uint32_t wave_max_to_63(uint32_t x) {
+  x = max(x, dpp0<0x111>(x));
+  x = max(x, dpp0<0x112>(x));
+  x = max(x, dpp0<0x114>(x));
+  x = max(x, dpp0<0x118>(x));
+  x = max(x, dpp0<0x142, 0xa>(x));
+  x = max(x, dpp0<0x143, 0xc>(x));
+  return x;
+}
+
 __device__ __forceinline__ StepScan stage_step(uint64_t mw, uint16_t* st, int lane, uint32_t sbase = 0,
                                                uint32_t pbase = 0) {
   const uint32_t pc = (uint32_t)__popcll(mw);
-  uint32_t incl = pc;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d);
-    if (lane >= d) incl += y;
-  }
+  const uint32_t incl = wave_incl_sum(pc);
   StepScan r;
   r.excl = incl - pc;
   r.total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (r.total == 0 || sbase + r.total > kStageIds) return r;
   st += sbase;
   uint64_t nz = __ballot(mw != 0ull);
-  uint32_t maxpc = pc;
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) maxpc = max(maxpc, (uint32_t)__shfl_xor(maxpc, m));
+  const uint32_t maxpc = (uint32_t)__builtin_amdgcn_readlane((int)wave_max_to_63(pc), 63);
   if (maxpc <= (uint32_t)__popcll(nz)) {
     uint64_t m = mw;
     uint32_t o = r.excl;
@@ -1386,30 +1416,91 @@ __device__ __forceinline__ uint64_t cnf_word(const BitmapCnf& C, int64_t w) {
 // values written.  wr / cached: the wave's words (lane = word) when its range
 // fits kSelRegs x 64 words; word_at(w) re-forms word w otherwise.  segc (may
 // be null): the block's count is also stored there.
-template <int G4, class GT, class WordAt>
+// The chained look-back of one block (wave 0): the sum of every
+// predecessor's count.  Each round reads the count and inclusive-prefix
+// flags of the 64 predecessors below e (lane l: e - 64 + l, one line group
+// of each, all loads in flight together); the nearest published inclusive
+// prefix ends the walk, otherwise the window's counts are added once all are
+// published and the walk moves 64 further down.  The cost is the flag lines'
+// request queue, not the number of rounds: 4 predecessors per lane (4x the
+// requests, a quarter of the rounds) measured slower -- C2 one launch 22.5
+// vs 18.6 us, C4 51-52 vs 45 us (profiles/r03/lb).
+__device__ __forceinline__ int64_t lookback_window(int64_t* __restrict__ lb, int64_t* __restrict__ inc, int64_t e,
+                                                   int64_t epoch, int lane, int64_t& in) {
+  const int64_t j = e - 64 + lane;
+  in = j >= 0 ? __hip_atomic_load(&inc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  return j >= 0 ? __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (epoch << 32);
+}
+
+// in0 / a0: the first window's flags (below blockIdx.x), loaded by the caller
+__device__ __forceinline__ int64_t chained_lookback(int64_t* __restrict__ lb, int64_t* __restrict__ inc,
+                                                    int64_t epoch, int lane, int64_t in0, int64_t a0) {
+  constexpr int64_t kLow = 0xffffffffll;
+  int64_t pre = 0;
+  int64_t e = blockIdx.x;
+  bool first = true;
+  while (e > 0) {
+    const int64_t j = e - 64 + lane;
+    const bool live = j >= 0;
+    int64_t in = in0, a = a0;
+    if (!first) a = lookback_window(lb, inc, e, epoch, lane, in);
+    first = false;
+    for (;;) {
+      const bool ok_in = live && (in >> 32) == epoch;
+      const bool ok_a = (a >> 32) == epoch;
+      const uint64_t im = __ballot(ok_in);
+      if (im) {
+        const int L = 63 - __clzll((long long)im);
+        if (!__any(lane > L && !ok_a)) {
+          pre += lane == L ? (in & kLow) : (lane > L ? (a & kLow) : 0);
+          e = 0;
+          break;
+        }
+      } else if (!__any(!ok_a)) {
+        pre += a & kLow;
+        e -= 64;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (live && !ok_in) in = __hip_atomic_load(&inc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!ok_a) a = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  return pre;
+}
+
+template <int G4, class GT, class WordAt, int NW = kWaves>
 __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int64_t c, bool cached, int64_t a0,
                                             int64_t a1, WordAt word_at, int lane, int wave, int64_t* __restrict__ lb,
                                             int64_t epoch, int64_t row_offset, int64_t* __restrict__ ids,
                                             int64_t* __restrict__ total, const GT& G, int64_t* __restrict__ stamps,
-                                            int32_t dbg, int64_t* __restrict__ segc, int64_t* wcount, int64_t* wpre,
-                                            uint16_t (*stage)[32 * 64]) {
+                                            int32_t dbg, int64_t* __restrict__ segc, int64_t nseg, int64_t* wcount,
+                                            int64_t* wpre, uint16_t (*stage)[32 * 64],
+                                            uint64_t* __restrict__ words_out = nullptr) {
   int64_t* const inc = lb + 1 + kLookbackBlocks;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
+  // wave 0 loads the look-back's first window (the 64 predecessors) BEFORE
+  // this block stores its own flag: vmcnt counts loads and stores in issue
+  // order, so a wait for a poll issued after the flag store also waits for
+  // that store's write-through round trip (and for any BitSet word stores
+  // before it -- k_scan_select stores its words at the end, words_out)
+  int64_t in0 = 0, a0f = epoch << 32;
+  if ((dbg & 8) && wave == 0 && blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
   if (lane == 0) wcount[wave] = c;
   __syncthreads();
   int64_t bc = 0;
-  for (int k = 0; k < kWaves; ++k) bc += wcount[k];
+  for (int k = 0; k < NW; ++k) bc += wcount[k];
   if (threadIdx.x == 0) {
     __hip_atomic_store(&lb[1 + blockIdx.x], (epoch << 32) | bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (segc) segc[blockIdx.x] = bc;  // the block's segment count of the BitSet it formed (k_scan_select)
     if (stamps) stamps[4 * blockIdx.x + 1] = wall_clock64();
   }
   // look-back: the predecessors' counts, all polls of a thread in flight together
-  int64_t v[kLookbackBlocks / kBlock];
+  constexpr int kThreads = 64 * NW;
+  int64_t v[kLookbackBlocks / kThreads];
 #pragma unroll
-  for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
-    const int64_t j = (int64_t)k * kBlock + threadIdx.x;
+  for (int k = 0; k < kLookbackBlocks / kThreads; ++k) {
+    const int64_t j = (int64_t)k * kThreads + threadIdx.x;
     if ((dbg & 8) || j >= (int64_t)blockIdx.x)
       v[k] = epoch << 32;
     else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
@@ -1448,42 +1539,14 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
   }
   int64_t pre = 0;
   if (dbg & 8) {
-    // chained form: wave 0 reads 64 predecessors per round (one line group),
+    // chained form: wave 0 walks back over its predecessors, 64 per round,
     // stops at the nearest one whose inclusive prefix is published and adds
     // the counts after it; other waves contribute 0
-    if (wave == 0) {
-      int64_t e = blockIdx.x;
-      while (e > 0) {
-        const int64_t j = e - 64 + lane;
-        const bool live = j >= 0;
-        int64_t in = live ? __hip_atomic_load(&inc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        int64_t a = live ? __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (epoch << 32);
-        for (;;) {
-          const bool ok_in = live && (in >> 32) == epoch;
-          const bool ok_a = (a >> 32) == epoch;
-          const uint64_t im = __ballot(ok_in);
-          if (im) {
-            const int L = 63 - __clzll((long long)im);
-            if (!__any(lane > L && !ok_a)) {
-              pre += lane == L ? (in & 0xffffffffll) : (lane > L ? (a & 0xffffffffll) : 0);
-              e = 0;
-              break;
-            }
-          } else if (!__any(!ok_a)) {
-            pre += a & 0xffffffffll;
-            e -= 64;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          if (live && !ok_in) in = __hip_atomic_load(&inc[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (!ok_a) a = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
+    if (wave == 0) pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
   } else {
 #pragma unroll
-  for (int k = 0; k < kLookbackBlocks / kBlock; ++k) {
-    const int64_t j = (int64_t)k * kBlock + threadIdx.x;
+  for (int k = 0; k < kLookbackBlocks / kThreads; ++k) {
+    const int64_t j = (int64_t)k * kThreads + threadIdx.x;
     while (!(dbg & 2) && (v[k] >> 32) != epoch) {
       if (dbg & 1)
         __builtin_amdgcn_s_sleep(16);
@@ -1500,7 +1563,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
   __syncthreads();
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
-  for (int k = 0; k < kWaves; ++k) off += wpre[k];
+  for (int k = 0; k < NW; ++k) off += wpre[k];
   if ((dbg & 8) && threadIdx.x == 0)
     __hip_atomic_store(&inc[blockIdx.x], (epoch << 32) | (off + bc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x == gridDim.x - 1) {
@@ -1510,7 +1573,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
     }
     // the flags of blocks this launch does not have carry its epoch too, so a
     // later, larger launch never finds a flag older than the previous launch
-    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += kBlock) {
+    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += kThreads) {
       lb[1 + j] = epoch << 32;
       if (dbg & 8) inc[j] = epoch << 32;
     }
@@ -1545,6 +1608,22 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
   } else {
     for (int64_t base = a0; base < a1; base += 64)
       emit_step<G4, GT>(base, base + lane < a1 ? word_at(base + lane) : 0ull, off, row_offset, ids, st, lane, G);
+  }
+  // the BitSet (k_scan_select): its words and one segment count per 4 waves
+  if (words_out) {
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t wd = a0 + r * 64 + lane;
+      if (wd < a1) words_out[wd] = wr[r];
+    }
+  }
+  if (segc && threadIdx.x < NW / kWaves) {
+    const int64_t sg = (int64_t)blockIdx.x * (NW / kWaves) + threadIdx.x;
+    if (sg < nseg) {
+      int64_t sc = 0;
+      for (int k = 0; k < kWaves; ++k) sc += wcount[threadIdx.x * kWaves + k];
+      segc[sg] = sc;
+    }
   }
   if (stamps) {
     __syncthreads();
@@ -1627,7 +1706,7 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
     for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(word_at(w));
   }
   select_tail<G4, GT>(wr, c, cached, a0, a1, word_at, lane, wave, lb, epoch, row_offset, ids, total, G, stamps, dbg,
-                      nullptr, wcount, wpre, stage);
+                      nullptr, 0, wcount, wpre, stage);
 }
 
 constexpr int kDefaultU = 2;
@@ -1650,14 +1729,14 @@ constexpr bool kDefaultNT = true;
 // is known -- no second launch, no re-read of the BitSet.  Plans of 1..4
 // 4-byte int literal terms (no float compare: no NaN reach), wave ranges of
 // <= kSelRegs x 16 tiles (tables up to ~134 M rows), <= kLookbackBlocks blocks.
-template <int K, bool DEL, int U, int TQ>
-__global__ __launch_bounds__(kBlock) void k_scan_select(ScanLaunch L, int64_t* __restrict__ lb, int64_t row_offset,
-                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                        int64_t* __restrict__ stamps, int32_t dbg) {
+template <int K, bool DEL, int U, int TQ, int NW>
+__global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* __restrict__ lb, int64_t row_offset,
+                                                         int64_t* __restrict__ ids, int64_t* __restrict__ total,
+                                                         int64_t* __restrict__ stamps, int32_t dbg) {
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
-  __shared__ int64_t wcount[kWaves];
-  __shared__ int64_t wpre[kWaves];
-  __shared__ uint16_t stage[kWaves][32 * 64];
+  __shared__ int64_t wcount[NW];
+  __shared__ int64_t wpre[NW];
+  __shared__ uint16_t stage[NW][32 * 64];
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
@@ -1666,10 +1745,13 @@ __global__ __launch_bounds__(kBlock) void k_scan_select(ScanLaunch L, int64_t* _
   const int64_t nrows = L.nrows;
   const int64_t nwords = (nrows + 63) >> 6;
   const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
-  const int64_t tb0 = (int64_t)blockIdx.x * L.tiles_per_block;
+  // NW / 4 BitSet segments per block, 4 waves per segment: wave w scans
+  // its quarter of segment blockIdx * NW / 4 + w / 4
+  const int64_t nseg = (ntiles + L.tiles_per_block - 1) / L.tiles_per_block;
+  const int64_t tb0 = min(((int64_t)blockIdx.x * (NW / kWaves) + wave / kWaves) * L.tiles_per_block, ntiles);
   const int64_t tb1 = min(tb0 + L.tiles_per_block, ntiles);
   const int64_t per = (tb1 - tb0 + kWaves - 1) / kWaves;  // tiles per wave (<= 16 * kSelRegs, host-checked)
-  const int64_t wt0 = min(tb0 + wave * per, tb1);
+  const int64_t wt0 = min(tb0 + (wave % kWaves) * per, tb1);
   const int64_t wt1 = min(wt0 + per, tb1);
   const int64_t a0 = wt0 * kWordsPerTile;
   const int64_t a1 = min(wt1 * kWordsPerTile, nwords);
@@ -1720,12 +1802,12 @@ __global__ __launch_bounds__(kBlock) void k_scan_select(ScanLaunch L, int64_t* _
     const int64_t wd = a0 + (int64_t)r * 64 + lane;
     wr[r] = wd < a1 ? cur : 0ull;
     c += __popcll(wr[r]);
-    if (L.out_words && wd < a1) L.out_words[wd] = wr[r];  // the BitSet output, after the loads
   }
   auto word_at = [&](int64_t) -> uint64_t { return 0ull; };  // never called: every range is cached
   const Gather4 G{};
-  select_tail<0, Gather4>(wr, c, true, a0, a1, word_at, lane, wave, lb, epoch, row_offset, ids, total, G, stamps,
-                          dbg, L.seg_counts, wcount, wpre, stage);
+  select_tail<0, Gather4, decltype(word_at), NW>(wr, c, true, a0, a1, word_at, lane, wave, lb, epoch, row_offset, ids,
+                                                 total, G, stamps, dbg, L.seg_counts, nseg, wcount, wpre, stage,
+                                                 L.out_words);
 }
 
 // Late materialisation (Heapfile.findRID + getRecord per output column,
@@ -2191,18 +2273,31 @@ bool scan_select_fusable(int64_t nrows, int64_t tiles_per_block, int32_t fast_k,
 }
 
 hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offset, int64_t* ids, int64_t* total,
-                              hipStream_t s, int64_t* stamps, int32_t dbg) {
-  const int64_t g = grid_blocks(L.nrows, L.tiles_per_block);
+                              hipStream_t s, int64_t* stamps, int32_t dbg, int32_t waves) {
+  // waves per block: 4 (one BitSet segment per block) or 16 (four): a
+  // quarter of the blocks publish and walk back
+  const int nw = waves == 16 ? 16 : kWaves;
+  const int64_t nseg = grid_blocks(L.nrows, L.tiles_per_block);
+  const int64_t g = (nseg + nw / kWaves - 1) / (nw / kWaves);
   // the chained look-back (32-bit inclusive prefixes: tables < 2^32 rows)
   dbg = (dbg & ~8) | (!(dbg & 8) ? 8 : 0);
   const bool del = L.deleted != nullptr;
-#define MBX_SCAN_SELECT(KK, UU)                                                                                  \
+#define MBX_SCAN_SELECT_NW(KK, UU, NW)                                                                            \
   if (del)                                                                                                      \
-    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms>), dim3((unsigned)g), dim3(kBlock), 0, s, L, lb, \
-                       row_offset, ids, total, stamps, dbg);                                                    \
+    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW>), dim3((unsigned)g), dim3(64 * NW), 0, s, L, \
+                       lb, row_offset, ids, total, stamps, dbg);                                                \
   else                                                                                                          \
-    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms>), dim3((unsigned)g), dim3(kBlock), 0, s, L, lb, \
-                       row_offset, ids, total, stamps, dbg)
+    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW>), dim3((unsigned)g), dim3(64 * NW), 0, s, L, \
+                       lb, row_offset, ids, total, stamps, dbg)
+#define MBX_SCAN_SELECT(KK, UU)          \
+  if (nw == 16) {                        \
+    MBX_SCAN_SELECT_NW(KK, UU, 16);      \
+  } else {                               \
+    MBX_SCAN_SELECT_NW(KK, UU, kWaves);  \
+  }
+  // tiles in flight per wave as in the fast scan; one column at U = 8 (a C2
+  // wave waits on two load batches instead of three) measured slower: the
+  // scan part of C2 ends at 10.4 instead of 9.2 us (profiles/r03/lb)
   switch (L.fast_k) {
     case 1: MBX_SCAN_SELECT(1, 4); break;
     case 2: MBX_SCAN_SELECT(2, 2); break;
@@ -2210,6 +2305,7 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
     default: MBX_SCAN_SELECT(4, 2); break;
   }
 #undef MBX_SCAN_SELECT
+#undef MBX_SCAN_SELECT_NW
   return hipGetLastError();
 }
 

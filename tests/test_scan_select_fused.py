@@ -134,6 +134,28 @@ def test_fused_segment_sizes_and_fallback(ctx, tune, tpb):
     assert np.array_equal(ctx.select(bm), ids)
 
 
+@pytest.mark.parametrize("waves", [4, 16])
+@pytest.mark.parametrize("n", [255, 70001, 3_000_017, 10_000_000])
+def test_fused_waves_per_block(ctx, tune, waves, n):
+    """one BitSet segment per 4-wave block, or four per 16-wave block (a
+    quarter of the blocks in the look-back): the same positions, words and
+    segment counts"""
+    tune("scan_select_waves", waves)
+    cols = int_cols(n, ncols=2, hi=1000, seed=n + waves)
+    dele = helpers.random_deleted(n, 0.03, seed=n) if n == 70001 else None
+    ot = oracle.Table(cols, dele)
+    t = ctx.stage(cols, dele, row_offset=64)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", 250))], [(oracle.GE, ("sym", 2), ("int", 100))]]
+    n_o, w_o, ids_o = oracle.filescan(ot, cnf)
+    plan = ctx.compile(t, cnf)
+    for _ in range(2):
+        bm, ids, k = run_async(ctx, plan, n)
+        assert k == n_o and np.array_equal(ids, ids_o + 64)
+        assert np.array_equal(bm.download(), w_o)
+        assert np.array_equal(ctx.select(bm, row_offset=64), ids_o + 64)
+        assert bm.count == n_o
+
+
 def test_fused_interleaved_with_cnf_select(ctx):
     """k_scan_select and k_cnf_select share the context's look-back words:
     alternating launches of different grid sizes stay exact"""
