@@ -216,8 +216,19 @@ def test_synthetic_cnf_large_wide_projection(ctx):
 
 # ------------------------------------------------- double-buffered cursor
 
+@pytest.mark.parametrize("prefetch", [1, 0])
 @pytest.mark.parametrize("sizes", [[1], [7], [64], [8192], [3, 100, 3, 100, 5000], [1000, 1, 1, 2000]])
-def test_cursor_batches_equal_one_materialise(ctx, sizes):
+def test_cursor_batches_equal_one_materialise(ctx, sizes, prefetch):
+    """double-buffered (prefetch 1) and on-demand (0) delivery: batches of any
+    size concatenate to the one-batch read, across a restart"""
+    ctx.set_tuning("cursor_prefetch", prefetch)
+    try:
+        _batches_equal_one_read(ctx, sizes)
+    finally:
+        ctx.set_tuning("cursor_prefetch", 1)
+
+
+def _batches_equal_one_read(ctx, sizes):
     n = 100_003
     cols = synth(n, seed=11)
     t = ctx.stage(cols)
