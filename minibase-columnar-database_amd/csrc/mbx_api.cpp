@@ -90,8 +90,9 @@ static void tuning_from_env(MbxTuning& t) {
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
   t.cursor_prefetch = (int32_t)env_knob("MBX_CURSOR_PREFETCH", 1);
-  t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 0);
+  t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 1);
   t.scan_select_waves = (int32_t)env_knob("MBX_SCAN_SELECT_WAVES", 16);
+  t.scan_words_wt = (int32_t)env_knob("MBX_SCAN_WORDS_WT", 1);
   t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
   if (t.select_blocks < 1) t.select_blocks = 1024;  // as mbx_set_tuning: never a zero / negative grid divisor
 }
@@ -288,6 +289,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "cursor_prefetch")) t.cursor_prefetch = v;
   else if (!strcmp(knob, "scan_select_fused")) t.scan_select_fused = v;
   else if (!strcmp(knob, "scan_select_waves")) t.scan_select_waves = v == 4 ? 4 : 16;
+  else if (!strcmp(knob, "scan_words_wt")) t.scan_words_wt = v != 0;
   else return fail(MBX_E_INVALID, "mbx_set_tuning: unknown knob `%s`", knob);
   return MBX_OK;
 }
@@ -896,6 +898,8 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.sink_lds = sink_fits && (tu.sink_lds == 2 || (tu.sink_lds == 1 && tpb >= 128));
   L.ticket_groups = ticket_groups_of(c);
   L.seg_counts = seg_counts;
+  L.words_wt = tu.scan_words_wt;
+  L.pad_wt_ = 0;
   L.fin_mode = tu.fin_mode >= 0 ? tu.fin_mode : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
   if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))
     L.fin_mode = kFinWriteThrough;
@@ -1433,7 +1437,8 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
     if (sel->nseg <= kMaxStampBlocks) stamps = c->stamps;
   }
   HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segc, row_offset, dev_ids, pc, dev_out, nproj,
-                            dev_total, c->stream, c->tune.select_dbg & 3, stamps, c->tune.gather_fused != 0,
+                            dev_total, c->stream, (c->tune.select_dbg & 3) | ((c->tune.select_dbg >> 4) & 32), stamps,
+                            c->tune.gather_fused != 0,
                             c->tune.select_blocks));
   return MBX_OK;
 }

@@ -129,6 +129,8 @@ struct ScanLaunch {
   int32_t sink_lds;           // 1: BitSet words of the block's full tiles staged in dynamic LDS
                               //    (tiles_per_block x 32 B) and stored in one burst at the block's end
   int64_t* seg_counts;        // BitSet scans: the output bitmap's per-segment counts (one per block)
+  int32_t words_wt;           // BitSet words stored write-through (sc1) instead of plain
+  int32_t pad_wt_;
 };
 
 // dynamic LDS per block for the staged BitSet (4 blocks per CU: <= 128 KB of

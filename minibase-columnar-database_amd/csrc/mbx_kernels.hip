@@ -541,6 +541,22 @@ struct GatherW {
   int32_t n;
 };
 
+// An output store of the compaction: plain, or write-through (`sc1`: the
+// line leaves the XCD's L2 with the store instead of staying dirty there
+// for the end-of-kernel write-back).  Write-through is the default for
+// positions-only compactions (G4 == 0): C2 k_select_ids 7.5 -> 7.0 us, C2
+// query 16.7 -> 15.6 us (one launch 16.3 -> 15.2); with gathered values
+// (C4) it is neutral for the projection and +1.2 us with positions, so
+// those stay plain.  Kernel dbg bit 5 (select_dbg 512) flips the choice
+// (profiles/r03/lb/wt_*).
+template <class T>
+__device__ __forceinline__ void put(T* p, T v, bool wt) {
+  if (wt)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
 __device__ __forceinline__ void wide_row(const GatherW& G, int64_t p, int64_t o) {
   for (int g = 0; g < G.n; ++g) {
     const int sw = G.sw[g];
@@ -565,7 +581,7 @@ __device__ __forceinline__ void wide_row(const GatherW& G, int64_t p, int64_t o)
 template <int G4, class GT = Gather4>
 __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const StepScan& r, int64_t& off,
                                            int64_t row_offset, int64_t* __restrict__ ids, const uint16_t* st,
-                                           int lane, const GT& G, uint32_t first = 0) {
+                                           int lane, const GT& G, uint32_t first = 0, bool wt = false) {
   if (r.total == 0) return;
   const int64_t lbase = base * 64;  // table-local row of bit 0 of word `base`
   if (r.total <= kStageIds) {
@@ -591,14 +607,14 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
             v1[g] = (uint32_t)G.col[g][p1];
           }
         if (ids) {
-          ids[off + i0] = row_offset + p0;
-          if (two) ids[off + i1] = row_offset + p1;
+          put(&ids[off + i0], row_offset + p0, wt);
+          if (two) put(&ids[off + i1], row_offset + p1, wt);
         }
 #pragma unroll
         for (int g = 0; g < G4; ++g)
           if (g < G.n) {
-            G.out[g][off + i0] = v0[g];
-            if (two) G.out[g][off + i1] = v1[g];
+            put(&G.out[g][off + i0], v0[g], wt);
+            if (two) put(&G.out[g][off + i1], v1[g], wt);
           }
       }
     }
@@ -614,13 +630,13 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
         const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         const int64_t p = lbase + j * 64 + lane;
         const int64_t o = off + slot + below;
-        if (ids) ids[o] = row_offset + p;
+        if (ids) put(&ids[o], row_offset + p, wt);
         if constexpr (G4 == kWide) {
           wide_row(G, p, o);
         } else {
 #pragma unroll
           for (int g = 0; g < G4; ++g)
-            if (g < G.n) G.out[g][o] = (uint32_t)G.col[g][p];
+            if (g < G.n) put(&G.out[g][o], (uint32_t)G.col[g][p], wt);
         }
       }
     }
@@ -630,9 +646,10 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
 
 template <int G4 = 0, class GT = Gather4>
 __device__ __forceinline__ void emit_step(int64_t base, uint64_t mw, int64_t& off, int64_t row_offset,
-                                          int64_t* __restrict__ ids, uint16_t* st, int lane, const GT& G) {
+                                          int64_t* __restrict__ ids, uint16_t* st, int lane, const GT& G,
+                                          bool wt = false) {
   const StepScan r = stage_step(mw, st, lane);
-  store_step<G4, GT>(base, mw, r, off, row_offset, ids, st, lane, G);
+  store_step<G4, GT>(base, mw, r, off, row_offset, ids, st, lane, G, 0, wt);
 }
 
 // ------------------------------------------------------------- fast scan
@@ -1001,7 +1018,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
         if (L.sink_lds)
           sink_stage[(t - t0) * kWordsPerTile + (lane & 3)] = sink;
         else
-          L.out_words[t * kWordsPerTile + (lane & 3)] = sink;
+          put(&L.out_words[t * kWordsPerTile + (lane & 3)], sink, L.words_wt != 0);
       }
       sink_t += 16 * ustep;
       sink_n = 0;
@@ -1043,7 +1060,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
       __syncthreads();
       const int64_t nw = (tf > t0 ? tf - t0 : 0) * kWordsPerTile;
       uint64_t* dst = L.out_words + t0 * kWordsPerTile;
-      for (int64_t i = threadIdx.x; i < nw; i += kBlock) dst[i] = sink_stage[i];
+      for (int64_t i = threadIdx.x; i < nw; i += kBlock) put(&dst[i], sink_stage[i], L.words_wt != 0);
     }
   }
   const int64_t tp = nrows / kTileRows;  // the partial tile, owned like any other tile of [t0, t1)
@@ -1355,7 +1372,10 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
   }
   for (int k = 0; k < wave; ++k) off += wcount[k];
   // one step = 64 consecutive words, lane = word
-  auto step = [&](int64_t base, uint64_t mw) { emit_step<G4>(base, mw, off, row_offset, ids, stage[wave], lane, G); };
+  const bool wt = (G4 == 0) != ((dbg & 32) != 0);
+  auto step = [&](int64_t base, uint64_t mw) {
+    emit_step<G4>(base, mw, off, row_offset, ids, stage[wave], lane, G, wt);
+  };
   if (dbg & 2) {
   } else if (cached) {
 #pragma unroll
@@ -1491,7 +1511,10 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
   __syncthreads();
   int64_t bc = 0;
   for (int k = 0; k < NW; ++k) bc += wcount[k];
-  if (threadIdx.x == 0) {
+  // the count is published by wave 1, not by the polling wave 0: each wave
+  // has its own vmcnt, and a wave's wait for a poll also waits for every
+  // store it issued before (the flag's write-through round trip)
+  if (threadIdx.x == 64) {
     __hip_atomic_store(&lb[1 + blockIdx.x], (epoch << 32) | bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (stamps) stamps[4 * blockIdx.x + 1] = wall_clock64();
   }
@@ -1579,6 +1602,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
     }
   }
   for (int k = 0; k < wave; ++k) off += wcount[k];
+  const bool wt = (G4 == 0) != ((dbg & 32) != 0);
   if (cached) {
     // the prefetched rows, then the rest of the staged ones, then the steps
     // that did not fit the stage one by one
@@ -1586,35 +1610,36 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
     for (int k = 0; k < kPrefetch; ++k) {
       const uint32_t i = (uint32_t)lane + 64u * k;
       if (i < tot) {
-        if (ids) ids[off + i] = row_offset + a0 * 64 + st[i];
+        if (ids) put(&ids[off + i], row_offset + a0 * 64 + st[i], wt);
         if constexpr (G4 == kWide) {
           wide_row(G, a0 * 64 + st[i], off + i);
         } else {
 #pragma unroll
           for (int g = 0; g < G4; ++g)
-            if (g < G.n) G.out[g][off + i] = pv[k][g];
+            if (g < G.n) put(&G.out[g][off + i], pv[k][g], wt);
         }
       }
     }
     const StepScan all{0u, tot};
-    store_step<G4, GT>(a0, 0ull, all, off, row_offset, ids, st, lane, G, 64u * kPrefetch);
+    store_step<G4, GT>(a0, 0ull, all, off, row_offset, ids, st, lane, G, 64u * kPrefetch, wt);
 #pragma unroll
     for (int r = 0; r < kSelRegs; ++r) {
       const int64_t base = a0 + r * 64;
       if (r < nst) continue;
       if (base >= a1) break;
-      emit_step<G4, GT>(base, wr[r], off, row_offset, ids, st, lane, G);
+      emit_step<G4, GT>(base, wr[r], off, row_offset, ids, st, lane, G, wt);
     }
   } else {
     for (int64_t base = a0; base < a1; base += 64)
-      emit_step<G4, GT>(base, base + lane < a1 ? word_at(base + lane) : 0ull, off, row_offset, ids, st, lane, G);
+      emit_step<G4, GT>(base, base + lane < a1 ? word_at(base + lane) : 0ull, off, row_offset, ids, st, lane, G,
+                        wt);
   }
   // the BitSet (k_scan_select): its words and one segment count per 4 waves
   if (words_out) {
 #pragma unroll
     for (int r = 0; r < kSelRegs; ++r) {
       const int64_t wd = a0 + r * 64 + lane;
-      if (wd < a1) words_out[wd] = wr[r];
+      if (wd < a1) put(&words_out[wd], wr[r], wt);
     }
   }
   if (segc && threadIdx.x < NW / kWaves) {
@@ -1771,6 +1796,45 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
   uint64_t wave_count = 0;
   uint64_t wr[kSelRegs];
   int64_t c = 0;
+  if (!(dbg & 64)) {
+    // the segment's 4 waves read its tiles interleaved (wave w % 4 takes
+    // tiles w % 4, + 4, + 8, ... as the fast scan does: at any moment the
+    // waves of a segment stream adjacent tiles), the words go to LDS (the
+    // stage, not yet in use) and each wave then takes its contiguous quarter
+    // of them into registers -- the positions stay ascending by wave
+    uint64_t* const segw =
+        reinterpret_cast<uint64_t*>(&stage[0][0]) + (int64_t)(wave / kWaves) * L.tiles_per_block * kWordsPerTile;
+    const int sub = wave % kWaves;
+    const int64_t tf = min(tb1, nrows / kTileRows);  // the segment's full tiles end here
+    for (int64_t base = tb0 + sub; base < tb1; base += (int64_t)kWaves * U) {
+      TileRegs<K, 0> D[U];
+      load_tiles<K, 0, U, kDefaultNT, true>(D, base, kWaves, tf, colp, strp, lane);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t t = base + (int64_t)u * kWaves;
+        uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
+        if (t < tf) {
+          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, true>(L, P, D[u], t, lane, nterms, all, 0, false, acc,
+                                                           wave_count, th, w);
+        } else if (t < tb1) {  // the table's one partial tile
+          TileRegs<K, 0> Dp;
+          load_partial<K, 0, true>(Dp, t, nrows, colp, strp, lane);
+          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, false>(L, P, Dp, t, lane, nterms, all, 0, false, acc,
+                                                            wave_count, th, w);
+        }
+        if (t < tb1 && lane < 4)
+          segw[(t - tb0) * kWordsPerTile + lane] = lane == 0 ? w[0] : (lane == 1 ? w[1] : (lane == 2 ? w[2] : w[3]));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSelRegs; ++r) {
+      const int64_t wd = a0 + (int64_t)r * 64 + lane;
+      wr[r] = wd < a1 ? segw[wd - tb0 * kWordsPerTile] : 0ull;
+      c += __popcll(wr[r]);
+    }
+    __syncthreads();  // select_tail stages positions over the same LDS
+  } else {
 #pragma unroll
   for (int r = 0; r < kSelRegs; ++r) {
     uint64_t cur = 0;
@@ -1802,6 +1866,7 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
     const int64_t wd = a0 + (int64_t)r * 64 + lane;
     wr[r] = wd < a1 ? cur : 0ull;
     c += __popcll(wr[r]);
+  }
   }
   auto word_at = [&](int64_t) -> uint64_t { return 0ull; };  // never called: every range is cached
   const Gather4 G{};

@@ -54,8 +54,9 @@ struct MbxTuning {
   int32_t gather_fused = 1;       // MBX_GATHER_FUSED: 0 = compaction, then k_gather (two launches)
   int32_t select_blocks = 1024;   // MBX_SELECT_BLOCKS: compaction blocks at most (segments per block = nseg / this)
   int32_t cursor_prefetch = 1;    // MBX_CURSOR_PREFETCH: 0 = mbx_cursor_next copies each batch on demand
-  int32_t scan_select_fused = 0;  // MBX_SCAN_SELECT_FUSED: 1 = BitSet + positions in one launch (k_scan_select)
+  int32_t scan_select_fused = 1;  // MBX_SCAN_SELECT_FUSED: 1 = BitSet + positions in one launch (k_scan_select)
   int32_t scan_select_waves = 16; // MBX_SCAN_SELECT_WAVES: waves per k_scan_select block (4 or 16)
+  int32_t scan_words_wt = 1;      // MBX_SCAN_WORDS_WT: BitSet scan words stored write-through
   int32_t select_dbg = 0;         // MBX_SELECT_DBG: diagnostic k_select_ids variants (bit 0 no prefix,
                                   // bit 1 no emission: wrong output), bit 3 per-block stamps, bits 4-5
                                   // k_cnf_select look-back variants (16 back-off, 32 no wait: wrong output,

@@ -283,3 +283,41 @@ def test_gpu_nan_async_surfaces_at_sync(m, ctx):
     with pytest.raises(m.MbxError):
         ctx.sync()
     ctx.sync()
+
+
+def test_gpu_nan_every_shard_context_synced_then_clean(m):
+    """ADVICE r2 (GpuShardedScan.syncAll): two shard contexts whose async
+    scans both reach a NaN each report it once at their own mbx_sync -- the
+    caller syncs every context and keeps the first error -- and a clean query
+    on either afterwards raises nothing (no sticky word left behind); a
+    NaN-free async BitSet scan (no finalize) leaves the word alone too."""
+    import torch
+
+    cols, dele = _table()
+    ctxs = [m.Context(0), m.Context(0)]
+    try:
+        tabs = [c.stage(cols, dele) for c in ctxs]
+        bad = [c.compile(t, CASES[1][1]) for c, t in zip(ctxs, tabs)]
+        ok = [c.compile(t, CASES[0][1]) for c, t in zip(ctxs, tabs)]
+        out = torch.zeros(8, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        for i, c in enumerate(ctxs):
+            c.scan_count_async(bad[i], out.data_ptr() + 8 * i)
+        errors = []
+        for c in ctxs:  # every context synced, the first error kept
+            try:
+                c.sync()
+            except m.MbxError as e:
+                errors.append(e.code)
+        assert errors == [m.mbx.E_TYPE, m.mbx.E_TYPE]
+        want = ctxs[0].scan_count(ok[0])
+        for i, c in enumerate(ctxs):
+            c.scan_count_async(ok[i], out.data_ptr() + 8 * i)
+            bm = c.bitmap_alloc(tabs[i].nrows)
+            c.scan_bitmap_async(ok[i], bm)
+            c.sync()  # clean
+            assert int(out[i].item()) == want
+            assert c.select(bm).size == want
+    finally:
+        for c in ctxs:
+            c.close()

@@ -177,3 +177,19 @@ def test_fused_interleaved_with_cnf_select(ctx):
             got, (v0,) = cur.next(max(1, n))
             assert np.array_equal(got, want) and np.array_equal(v0, c0[want]), n
     del rng
+
+
+def test_fused_100m_rows_large_segments(ctx):
+    """100 M rows: 382-tile segments, four per 16-wave block (256 blocks,
+    96 tiles per wave, the segment's words staged through 48 KB of LDS):
+    positions, count and BitSet equal to the oracle's"""
+    n = 100_000_000
+    cols = [(oracle.INTEGER, 4, c) for c in helpers.synthetic_int_table(n, 2)]
+    ot = oracle.Table(cols)
+    t = ctx.stage(cols)
+    cnf = [[(oracle.LT, ("sym", 1), ("int", 1 << 19))], [(oracle.GE, ("sym", 2), ("int", 1 << 19))]]
+    n_o, w_o, ids_o = oracle.filescan(ot, cnf)
+    plan = ctx.compile(t, cnf)
+    bm, ids, k = run_async(ctx, plan, n)
+    assert k == n_o and np.array_equal(ids, ids_o)
+    assert np.array_equal(bm.download(), w_o)

@@ -117,8 +117,8 @@ def main():
             out({"part": "c2", "rows": n, "variant": name, "selected": want, "us": med})
         # per-block wall_clock64 stamps (100 MHz) of one compaction after its
         # scan (two launches), and of the one-launch form
-        for stamp_cfg in ({"select_dbg": 8}, {"select_dbg": 8, "scan_select_fused": 1},
-                          {"select_dbg": 8, "scan_select_fused": 1, "scan_select_waves": 4}):
+        for stamp_cfg in ({"select_dbg": 8, "scan_select_fused": 0}, {"select_dbg": 8, "scan_select_fused": 1},
+                          {"select_dbg": 8 | 1024, "scan_select_fused": 1}):
           apply(stamp_cfg)
           bm = ctx.bitmap_alloc(n)
           for _ in range(5):
