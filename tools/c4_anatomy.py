@@ -85,9 +85,13 @@ def main():
     assert int(cnt.item()) == want
     print(json.dumps({"part": "c4_times_us", "rows": n, "selected": want, **r}), flush=True)
 
-    # look-back variants (select_dbg bits 4-5): polls with a 1024-clock
-    # back-off; no wait at all (wrong output: the look-back's own cost)
-    for name, dbg in (("backoff", 16), ("no_wait", 32), ("first_round_plain", 64)):
+    # variants (select_dbg >> 4 = the kernel's dbg): 512 = write-through
+    # output stores; interleaved with the default so box drift does not pass
+    # for a difference.  (Round 3 also measured the operand-word phase at
+    # raised wave priority: every block then publishes by 7.9 us instead of
+    # the 4th block per CU at ~27 us, but the launch stays 43.0 us -- the
+    # gathers are bandwidth-bound either way; profiles/r03/c4.)
+    for name, dbg in (("default", 0), ("write_through", 512), ("default", 0)):
         ctx.set_tuning("select_dbg", dbg)
         print(json.dumps({"part": "c4_lookback_variant", "variant": name,
                           "one_launch_projection": timed(lambda: M._chk(L.mbx_cnf_materialize_async(
@@ -100,7 +104,7 @@ def main():
     assert int(cnt.item()) == want
 
     for label, fn, dbg in (("count_only", fused_count_only, 8), ("positions_and_projection", fused, 8),
-                           ("count_only_first_round_plain", fused_count_only, 8 | 64)):
+                           ):
       ctx.set_tuning("select_dbg", dbg)
       for _ in range(5):
         fn()
