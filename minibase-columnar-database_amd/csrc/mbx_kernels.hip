@@ -1489,8 +1489,8 @@ __device__ __forceinline__ int64_t chained_lookback(int64_t* __restrict__ lb, in
   return pre;
 }
 
-template <int G4, class GT, class WordAt, int NW = kWaves>
-__device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int64_t c, bool cached, int64_t a0,
+template <int G4, class GT, class WordAt, int NW = kWaves, int NR = kSelRegs>
+__device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c, bool cached, int64_t a0,
                                             int64_t a1, WordAt word_at, int lane, int wave, int64_t* __restrict__ lb,
                                             int64_t epoch, int64_t row_offset, int64_t* __restrict__ ids,
                                             int64_t* __restrict__ total, const GT& G, int64_t* __restrict__ stamps,
@@ -1537,10 +1537,10 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
   uint32_t tot = 0;  // staged positions (offsets from bit 0 of word a0: < 8 x 4096)
   int nst = 0;       // steps staged
   constexpr int kPrefetch = prefetch_rows<G4>();
-  uint32_t pv[kPrefetch][G4 > 0 ? G4 : 1];
+  uint32_t pv[kPrefetch > 0 ? kPrefetch : 1][G4 > 0 ? G4 : 1];
   if (cached) {
 #pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
+    for (int r = 0; r < NR; ++r) {
       if (a0 + r * 64 >= a1) break;
       const StepScan q = stage_step(wr[r], st, lane, tot, (uint32_t)r * 4096u);
       if (tot + q.total > kStageIds) break;
@@ -1623,7 +1623,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
     const StepScan all{0u, tot};
     store_step<G4, GT>(a0, 0ull, all, off, row_offset, ids, st, lane, G, 64u * kPrefetch, wt);
 #pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int64_t base = a0 + r * 64;
       if (r < nst) continue;
       if (base >= a1) break;
@@ -1637,7 +1637,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[kSelRegs], int6
   // the BitSet (k_scan_select): its words and one segment count per 4 waves
   if (words_out) {
 #pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int64_t wd = a0 + r * 64 + lane;
       if (wd < a1) put(&words_out[wd], wr[r], wt);
     }
@@ -1754,14 +1754,14 @@ constexpr bool kDefaultNT = true;
 // is known -- no second launch, no re-read of the BitSet.  Plans of 1..4
 // 4-byte int literal terms (no float compare: no NaN reach), wave ranges of
 // <= kSelRegs x 16 tiles (tables up to ~134 M rows), <= kLookbackBlocks blocks.
-template <int K, bool DEL, int U, int TQ, int NW>
+template <int K, bool DEL, int U, int TQ, int NW, int NR>
 __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* __restrict__ lb, int64_t row_offset,
                                                          int64_t* __restrict__ ids, int64_t* __restrict__ total,
                                                          int64_t* __restrict__ stamps, int32_t dbg) {
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
   __shared__ int64_t wcount[NW];
   __shared__ int64_t wpre[NW];
-  __shared__ uint16_t stage[NW][32 * 64];
+  __shared__ __attribute__((aligned(16))) uint16_t stage[NW][32 * 64];  // also the segment words (uint64)
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
@@ -1775,12 +1775,11 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
   const int64_t nseg = (ntiles + L.tiles_per_block - 1) / L.tiles_per_block;
   const int64_t tb0 = min(((int64_t)blockIdx.x * (NW / kWaves) + wave / kWaves) * L.tiles_per_block, ntiles);
   const int64_t tb1 = min(tb0 + L.tiles_per_block, ntiles);
-  const int64_t per = (tb1 - tb0 + kWaves - 1) / kWaves;  // tiles per wave (<= 16 * kSelRegs, host-checked)
+  const int64_t per = (tb1 - tb0 + kWaves - 1) / kWaves;  // tiles per wave (<= 16 * NR, launcher-checked)
   const int64_t wt0 = min(tb0 + (wave % kWaves) * per, tb1);
   const int64_t wt1 = min(wt0 + per, tb1);
   const int64_t a0 = wt0 * kWordsPerTile;
   const int64_t a1 = min(wt1 * kWordsPerTile, nwords);
-  const int64_t tfull = min(wt1, nrows / kTileRows);  // this wave's full tiles end here
   const int nterms = P->nterms;
   const uint32_t all = P->all_conj;
   const int32_t* colp[K];
@@ -1794,9 +1793,9 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
   Acc acc;
   acc_init(acc);
   uint64_t wave_count = 0;
-  uint64_t wr[kSelRegs];
+  uint64_t wr[NR];
   int64_t c = 0;
-  if (!(dbg & 64)) {
+  {
     // the segment's 4 waves read its tiles interleaved (wave w % 4 takes
     // tiles w % 4, + 4, + 8, ... as the fast scan does: at any moment the
     // waves of a segment stream adjacent tiles), the words go to LDS (the
@@ -1828,51 +1827,18 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int64_t wd = a0 + (int64_t)r * 64 + lane;
       wr[r] = wd < a1 ? segw[wd - tb0 * kWordsPerTile] : 0ull;
       c += __popcll(wr[r]);
     }
     __syncthreads();  // select_tail stages positions over the same LDS
-  } else {
-#pragma unroll
-  for (int r = 0; r < kSelRegs; ++r) {
-    uint64_t cur = 0;
-    const int64_t g0 = wt0 + (int64_t)r * 16;  // first tile of register group r
-    for (int i = 0; i < 16; i += U) {
-      const int64_t base = g0 + i;
-      if (base >= wt1) break;
-      TileRegs<K, 0> D[U];
-      load_tiles<K, 0, U, kDefaultNT, true>(D, base, 1, tfull, colp, strp, lane);
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int64_t t = base + u;
-        uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
-        if (t < tfull) {
-          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, true>(L, P, D[u], t, lane, nterms, all, 0, false, acc,
-                                                           wave_count, th, w);
-        } else if (t < wt1) {  // the table's one partial tile
-          TileRegs<K, 0> Dp;
-          load_partial<K, 0, true>(Dp, t, nrows, colp, strp, lane);
-          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, false>(L, P, Dp, t, lane, nterms, all, 0, false, acc,
-                                                            wave_count, th, w);
-        }
-        if ((lane >> 2) == i + u) {
-          const int j = lane & 3;
-          cur = j == 0 ? w[0] : (j == 1 ? w[1] : (j == 2 ? w[2] : w[3]));
-        }
-      }
-    }
-    const int64_t wd = a0 + (int64_t)r * 64 + lane;
-    wr[r] = wd < a1 ? cur : 0ull;
-    c += __popcll(wr[r]);
-  }
   }
   auto word_at = [&](int64_t) -> uint64_t { return 0ull; };  // never called: every range is cached
   const Gather4 G{};
-  select_tail<0, Gather4, decltype(word_at), NW>(wr, c, true, a0, a1, word_at, lane, wave, lb, epoch, row_offset, ids,
-                                                 total, G, stamps, dbg, L.seg_counts, nseg, wcount, wpre, stage,
-                                                 L.out_words);
+  select_tail<0, Gather4, decltype(word_at), NW, NR>(wr, c, true, a0, a1, word_at, lane, wave, lb, epoch, row_offset,
+                                                     ids, total, G, stamps, dbg, L.seg_counts, nseg, wcount, wpre,
+                                                     stage, L.out_words);
 }
 
 // Late materialisation (Heapfile.findRID + getRecord per output column,
@@ -2347,18 +2313,30 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
   // the chained look-back (32-bit inclusive prefixes: tables < 2^32 rows)
   dbg = (dbg & ~8) | (!(dbg & 8) ? 8 : 0);
   const bool del = L.deleted != nullptr;
-#define MBX_SCAN_SELECT_NW(KK, UU, NW)                                                                            \
-  if (del)                                                                                                      \
-    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW>), dim3((unsigned)g), dim3(64 * NW), 0, s, L, \
-                       lb, row_offset, ids, total, stamps, dbg);                                                \
-  else                                                                                                          \
-    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW>), dim3((unsigned)g), dim3(64 * NW), 0, s, L, \
-                       lb, row_offset, ids, total, stamps, dbg)
-#define MBX_SCAN_SELECT(KK, UU)          \
-  if (nw == 16) {                        \
-    MBX_SCAN_SELECT_NW(KK, UU, 16);      \
-  } else {                               \
-    MBX_SCAN_SELECT_NW(KK, UU, kWaves);  \
+  // registers of 64 words per wave: only as many as a wave's quarter
+  // segment needs (C2: one) -- the unrolled count / staging / emission code
+  // of unused registers is not instantiated (a smaller kernel for the
+  // instruction cache, fewer VGPRs)
+  const int64_t wave_words = (L.tiles_per_block + kWaves - 1) / kWaves * kWordsPerTile;
+  const int nr = wave_words <= 64 ? 1 : wave_words <= 128 ? 2 : wave_words <= 256 ? 4 : kSelRegs;
+#define MBX_SCAN_SELECT_NW(KK, UU, NW, NR)                                                                          \
+  if (del)                                                                                                        \
+    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, s, \
+                       L, lb, row_offset, ids, total, stamps, dbg);                                               \
+  else                                                                                                            \
+    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \
+                       s, L, lb, row_offset, ids, total, stamps, dbg)
+#define MBX_SCAN_SELECT(KK, UU)                  \
+  if (nw != 16) {                                \
+    MBX_SCAN_SELECT_NW(KK, UU, kWaves, kSelRegs); \
+  } else if (nr == 1) {                          \
+    MBX_SCAN_SELECT_NW(KK, UU, 16, 1);           \
+  } else if (nr == 2) {                          \
+    MBX_SCAN_SELECT_NW(KK, UU, 16, 2);           \
+  } else if (nr == 4) {                          \
+    MBX_SCAN_SELECT_NW(KK, UU, 16, 4);           \
+  } else {                                       \
+    MBX_SCAN_SELECT_NW(KK, UU, 16, kSelRegs);    \
   }
   // tiles in flight per wave as in the fast scan; one column at U = 8 (a C2
   // wave waits on two load batches instead of three) measured slower: the
