@@ -275,16 +275,27 @@ def main():
     G = args.graph_steps if (args.graph_steps > 0 and not gloo_works and not (exchange and comm is None)) else 0
     graphs = []
     if G:
-        k0 = warmup
-        while k0 < warmup + steps:
-            g = min(G, warmup + steps - k0)
-            ctx.graph_begin()
-            run_steps(k0, k0 + g)
-            graphs.append(ctx.graph_end())
-            k0 += g
-        for gr in graphs:  # one untimed replay
-            gr.launch()
-        drain()
+        try:
+            k0 = warmup
+            while k0 < warmup + steps:
+                g = min(G, warmup + steps - k0)
+                ctx.graph_begin()
+                try:
+                    run_steps(k0, k0 + g)
+                finally:
+                    graphs.append(ctx.graph_end())
+                k0 += g
+            for gr in graphs:  # one untimed replay
+                gr.launch()
+            drain()
+        except m.MbxError as err:
+            # a capture the runtime refuses (e.g. a collective it cannot
+            # capture) is not fatal: the steps run eagerly instead
+            print(f"rank {rank}: HIP graph capture failed ({err}); timing eager steps", file=sys.stderr)
+            for gr in graphs:
+                gr.close()
+            graphs, G = [], 0
+            ctx.sync()
     counts.zero_()
     torch.cuda.synchronize()
     if world > 1:

@@ -364,13 +364,20 @@ extern "C" int mbx_graph_end(mbx_ctx* c, mbx_graph** out) {
   HIPCHK(hipSetDevice(c->device));
   c->capturing = false;
   // the exchange stream's captured work joins the origin stream (a capture
-  // ends only with every forked stream joined back)
+  // ends only with every forked stream joined back); the capture is ended
+  // even when the join (or anything captured before it) failed, so the
+  // stream never stays in capture mode
+  hipError_t je = hipSuccess;
   if (c->comm) {
-    HIPCHK(hipEventRecord(c->comm->ev_x, c->comm->xs));
-    HIPCHK(hipStreamWaitEvent(c->stream, c->comm->ev_x, 0));
+    je = hipEventRecord(c->comm->ev_x, c->comm->xs);
+    if (je == hipSuccess) je = hipStreamWaitEvent(c->stream, c->comm->ev_x, 0);
   }
   hipGraph_t g = nullptr;
-  HIPCHK(hipStreamEndCapture(c->stream, &g));
+  const hipError_t ee = hipStreamEndCapture(c->stream, &g);
+  if (je != hipSuccess || ee != hipSuccess) {
+    if (g) hipGraphDestroy(g);
+    return fail(MBX_E_DEVICE, "graph_end: %s", hipGetErrorString(je != hipSuccess ? je : ee));
+  }
   mbx_graph* mg = new (std::nothrow) mbx_graph();
   if (!mg) {
     hipGraphDestroy(g);
