@@ -285,6 +285,7 @@ def test_gpu_nan_async_surfaces_at_sync(m, ctx):
     ctx.sync()
 
 
+@pytest.mark.gpu
 def test_gpu_nan_every_shard_context_synced_then_clean(m):
     """ADVICE r2 (GpuShardedScan.syncAll): two shard contexts whose async
     scans both reach a NaN each report it once at their own mbx_sync -- the
