@@ -327,6 +327,17 @@ int mbx_comm_info(const mbx_comm *comm, int32_t *nranks, int32_t *rank);
 int mbx_comm_wait(mbx_comm *comm);
 int mbx_comm_allreduce_count_async(mbx_comm *comm, int64_t *dev_counts, int64_t n);
 int mbx_comm_allreduce_agg_async(mbx_comm *comm, mbx_agg *dev_rec);
+/* One COUNT query of this rank's shard combined over all ranks into
+ * *dev_count (Query.executeFileScan's resultCount, R/input/Query.java:121-155,
+ * for the whole row-range-sharded table): the scan launch leaves one count
+ * per block in dev_parts (parts_cap int64 slots, device memory, caller-owned;
+ * ~1024 suffice, one buffer per query in flight) and does no finalize; the
+ * exchange stream sums them into *dev_count and all-reduces it -- the sum and
+ * the collective overlap the context stream's next scan.  A plan with a float
+ * term keeps the scan's own finalize (its NaN check): scan, then the
+ * all-reduce, dev_parts unused. */
+int mbx_comm_scan_count_async(mbx_comm *comm, const mbx_plan *plan, int64_t *dev_parts, int64_t parts_cap,
+                              int64_t *dev_count);
 /* dev_all[r] = rank r's *dev_count (device memory, nranks entries) */
 int mbx_comm_allgather_count_async(mbx_comm *comm, const int64_t *dev_count, int64_t *dev_all);
 /* one process, n communicators of one mbx_comm_init_all clique (rank order) */

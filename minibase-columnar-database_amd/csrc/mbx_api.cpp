@@ -910,7 +910,8 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   // plan with no float term (no NaN to report): no finalize at all -- its
   // ticket round trips are ~1 us at the end of every launch (10 M rows:
   // 10.7 -> 9.7 us, profiles/r03/fin)
-  if (!need_count && mode == kModeBitmap && seg_counts && !p->host.has_real && tu.fin_mode < 0)
+  if (!need_count && (mode == kModeBitmap || mode == kModeCount) && seg_counts && !p->host.has_real &&
+      tu.fin_mode < 0)
     L.fin_mode = kFinSegOnly;
   if (L.fin_mode == kFinSeparate) L.ticket = nullptr;
   if (fused) {
@@ -964,6 +965,24 @@ extern "C" int mbx_scan_count(mbx_ctx* c, const mbx_plan* pc, int64_t* count) {
   HIPCHK(hipStreamSynchronize(c->stream));
   *count = h[0];
   return check_nan(c);
+}
+
+bool mbx::plan_has_real(const mbx_plan* p) { return p->host.has_real != 0; }
+
+int mbx::scan_count_parts(mbx_ctx* c, const mbx_plan* pc, int64_t* dev_parts, int64_t cap, int64_t* nparts) {
+  mbx_plan* p = const_cast<mbx_plan*>(pc);
+  if (p->host.has_real)
+    return fail(MBX_E_INVALID, "scan_count_parts: a plan with a float term needs the in-launch finalize (NaN)");
+  PlanVariant* v = nullptr;
+  int rc = plan_variant(p, -1, &v);
+  if (rc) return rc;
+  const int64_t tpb = scan_tiles_per_block(c, p->t->nrows, *v);
+  const int64_t nb = grid_blocks(p->t->nrows, tpb);
+  if (nb > cap) return fail(MBX_E_INVALID, "scan_count_parts: %lld blocks, capacity %lld", (long long)nb, (long long)cap);
+  if ((rc = ensure_partials(c, nb))) return rc;
+  *nparts = nb;
+  return enqueue_scan(c, p, *v, kModeCount, nullptr, c->partials, tpb, nullptr, nullptr, c->dnan, dev_parts, nullptr,
+                      false);
 }
 
 extern "C" int mbx_scan_count_async(mbx_ctx* c, const mbx_plan* pc, int64_t* dev_count) {

@@ -249,6 +249,25 @@ extern "C" int mbx_comm_allreduce_count_async(mbx_comm* m, int64_t* dev_counts, 
   return MBX_OK;
 }
 
+extern "C" int mbx_comm_scan_count_async(mbx_comm* m, const mbx_plan* p, int64_t* dev_parts, int64_t parts_cap,
+                                         int64_t* dev_count) {
+  NOTNULL(m);
+  NOTNULL(p);
+  NOTNULL(dev_count);
+  HIPCHK(hipSetDevice(m->ctx->device));
+  if (plan_has_real(p)) {  // the NaN check needs the scan's own finalize: scan, then the collective
+    if (int rc = mbx_scan_count_async(m->ctx, p, dev_count)) return rc;
+    return mbx_comm_allreduce_count_async(m, dev_count, 1);
+  }
+  NOTNULL(dev_parts);
+  int64_t nb = 0;
+  if (int rc = scan_count_parts(m->ctx, p, dev_parts, parts_cap, &nb)) return rc;
+  if (int rc = fork_after_main(m)) return rc;
+  HIPCHK(launch_count_sum(dev_parts, nb, dev_count, m->xs));
+  NCCLCHK(ncclAllReduce(dev_count, dev_count, 1, ncclInt64, ncclSum, m->nc, m->xs));
+  return MBX_OK;
+}
+
 extern "C" int mbx_comm_allreduce_agg_async(mbx_comm* m, mbx_agg* dev_rec) {
   NOTNULL(m);
   NOTNULL(dev_rec);

@@ -180,6 +180,11 @@ int ensure_count(mbx_ctx* c, mbx_bitmap* b);
 // recount per-segment popcounts of a bitmap written on the device, sync, and
 // set b->count
 int bitmap_recount(mbx_ctx* c, mbx_bitmap* b);
+// a COUNT scan that leaves one count per block in dev_parts (no finalize,
+// no count): *nparts = the blocks; MBX_E_INVALID for a plan with a float
+// term (its NaN needs the finalize) or more blocks than cap
+int scan_count_parts(mbx_ctx* c, const mbx_plan* p, int64_t* dev_parts, int64_t cap, int64_t* nparts);
+bool plan_has_real(const mbx_plan* p);
 // mbx_comm.cpp: mbx_sync / mbx_free of a context with a communicator
 int comm_sync(mbx_ctx* c);
 void comm_release_of(mbx_ctx* c);

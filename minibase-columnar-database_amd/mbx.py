@@ -89,7 +89,8 @@ EXPORTS = [
     "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close", "mbx_cursor_stats", "mbx_cnf_cursor_open", "mbx_cnf_cursor_launch",
     "mbx_probe_read", "mbx_set_tuning",
     "mbx_diag_select_stamps", "mbx_dev_alloc", "mbx_dev_free", "mbx_dev_download", "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
-    "mbx_comm_info", "mbx_comm_wait", "mbx_comm_allreduce_count_async", "mbx_comm_allreduce_agg_async",
+    "mbx_comm_info", "mbx_comm_wait", "mbx_comm_allreduce_count_async", "mbx_comm_scan_count_async",
+    "mbx_comm_allreduce_agg_async",
     "mbx_comm_allgather_count_async", "mbx_comm_allreduce_count_all", "mbx_comm_allreduce_agg_all",
     "mbx_comm_allgather_count_all",
     "mbx_graph_begin", "mbx_graph_end", "mbx_graph_launch", "mbx_graph_free",
@@ -184,6 +185,7 @@ def lib():
         "mbx_comm_info": ([V, P(I32), P(I32)], ctypes.c_int),
         "mbx_comm_wait": ([V], ctypes.c_int),
         "mbx_comm_allreduce_count_async": ([V, V, I64], ctypes.c_int),
+        "mbx_comm_scan_count_async": ([V, V, V, I64, V], ctypes.c_int),
         "mbx_comm_allreduce_agg_async": ([V, V], ctypes.c_int),
         "mbx_comm_allgather_count_async": ([V, V, V], ctypes.c_int),
         "mbx_comm_allreduce_count_all": ([P(V), I32, P(V), I64], ctypes.c_int),
@@ -715,6 +717,12 @@ class Comm:
 
     def allreduce_count_async(self, dev_ptr, n=1):
         _chk(lib().mbx_comm_allreduce_count_async(self.h, dev_ptr, n))
+
+    def scan_count_async(self, plan, dev_parts, parts_cap, dev_count):
+        """one COUNT query combined over all ranks into *dev_count; the scan's
+        per-block counts go to dev_parts (parts_cap int64 device slots), the
+        exchange stream sums and all-reduces them"""
+        _chk(lib().mbx_comm_scan_count_async(self.h, plan.h, dev_parts, parts_cap, dev_count))
 
     def allreduce_agg_async(self, dev_ptr):
         _chk(lib().mbx_comm_allreduce_agg_async(self.h, dev_ptr))

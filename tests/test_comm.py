@@ -162,3 +162,56 @@ def test_graph_replays_scan_and_exchange(m, torch_cuda, with_comm):
         g.close()
     finally:
         ctx.close()
+
+
+INT_CNFS = [
+    [[(oracle.LT, ("sym", 1), ("int", 1 << 19))], [(oracle.GE, ("sym", 2), ("int", 1 << 19))]],
+    [[(oracle.EQ, ("sym", 1), ("int", 7)), (oracle.GT, ("sym", 2), ("int", 1000))]],
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deleted", [False, True])
+def test_comm_scan_count_parts_and_exchange(m, torch_cuda, deleted):
+    """mbx_comm_scan_count_async (one-rank clique): the scan leaves one count
+    per block in dev_parts, the exchange stream sums and all-reduces them --
+    equal to the scan's own COUNT for int plans, eagerly and replayed from a
+    graph; a float plan keeps the finalize (scan, then the collective); too
+    small a parts buffer is refused"""
+    torch = torch_cuda
+    ctx = m.Context(0)
+    try:
+        n = 3_000_017
+        cols = [(oracle.INTEGER, 4, c) for c in helpers.synthetic_int_table(n, 2, hi=1 << 20, seed=9)]
+        cols.append((oracle.REAL, 4, np.random.Generator(np.random.PCG64(2)).random(n, dtype=np.float32)))
+        dele = helpers.random_deleted(n, 0.05, seed=4) if deleted else None
+        t = ctx.stage(cols, dele, row_offset=128)
+        comm = ctx.comm_init_rank(1, 0, m.mbx.comm_unique_id())
+        cap = 2048
+        parts = torch.zeros(8 * cap, dtype=torch.int64, device="cuda")
+        out = torch.zeros(8, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        float_cnf = [[(oracle.LT, ("sym", 1), ("int", 1 << 19))], [(oracle.LT, ("sym", 3), ("real", 0.25))]]
+        plans = [ctx.compile(t, cnf) for cnf in INT_CNFS] + [ctx.compile(t, float_cnf)]
+        wants = [ctx.scan_count(p) for p in plans]
+        for i, p in enumerate(plans):
+            comm.scan_count_async(p, parts.data_ptr() + 8 * cap * i, cap, out.data_ptr() + 8 * i)
+        ctx.sync()
+        assert out[:len(plans)].cpu().tolist() == wants
+        # a graph of the int queries, replayed
+        ctx.graph_begin()
+        for i, p in enumerate(plans[:2]):
+            comm.scan_count_async(p, parts.data_ptr() + 8 * cap * (4 + i), cap, out.data_ptr() + 8 * (4 + i))
+        g = ctx.graph_end()
+        for _ in range(3):
+            out.zero_()
+            torch.cuda.synchronize()
+            g.launch()
+            ctx.sync()
+            assert out[4:6].cpu().tolist() == wants[:2]
+        g.close()
+        with pytest.raises(m.MbxError):
+            comm.scan_count_async(plans[0], parts.data_ptr(), 4, out.data_ptr())
+        ctx.sync()
+    finally:
+        ctx.close()
