@@ -8,8 +8,10 @@ One "step" = one ColumnarFileScan COUNT pass over the resident table:
 executed as ONE kernel launch per GPU (k_scan_fast<2, COUNT>; its last block
 folds the per-block counts), plus -- on N > 1 GPUs -- the path's one exchange
 step: an in-place RCCL all-reduce of the COUNTs over xGMI, issued by libmbx
-(mbx_comm_allreduce_count_async) on the communicator's exchange stream, so
-the next scans overlap it.  Every step (= query) has its own collective
+(mbx_comm_allreduce_count_async) right after the scan on the same stream
+(libmbx's default: inside a captured graph a collective forked to a second
+stream is not overlapped on this ROCm and costs more, profiles/r03/parts).
+Every step (= query) has its own collective
 (--exchange-bucket 1, the default: SURVEY 8(e)'s per-query
 N_total / (max_k t_kernel,k + t_reduce)); --exchange-bucket B > 1 lets the
 COUNTs of B consecutive steps share one all-reduce (a diagnostic: a tiny
@@ -245,6 +247,11 @@ def main():
     gloo_works = []
 
     B = max(1, args.exchange_bucket)
+    # diagnostic (MBX_BENCH_XS_KERNEL=1): one more real kernel per step where
+    # the collective runs (an aggregate all-gather + device fold of a dummy
+    # record), standing in on one GPU for an N-rank collective's kernel
+    xs_kernel = comm is not None and os.environ.get("MBX_BENCH_XS_KERNEL") == "1"
+    dummy = torch.zeros(8, dtype=torch.int64, device="cuda") if xs_kernel else None
 
     def run_steps(k0, k1):
         """steps k0..k1-1: one scan each; the exchange all-reduces the COUNTs
@@ -256,6 +263,8 @@ def main():
                 ctx.scan_count_async(plan, base + 8 * k)
             if comm is not None:
                 comm.allreduce_count_async(base + 8 * j, je - j)
+                if xs_kernel:
+                    comm.allreduce_agg_async(dummy.data_ptr())
             elif exchange:  # same-device rehearsal: gloo over host copies
                 gloo_works.extend(range(j, je))
 
@@ -351,9 +360,9 @@ def main():
         ms_per_step = t_max * 1e3 / steps
         algo_bytes = 2 * 4 * n  # c0 + c1 read once per launch (rank 0's shard)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        xchg = ((f"RCCL all-reduce of the COUNTs of every {B} steps (libmbx mbx_comm, exchange stream)" if B > 1
-                 else "RCCL all-reduce of every step's COUNT (one collective per query; libmbx mbx_comm, "
-                      "exchange stream)")
+        xchg = ((f"RCCL all-reduce of the COUNTs of every {B} steps (libmbx mbx_comm, after the scans)" if B > 1
+                 else "RCCL all-reduce of every step's COUNT (one collective per query; libmbx mbx_comm, right "
+                      "after the step's scan on the same stream)")
                 if comm is not None else None) or (
             "gloo all-reduce (same-device rehearsal)" if exchange else "none")
         out = {

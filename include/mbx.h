@@ -306,10 +306,13 @@ int mbx_cnf_cursor_launch(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *co
  *                        MIN/MAX over the per-rank values)
  *   positions         -> all-gather of the per-rank counts (the concatenation
  *                        offsets; shard order = ascending global positions)
- * Stream order: a collective runs on the communicator's exchange stream after
- * everything already enqueued on the context stream; the context stream does
- * not wait for it (the next scans overlap).  mbx_sync waits for both;
- * mbx_comm_wait makes later context work (device side) wait for it. */
+ * Stream order: a collective runs after everything already enqueued on the
+ * context stream -- on the context stream itself (the default), or with the
+ * tuning knob comm_same_stream = 0 (MBX_COMM_SAME_STREAM=0) on the
+ * communicator's exchange stream, which the context stream does not wait for
+ * (the next scans may overlap it; inside a captured HIP graph on this ROCm
+ * they do not, and the fork costs more than it hides).  mbx_sync waits for
+ * both; mbx_comm_wait makes later context work (device side) wait for it. */
 typedef struct mbx_comm mbx_comm;
 #define MBX_COMM_ID_BYTES 128
 

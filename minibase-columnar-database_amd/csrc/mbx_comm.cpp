@@ -98,8 +98,20 @@ void comm_release(mbx_comm* m) {
   delete m;
 }
 
+// where a collective runs: the context stream itself, right after the query
+// that feeds it (knob comm_same_stream, default), or the communicator's
+// exchange stream (the next scans could overlap it).  Measured on one GPU,
+// 12.5 M-row shard, one collective per query, HIP graphs of 10 steps, with a
+// stand-in real kernel per step beside the one-rank all-reduce: 20.4-20.6
+// us per step on the context stream vs 34-35 us on the exchange stream (a
+// kernel forked to a second stream inside a graph is not overlapped on this
+// ROCm); 17.5-17.7 vs 18.0-18.2 without it (profiles/r03/parts)
+bool same_stream(const mbx_comm* m) { return m->ctx->tune.comm_same_stream != 0; }
+hipStream_t xstream(const mbx_comm* m) { return same_stream(m) ? m->ctx->stream : m->xs; }
+
 // the exchange stream waits for the context stream's work so far
 int fork_after_main(mbx_comm* m) {
+  if (same_stream(m)) return MBX_OK;
   HIPCHK(hipEventRecord(m->ev_main, m->ctx->stream));
   HIPCHK(hipStreamWaitEvent(m->xs, m->ev_main, 0));
   return MBX_OK;
@@ -234,6 +246,7 @@ extern "C" int mbx_comm_info(const mbx_comm* m, int32_t* nranks, int32_t* rank) 
 extern "C" int mbx_comm_wait(mbx_comm* m) {
   NOTNULL(m);
   HIPCHK(hipSetDevice(m->ctx->device));
+  if (same_stream(m)) return MBX_OK;  // already in the context stream's order
   HIPCHK(hipEventRecord(m->ev_x, m->xs));
   HIPCHK(hipStreamWaitEvent(m->ctx->stream, m->ev_x, 0));
   return MBX_OK;
@@ -245,7 +258,7 @@ extern "C" int mbx_comm_allreduce_count_async(mbx_comm* m, int64_t* dev_counts, 
   if (n <= 0) return fail(MBX_E_INVALID, "allreduce_count: n = %lld", (long long)n);
   HIPCHK(hipSetDevice(m->ctx->device));
   if (int rc = fork_after_main(m)) return rc;
-  NCCLCHK(ncclAllReduce(dev_counts, dev_counts, (size_t)n, ncclInt64, ncclSum, m->nc, m->xs));
+  NCCLCHK(ncclAllReduce(dev_counts, dev_counts, (size_t)n, ncclInt64, ncclSum, m->nc, xstream(m)));
   return MBX_OK;
 }
 
@@ -263,8 +276,8 @@ extern "C" int mbx_comm_scan_count_async(mbx_comm* m, const mbx_plan* p, int64_t
   int64_t nb = 0;
   if (int rc = scan_count_parts(m->ctx, p, dev_parts, parts_cap, &nb)) return rc;
   if (int rc = fork_after_main(m)) return rc;
-  HIPCHK(launch_count_sum(dev_parts, nb, dev_count, m->xs));
-  NCCLCHK(ncclAllReduce(dev_count, dev_count, 1, ncclInt64, ncclSum, m->nc, m->xs));
+  HIPCHK(launch_count_sum(dev_parts, nb, dev_count, xstream(m)));
+  NCCLCHK(ncclAllReduce(dev_count, dev_count, 1, ncclInt64, ncclSum, m->nc, xstream(m)));
   return MBX_OK;
 }
 
@@ -274,8 +287,8 @@ extern "C" int mbx_comm_allreduce_agg_async(mbx_comm* m, mbx_agg* dev_rec) {
   static_assert(sizeof(mbx_agg) == sizeof(AggOut), "mbx_agg layout");
   HIPCHK(hipSetDevice(m->ctx->device));
   if (int rc = fork_after_main(m)) return rc;
-  NCCLCHK(ncclAllGather(dev_rec, m->gathered, sizeof(AggOut) / sizeof(int64_t), ncclInt64, m->nc, m->xs));
-  hipLaunchKernelGGL(k_fold_agg, dim3(1), dim3(64), 0, m->xs, m->gathered, m->nranks, (AggOut*)dev_rec);
+  NCCLCHK(ncclAllGather(dev_rec, m->gathered, sizeof(AggOut) / sizeof(int64_t), ncclInt64, m->nc, xstream(m)));
+  hipLaunchKernelGGL(k_fold_agg, dim3(1), dim3(64), 0, xstream(m), m->gathered, m->nranks, (AggOut*)dev_rec);
   HIPCHK(hipGetLastError());
   return MBX_OK;
 }
@@ -286,7 +299,7 @@ extern "C" int mbx_comm_allgather_count_async(mbx_comm* m, const int64_t* dev_co
   NOTNULL(dev_all);
   HIPCHK(hipSetDevice(m->ctx->device));
   if (int rc = fork_after_main(m)) return rc;
-  NCCLCHK(ncclAllGather(dev_count, dev_all, 1, ncclInt64, m->nc, m->xs));
+  NCCLCHK(ncclAllGather(dev_count, dev_all, 1, ncclInt64, m->nc, xstream(m)));
   return MBX_OK;
 }
 
@@ -303,7 +316,7 @@ extern "C" int mbx_comm_allreduce_count_all(mbx_comm* const* comms, int32_t n, i
   NCCLCHK(ncclGroupStart());
   for (int32_t i = 0; i < n; ++i) {
     const ncclResult_t r =
-        ncclAllReduce(dev_counts[i], dev_counts[i], (size_t)count, ncclInt64, ncclSum, comms[i]->nc, comms[i]->xs);
+        ncclAllReduce(dev_counts[i], dev_counts[i], (size_t)count, ncclInt64, ncclSum, comms[i]->nc, xstream(comms[i]));
     if (r != ncclSuccess) {
       ncclGroupEnd();
       return fail(MBX_E_DEVICE, "ncclAllReduce (rank %d): %s", i, ncclGetErrorString(r));
@@ -326,7 +339,7 @@ extern "C" int mbx_comm_allgather_count_all(mbx_comm* const* comms, int32_t n, c
   }
   NCCLCHK(ncclGroupStart());
   for (int32_t i = 0; i < n; ++i) {
-    const ncclResult_t r = ncclAllGather(dev_counts[i], dev_alls[i], 1, ncclInt64, comms[i]->nc, comms[i]->xs);
+    const ncclResult_t r = ncclAllGather(dev_counts[i], dev_alls[i], 1, ncclInt64, comms[i]->nc, xstream(comms[i]));
     if (r != ncclSuccess) {
       ncclGroupEnd();
       return fail(MBX_E_DEVICE, "ncclAllGather (rank %d): %s", i, ncclGetErrorString(r));
@@ -347,7 +360,7 @@ extern "C" int mbx_comm_allreduce_agg_all(mbx_comm* const* comms, int32_t n, mbx
   NCCLCHK(ncclGroupStart());
   for (int32_t i = 0; i < n; ++i) {
     const ncclResult_t r = ncclAllGather(dev_recs[i], comms[i]->gathered, sizeof(AggOut) / sizeof(int64_t),
-                                         ncclInt64, comms[i]->nc, comms[i]->xs);
+                                         ncclInt64, comms[i]->nc, xstream(comms[i]));
     if (r != ncclSuccess) {
       ncclGroupEnd();
       return fail(MBX_E_DEVICE, "ncclAllGather (rank %d): %s", i, ncclGetErrorString(r));
@@ -357,7 +370,7 @@ extern "C" int mbx_comm_allreduce_agg_all(mbx_comm* const* comms, int32_t n, mbx
   // the folds follow their all-gathers on each exchange stream
   for (int32_t i = 0; i < n; ++i) {
     HIPCHK(hipSetDevice(comms[i]->ctx->device));
-    hipLaunchKernelGGL(k_fold_agg, dim3(1), dim3(64), 0, comms[i]->xs, comms[i]->gathered, n,
+    hipLaunchKernelGGL(k_fold_agg, dim3(1), dim3(64), 0, xstream(comms[i]), comms[i]->gathered, n,
                        (AggOut*)dev_recs[i]);
     HIPCHK(hipGetLastError());
   }
@@ -387,7 +400,7 @@ extern "C" int mbx_graph_end(mbx_ctx* c, mbx_graph** out) {
   // even when the join (or anything captured before it) failed, so the
   // stream never stays in capture mode
   hipError_t je = hipSuccess;
-  if (c->comm) {
+  if (c->comm && !same_stream(c->comm)) {
     je = hipEventRecord(c->comm->ev_x, c->comm->xs);
     if (je == hipSuccess) je = hipStreamWaitEvent(c->stream, c->comm->ev_x, 0);
   }
