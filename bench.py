@@ -175,6 +175,10 @@ def main():
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured HIP graph (0: eager launches)")
     ap.add_argument("--exchange-bucket", type=int, default=1,
                     help="steps whose COUNTs share one all-reduce (1, the default: one collective per query)")
+    ap.add_argument("--count", choices=["auto", "frame", "finalize"], default="auto",
+                    help="frame: each scan adds its COUNT into a 32-slot count frame (no in-launch finalize; the "
+                         "exchange all-reduces whole frames); finalize: the scan's last block writes the COUNT; "
+                         "auto: frame with an exchange, finalize without")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -240,7 +244,13 @@ def main():
     assert got == want, f"rank {rank}: scan count {got} != reference {want}"
 
     steps, warmup = args.steps, args.warmup
-    counts = torch.zeros(steps + warmup, dtype=torch.int64, device="cuda")
+    # count frames (mbx_scan_count_frame_async): with an exchange, each step's
+    # scan adds its packed per-block counts into its own zeroed 4 KB frame with
+    # no-return atomics and the all-reduce sums whole frames -- the launch ends
+    # without the finalize's dependent atomic round trips
+    frames = args.count == "frame" or (args.count == "auto" and exchange)
+    FW = m.mbx.COUNT_FRAME_WORDS if frames else 1
+    counts = torch.zeros((steps + warmup, FW), dtype=torch.int64, device="cuda")
     ext = torch.cuda.ExternalStream(ctx.stream)
     torch.cuda.set_stream(ext)
     base = counts.data_ptr()
@@ -260,9 +270,12 @@ def main():
         for j in range(k0, k1, B):
             je = min(j + B, k1)
             for k in range(j, je):
-                ctx.scan_count_async(plan, base + 8 * k)
+                if frames:
+                    ctx.scan_count_frame_async(plan, base + 8 * FW * k)
+                else:
+                    ctx.scan_count_async(plan, base + 8 * k)
             if comm is not None:
-                comm.allreduce_count_async(base + 8 * j, je - j)
+                comm.allreduce_count_async(base + 8 * FW * j, FW * (je - j))
                 if xs_kernel:
                     comm.allreduce_agg_async(dummy.data_ptr())
             elif exchange:  # same-device rehearsal: gloo over host copies
@@ -324,7 +337,24 @@ def main():
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
-    c = counts[warmup:].cpu()
+    if frames:
+        # decode every step's frame (mbx_count_frame_decode's sums, on the
+        # device): count = sum of the slots' high bits; every block of every
+        # rank must have arrived exactly once
+        slots = counts[warmup:].view(steps, 32, 16)[:, :, 0]
+        c = (slots >> 24).sum(1).cpu()
+        arrivals = (slots & 0xFFF).sum(1).cpu()
+        nblocks = ctx.scan_blocks(plan)
+        if world > 1:  # shards may differ by a block: the frames hold every rank's
+            tb = torch.tensor([nblocks], dtype=torch.int64)
+            dist.all_reduce(tb)
+            nblocks = int(tb[0])
+        assert bool((arrivals == nblocks).all()), f"rank {rank}: frame arrivals {arrivals[:4].tolist()} != {nblocks}"
+        assert int(((slots >> 12) & 0xFFF).sum()) == 0, "NaN blocks in an integer plan"
+        h0 = counts[warmup].cpu().numpy()
+        assert m.mbx.count_frame_decode(h0)[0] == int(c[0])
+    else:
+        c = counts[warmup:, 0].cpu()
 
     # kernel duration: the scans alone again, each bracketed by HIP events
     # recorded on the stream the kernel runs on (the library's stream)
@@ -332,7 +362,10 @@ def main():
     ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     for k in range(steps):
         ev_s[k].record(ext)
-        ctx.scan_count_async(plan, base + 8 * (warmup + k))
+        if frames:
+            ctx.scan_count_frame_async(plan, base + 8 * FW * (warmup + k))
+        else:
+            ctx.scan_count_async(plan, base + 8 * (warmup + k))
         ev_e[k].record(ext)
     ctx.sync()
     kern_ms = sum(a.elapsed_time(b) for a, b in zip(ev_s, ev_e)) / steps
@@ -390,6 +423,8 @@ def main():
                 "exchange": xchg,
                 "graph_steps": G,
                 "exchange_bucket_steps": B if exchange else None,
+                "count": "frame (32 packed slots per query, summed by the all-reduce; mbx_scan_count_frame_async)"
+                         if frames else "in-launch finalize (mbx_scan_count_async)",
             },
             "phases_us": {
                 "step_wall": ms_per_step * 1e3,

@@ -181,6 +181,22 @@ int mbx_plan_free(mbx_plan *p);
 int mbx_scan_count(mbx_ctx *ctx, const mbx_plan *p, int64_t *count);
 /* enqueue only; *dev_count (device memory) receives the count */
 int mbx_scan_count_async(mbx_ctx *ctx, const mbx_plan *p, int64_t *dev_count);
+/* Count frame: the same COUNT (Query.executeFileScan's resultCount,
+ * R/input/Query.java:137-152) enqueued with no in-launch finalize -- every
+ * block adds its packed (count, NaN block, arrival) word to one of 32 slots
+ * of a caller-zeroed, 128-byte-aligned frame of MBX_COUNT_FRAME_WORDS int64
+ * words (slot s at word 16 s) with a no-return atomic, so the launch ends
+ * without the last-arriver round trips.  Frames are additive: an in-place
+ * int64 sum all-reduce of whole frames (mbx_comm_allreduce_count_async with
+ * n = MBX_COUNT_FRAME_WORDS) combines ranks, and mbx_count_frame_decode
+ * reads the total from a host copy.  A NaN in a float comparison is counted
+ * per block in the frame and also raised at the next mbx_sync, like every
+ * async scan.  Tables up to 2^36 rows per rank and 16 ranks per frame. */
+#define MBX_COUNT_FRAME_WORDS 512
+int mbx_scan_count_frame_async(mbx_ctx *ctx, const mbx_plan *p, int64_t *dev_frame);
+int mbx_count_frame_decode(const int64_t *host_frame, int64_t *count, int64_t *nan_blocks, int64_t *arrivals);
+/* blocks of this plan's COUNT launch (= the arrivals one frame records) */
+int mbx_scan_blocks(mbx_ctx *ctx, const mbx_plan *p, int64_t *blocks);
 /* the selection as a device BitSet (the get_next_tid() stream as positions) */
 int mbx_scan_bitmap(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap **out, int64_t *count);
 int mbx_scan_bitmap_async(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap *out);

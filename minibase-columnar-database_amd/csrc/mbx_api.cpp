@@ -870,7 +870,7 @@ struct FusedSelect {
 static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int32_t mode, uint64_t* out_words,
                         Partial* parts, int64_t tpb, int64_t* count_out, AggOut* agg_out, int32_t* nan_out,
                         int64_t* seg_counts = nullptr, const FusedSelect* fused = nullptr,
-                        bool need_count = true) {
+                        bool need_count = true, bool frame = false) {
   ScanLaunch L;
   L.plan = v.dev;
   L.nrows = p->t->nrows;
@@ -915,6 +915,10 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   if (!need_count && (mode == kModeBitmap || mode == kModeCount) && seg_counts && !p->host.has_real &&
       tu.fin_mode < 0)
     L.fin_mode = kFinSegOnly;
+  if (frame) {  // mbx_scan_count_frame_async: count_out is the frame
+    L.fin_mode = kFinFrame;
+    L.ticket = nullptr;
+  }
   if (L.fin_mode == kFinSeparate) L.ticket = nullptr;
   if (fused) {
     int64_t* stamps = nullptr;
@@ -992,6 +996,60 @@ extern "C" int mbx_scan_count_async(mbx_ctx* c, const mbx_plan* pc, int64_t* dev
   NOTNULL(pc);
   NOTNULL(dev_count);
   return scan_to_count(c, const_cast<mbx_plan*>(pc), dev_count, c->dnan);
+}
+
+// a frame slot holds < 4096 arrivals (and NaN blocks) summed over every rank
+// that adds into it: ceil(blocks / 32) <= 255 keeps 16 ranks' frames exact
+constexpr int64_t kFrameMaxArrivalsPerSlot = 255;
+
+extern "C" int mbx_scan_count_frame_async(mbx_ctx* c, const mbx_plan* pc, int64_t* dev_frame) {
+  NOTNULL(c);
+  NOTNULL(pc);
+  NOTNULL(dev_frame);
+  static_assert(kFrameSlots * kFrameSlotStride == MBX_COUNT_FRAME_WORDS, "count frame layout");
+  mbx_plan* p = const_cast<mbx_plan*>(pc);
+  if ((reinterpret_cast<uintptr_t>(dev_frame) & 127) != 0)
+    return fail(MBX_E_INVALID, "scan_count_frame: the frame must be 128-byte aligned");
+  int rc = set_device(c);
+  if (rc) return rc;
+  PlanVariant* v = nullptr;
+  if ((rc = plan_variant(p, -1, &v))) return rc;
+  const int64_t tpb = scan_tiles_per_block(c, p->t->nrows, *v);
+  const int64_t nb = grid_blocks(p->t->nrows, tpb);
+  if ((nb + kFrameSlots - 1) / kFrameSlots > kFrameMaxArrivalsPerSlot || p->t->nrows >= (int64_t(1) << 36))
+    return fail(MBX_E_INVALID, "scan_count_frame: %lld rows in %lld blocks do not fit a count frame",
+                (long long)p->t->nrows, (long long)nb);
+  if ((rc = ensure_partials(c, nb))) return rc;
+  return enqueue_scan(c, p, *v, kModeCount, nullptr, c->partials, tpb, dev_frame, nullptr, c->dnan, nullptr, nullptr,
+                      true, true);
+}
+
+extern "C" int mbx_count_frame_decode(const int64_t* frame, int64_t* count, int64_t* nan_blocks, int64_t* arrivals) {
+  NOTNULL(frame);
+  NOTNULL(count);
+  int64_t n = 0, nan = 0, arr = 0;
+  for (int s = 0; s < kFrameSlots; ++s) {
+    const uint64_t w = (uint64_t)frame[(size_t)s * kFrameSlotStride];
+    n += (int64_t)(w >> 24);
+    nan += (int64_t)((w >> 12) & 0xfff);
+    arr += (int64_t)(w & 0xfff);
+  }
+  *count = n;
+  if (nan_blocks) *nan_blocks = nan;
+  if (arrivals) *arrivals = arr;
+  return MBX_OK;
+}
+
+extern "C" int mbx_scan_blocks(mbx_ctx* c, const mbx_plan* pc, int64_t* blocks) {
+  NOTNULL(c);
+  NOTNULL(pc);
+  NOTNULL(blocks);
+  mbx_plan* p = const_cast<mbx_plan*>(pc);
+  PlanVariant* v = nullptr;
+  int rc = plan_variant(p, -1, &v);
+  if (rc) return rc;
+  *blocks = grid_blocks(p->t->nrows, scan_tiles_per_block(c, p->t->nrows, *v));
+  return MBX_OK;
 }
 
 static int scan_bitmap_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int32_t* dev_nan, bool need_count = true) {

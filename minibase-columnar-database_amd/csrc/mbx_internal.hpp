@@ -161,7 +161,17 @@ enum FinMode : int32_t {
                          // no NaN to report): no ticket, no count.  Forced on
                          // a COUNT scan (MBX_FIN_MODE=4) it is a diagnostic:
                          // the count is not produced -- what the finalize costs
+  kFinFrame = 5,         // COUNT into a caller-zeroed count frame: each block adds
+                         // its packed (count, nan, 1) word to slot blockIdx % 32
+                         // with a no-return atomic -- no ticket, no last arriver,
+                         // no dependent round trip at the end of the launch; the
+                         // reader adds the 32 slots (mbx_count_frame_decode)
 };
+
+// count frame (mbx_scan_count_frame_async): MBX_COUNT_FRAME_SLOTS packed words,
+// one per 128-byte line so the slots' atomics do not share a line
+constexpr int kFrameSlots = 32;
+constexpr int kFrameSlotStride = 16;  // int64 words per slot line
 
 struct ProjCol {
   const void* base;

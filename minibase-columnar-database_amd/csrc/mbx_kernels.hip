@@ -352,6 +352,18 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
     }
     return;
   }
+  if (!FULL && L.fin_mode == kFinFrame) {
+    if (threadIdx.x == 0) {
+      Acc r = sh[0];
+#pragma unroll
+      for (int w = 1; w < kWaves; ++w) acc_merge(r, sh[w]);
+      // result unused: a no-return atomic, nothing waits for it in the block
+      __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(L.count_out) + (blockIdx.x % kFrameSlots) * kFrameSlotStride,
+                             pack_count(r.count, r.nan ? 1u : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (r.nan && L.nan_out) __hip_atomic_store(L.nan_out + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   if (!FULL && L.ticket && L.fin_mode == kFinPackedCount) {
     if (threadIdx.x == 0) {
       Acc r = sh[0];

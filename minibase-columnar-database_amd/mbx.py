@@ -81,7 +81,8 @@ def java_mutf8(s):
 EXPORTS = [
     "mbx_abi_version", "mbx_last_error", "mbx_device_count", "mbx_init", "mbx_free", "mbx_sync", "mbx_stream",
     "mbx_table_stage", "mbx_table_wrap", "mbx_table_free", "mbx_table_info", "mbx_plan_compile", "mbx_plan_free",
-    "mbx_scan_count", "mbx_scan_count_async", "mbx_scan_bitmap", "mbx_scan_bitmap_async", "mbx_scan_select",
+    "mbx_scan_count", "mbx_scan_count_async", "mbx_scan_count_frame_async", "mbx_count_frame_decode",
+    "mbx_scan_blocks", "mbx_scan_bitmap", "mbx_scan_bitmap_async", "mbx_scan_select",
     "mbx_scan_select_async", "mbx_scan_aggregate",
     "mbx_scan_aggregate_async", "mbx_bitmap_alloc", "mbx_bitmap_upload", "mbx_bitmap_download", "mbx_bitmap_info",
     "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_cnf_materialize_async", "mbx_bitmap_index_build",
@@ -144,6 +145,9 @@ def lib():
         "mbx_plan_free": ([V], ctypes.c_int),
         "mbx_scan_count": ([V, V, P(I64)], ctypes.c_int),
         "mbx_scan_count_async": ([V, V, V], ctypes.c_int),
+        "mbx_scan_count_frame_async": ([V, V, V], ctypes.c_int),
+        "mbx_count_frame_decode": ([V, P(I64), P(I64), P(I64)], ctypes.c_int),
+        "mbx_scan_blocks": ([V, V, P(I64)], ctypes.c_int),
         "mbx_scan_bitmap": ([V, V, P(V), P(I64)], ctypes.c_int),
         "mbx_scan_bitmap_async": ([V, V, V], ctypes.c_int),
         "mbx_scan_select": ([V, V, V, I64, P(I64)], ctypes.c_int),
@@ -466,6 +470,16 @@ class Context:
     def scan_count_async(self, plan, dev_ptr):
         _chk(lib().mbx_scan_count_async(self.h, plan.h, dev_ptr))
 
+    def scan_count_frame_async(self, plan, dev_frame):
+        """COUNT added into a zeroed, 128-byte-aligned frame of COUNT_FRAME_WORDS
+        int64 words at dev_frame (no in-launch finalize; count_frame_decode)."""
+        _chk(lib().mbx_scan_count_frame_async(self.h, plan.h, dev_frame))
+
+    def scan_blocks(self, plan):
+        b = ctypes.c_int64()
+        _chk(lib().mbx_scan_blocks(self.h, plan.h, ctypes.byref(b)))
+        return b.value
+
     def scan_bitmap(self, plan):
         h = ctypes.c_void_p()
         n = ctypes.c_int64()
@@ -653,6 +667,18 @@ class _Handle:
 
 
 COMM_ID_BYTES = 128
+COUNT_FRAME_WORDS = 512
+
+
+def count_frame_decode(frame):
+    """(count, nan_blocks, arrivals) of a host copy of a count frame (a numpy
+    int64 array of COUNT_FRAME_WORDS words, possibly all-reduced over ranks)."""
+    import numpy as np
+    f = np.ascontiguousarray(frame, dtype=np.int64)
+    assert f.size >= COUNT_FRAME_WORDS, f.size
+    n, nan, arr = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    _chk(lib().mbx_count_frame_decode(f.ctypes.data, ctypes.byref(n), ctypes.byref(nan), ctypes.byref(arr)))
+    return n.value, nan.value, arr.value
 
 
 def comm_unique_id():
