@@ -81,6 +81,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.tiles_per_block = env_knob("MBX_TILES_PER_BLOCK", -1);
   t.force_generic = (int32_t)env_knob("MBX_FORCE_GENERIC", 0);
   t.scan_hoist = (int32_t)env_knob("MBX_SCAN_HOIST", 1);
+  t.scan_int_range = (int32_t)env_knob("MBX_SCAN_INT_RANGE", 1);
   t.scan_ri = (int32_t)env_knob("MBX_SCAN_RI", 1);
   t.sink_lds = (int32_t)env_knob("MBX_SINK_LDS", 1);
   t.ticket_groups = (int32_t)env_knob("MBX_TICKET_GROUPS", -1);
@@ -278,6 +279,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   if (!strcmp(knob, "tiles_per_block")) t.tiles_per_block = value;
   else if (!strcmp(knob, "force_generic")) t.force_generic = v;
   else if (!strcmp(knob, "scan_hoist")) t.scan_hoist = v;
+  else if (!strcmp(knob, "scan_int_range")) t.scan_int_range = v;
   else if (!strcmp(knob, "scan_ri")) t.scan_ri = v;
   else if (!strcmp(knob, "sink_lds")) t.sink_lds = v;
   else if (!strcmp(knob, "ticket_groups")) t.ticket_groups = v;
@@ -576,6 +578,8 @@ static int32_t cmp_op_of(int32_t op) {
 }
 
 // comp(lit, col) = -comp(col, lit): mirror the operator
+static void int_range_of(KTerm& kt);
+
 static int32_t flip(int32_t op) {
   switch (op) {
     case kLT: return kGT;
@@ -707,7 +711,10 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
       kt.op = op;
       kt.nan_lit = nan_lit ? 1 : 0;
       if (kt.rhs < 0) {
-        if (ctype == MBX_ATTR_INTEGER) kt.ilit = lit->integer;
+        if (ctype == MBX_ATTR_INTEGER) {
+          kt.ilit = lit->integer;
+          int_range_of(kt);
+        }
         else if (real) kt.flit = lit->real;
         else {
           int rc = add_pool_string(p, *lit, pool_used, kt);
@@ -732,6 +739,28 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
   p->host.nterms = nterms;
   p->host.all_conj = all;
   return MBX_OK;
+}
+
+// kt.op against kt.ilit as one unsigned range test: a OP lit holds iff
+// ((uint32)a - (uint32)rlo <= rspan) != rneg -- the same truth table as the
+// kernels' cmp4 for every int32 a (empty ranges: the full range negated)
+static void int_range_of(KTerm& kt) {
+  const int64_t lit = kt.ilit, mn = INT32_MIN, mx = INT32_MAX;
+  int64_t lo = mn, hi = mx;
+  bool neg = false, empty = false;
+  switch (kt.op) {
+    case kLT: empty = lit == mn; hi = lit - 1; break;
+    case kLE: hi = lit; break;
+    case kGT: empty = lit == mx; lo = lit + 1; break;
+    case kGE: lo = lit; break;
+    case kEQ: lo = hi = lit; break;
+    case kNE: lo = hi = lit; neg = true; break;
+    default: empty = true; break;  // kNever
+  }
+  if (empty) lo = mn, hi = mx, neg = true;
+  kt.rlo = (int32_t)lo;
+  kt.rspan = (uint32_t)hi - (uint32_t)(int32_t)lo;
+  kt.rneg = neg ? 1 : 0;
 }
 
 static int plan_variant(mbx_plan* p, int32_t agg_col, PlanVariant** out) {
@@ -901,7 +930,13 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.ticket_groups = ticket_groups_of(c);
   L.seg_counts = seg_counts;
   L.words_wt = tu.scan_words_wt;
-  L.pad_wt_ = 0;
+  L.int_range = 0;
+  if (tu.scan_int_range && !p->host.has_real && v.fast_ks == 0) {
+    bool ir = p->host.nterms >= 1;
+    for (int32_t i = 0; i < p->host.nterms; i++)
+      ir = ir && p->host.terms[i].kind == kInt && p->host.terms[i].rhs < 0;
+    L.int_range = ir ? 1 : 0;
+  }
   L.fin_mode = tu.fin_mode >= 0 ? tu.fin_mode : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
   if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))
     L.fin_mode = kFinWriteThrough;

@@ -61,6 +61,12 @@ struct KTerm {
   // raises (TupleUtils.java:61-69 falls through to the string branch).
   uint32_t req_below;  // all_conj & (conj_bit - 1)
   int32_t nan_lit;     // the literal is NaN (or a literal-vs-literal NaN term): raises whenever reached
+  // int `column OP literal` as one unsigned range test (the scan's branch-free
+  // term body, ScanLaunch.int_range): holds iff ((uint32)(a - rlo) <= rspan) != rneg
+  int32_t rlo;
+  uint32_t rspan;
+  int32_t rneg;
+  int32_t rpad_;
 };
 
 // The compiled predicate (PredEval over one CNF) + optional aggregate column.
@@ -130,7 +136,7 @@ struct ScanLaunch {
                               //    (tiles_per_block x 32 B) and stored in one burst at the block's end
   int64_t* seg_counts;        // BitSet scans: the output bitmap's per-segment counts (one per block)
   int32_t words_wt;           // BitSet words stored write-through (sc1) instead of plain
-  int32_t pad_wt_;
+  int32_t int_range;          // every term an int literal compare: branch-free range-test body
 };
 
 // dynamic LDS per block for the staged BitSet (4 blocks per CU: <= 128 KB of

@@ -712,7 +712,10 @@ __device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const u
 // own conjunct did (R/iterator/PredEval.java:164-175); KTerm.req_below.
 // WHOLE: the tile is one of the table's full tiles (the main loop's): no row
 // bound checks -- only the one partial tile needs them
-template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool RI = false, bool WHOLE = false>
+// IR: every term is an int `column OP literal` (ScanLaunch.int_range): the
+// term body is one unsigned range test per row, no branch on the operator or
+// the comparison type (KTerm.rlo / rspan / rneg, mbx_api.cpp int_range_of)
+template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool RI = false, bool WHOLE = false, bool IR = false>
 __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, KS>& D,
                                           int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
                                           Acc& acc, uint64_t& wave_count, const KTerm* th = nullptr,
@@ -729,7 +732,21 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
     const KTerm& T = TQ > 0 ? th[ti] : P->terms[ti];
     const int lhs = T.lhs;
     bool r[4];
-    if (KS > 0 && T.kind == kStr) {
+    if constexpr (IR) {
+      int32_t a[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
+#pragma unroll
+      for (int s = 1; s < K; ++s)
+        if (lhs == s) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
+        }
+      const uint32_t lo = (uint32_t)T.rlo, span = T.rspan;
+      const bool neg = T.rneg != 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) r[j] = (((uint32_t)a[j] - lo) <= span) != neg;
+    } else if (KS > 0 && T.kind == kStr) {
       uint32_t lit[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) lit[i] = i < T.swords ? __builtin_bswap32(P->pool[T.soff + i]) : 0u;
@@ -975,7 +992,7 @@ __device__ __forceinline__ void load_partial(TileRegs<K, KS>& D, int64_t t, int6
 // counts feed compaction).  A grid-stride interleave measured equal on MI355X
 // (DESIGN.md section 5).
 // TQ > 0: <= TQ literal terms hoisted into registers, term loop unrolled.
-template <int K, int KS, int MODE, bool DEL, int U, bool NT, int TQ = 0, bool RI = false>
+template <int K, int KS, int MODE, bool DEL, int U, bool NT, int TQ = 0, bool RI = false, bool IR = false>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
@@ -1043,16 +1060,16 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
       if (t < tf) {
         if constexpr (kSink) {
           uint64_t w[4];
-          fast_tile<K, KS, MODE, DEL, TQ, RI, true>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
-                                              th, w);
+          fast_tile<K, KS, MODE, DEL, TQ, RI, true, IR>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc,
+                                                  wave_count, th, w);
           if ((lane >> 2) == sink_n) {
             const int j = lane & 3;
             sink = j == 0 ? w[0] : (j == 1 ? w[1] : (j == 2 ? w[2] : w[3]));
           }
           if (++sink_n == 16) sink_flush();
         } else {
-          fast_tile<K, KS, MODE, DEL, TQ, RI, true>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
-                                              th);
+          fast_tile<K, KS, MODE, DEL, TQ, RI, true, IR>(L, P, D[u], t, lane, nterms, all, agg_slot, agg_real, acc,
+                                                  wave_count, th);
         }
       }
     }
@@ -1079,7 +1096,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   if ((nrows % kTileRows) != 0 && tp >= t0 + wave && tp < t1 && (tp - t0 - wave) % ustep == 0) {
     TileRegs<K, KS> D;
     load_partial<K, KS, RI>(D, tp, nrows, colp, strp, lane);
-    fast_tile<K, KS, MODE, DEL, TQ, RI>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count, th);
+    fast_tile<K, KS, MODE, DEL, TQ, RI, false, IR>(L, P, D, tp, lane, nterms, all, agg_slot, agg_real, acc, wave_count,
+                                                 th);
   }
   acc.count = lane == 0 ? (int64_t)wave_count : 0;
   block_reduce_store<MODE == kModeAgg>(acc, L);
@@ -2099,6 +2117,13 @@ static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   // two columns at U=2); 100M rows: COUNT 69.7 -> 67.3 us, BitSet 87.5 -> 81.0 us
   constexpr int kU = K == 1 && KS == 0 ? 4 : kDefaultU;
   const unsigned lds = L.sink_lds ? (unsigned)(L.tiles_per_block * kWordsPerTile * sizeof(uint64_t)) : 0u;
+  // int literal terms as branch-free range tests (COUNT scans)
+  if constexpr (KS == 0 && MODE == kModeCount) {
+    if (L.hoist_terms && L.int_range) {
+      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, TQ, RI, true>), grid, dim3(kBlock), lds, s, L);
+      return;
+    }
+  }
   if (KS == 0 && L.hoist_terms)
     hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, TQ, RI>), grid, dim3(kBlock), lds, s, L);
   else
