@@ -1784,7 +1784,7 @@ constexpr bool kDefaultNT = true;
 // is known -- no second launch, no re-read of the BitSet.  Plans of 1..4
 // 4-byte int literal terms (no float compare: no NaN reach), wave ranges of
 // <= kSelRegs x 16 tiles (tables up to ~134 M rows), <= kLookbackBlocks blocks.
-template <int K, bool DEL, int U, int TQ, int NW, int NR>
+template <int K, bool DEL, int U, int TQ, int NW, int NR, bool IR = false>
 __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* __restrict__ lb, int64_t row_offset,
                                                          int64_t* __restrict__ ids, int64_t* __restrict__ total,
                                                          int64_t* __restrict__ stamps, int32_t dbg) {
@@ -1843,12 +1843,12 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
         const int64_t t = base + (int64_t)u * kWaves;
         uint64_t w[4] = {0ull, 0ull, 0ull, 0ull};
         if (t < tf) {
-          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, true>(L, P, D[u], t, lane, nterms, all, 0, false, acc,
+          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, true, IR>(L, P, D[u], t, lane, nterms, all, 0, false, acc,
                                                            wave_count, th, w);
         } else if (t < tb1) {  // the table's one partial tile
           TileRegs<K, 0> Dp;
           load_partial<K, 0, true>(Dp, t, nrows, colp, strp, lane);
-          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, false>(L, P, Dp, t, lane, nterms, all, 0, false, acc,
+          fast_tile<K, 0, kModeBitmap, DEL, TQ, true, false, IR>(L, P, Dp, t, lane, nterms, all, 0, false, acc,
                                                             wave_count, th, w);
         }
         if (t < tb1 && lane < 4)
@@ -2117,8 +2117,8 @@ static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   // two columns at U=2); 100M rows: COUNT 69.7 -> 67.3 us, BitSet 87.5 -> 81.0 us
   constexpr int kU = K == 1 && KS == 0 ? 4 : kDefaultU;
   const unsigned lds = L.sink_lds ? (unsigned)(L.tiles_per_block * kWordsPerTile * sizeof(uint64_t)) : 0u;
-  // int literal terms as branch-free range tests (COUNT scans)
-  if constexpr (KS == 0 && MODE == kModeCount) {
+  // int literal terms as branch-free range tests
+  if constexpr (KS == 0) {
     if (L.hoist_terms && L.int_range) {
       hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, TQ, RI, true>), grid, dim3(kBlock), lds, s, L);
       return;
@@ -2350,17 +2350,24 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
   // the chained look-back (32-bit inclusive prefixes: tables < 2^32 rows)
   dbg = (dbg & ~8) | (!(dbg & 8) ? 8 : 0);
   const bool del = L.deleted != nullptr;
+  const bool ir = L.int_range != 0;  // branch-free int terms (every fused plan qualifies; the knob can turn it off)
   // registers of 64 words per wave: only as many as a wave's quarter
   // segment needs (C2: one) -- the unrolled count / staging / emission code
   // of unused registers is not instantiated (a smaller kernel for the
   // instruction cache, fewer VGPRs)
   const int64_t wave_words = (L.tiles_per_block + kWaves - 1) / kWaves * kWordsPerTile;
   const int nr = wave_words <= 64 ? 1 : wave_words <= 128 ? 2 : wave_words <= 256 ? 4 : kSelRegs;
-#define MBX_SCAN_SELECT_NW(KK, UU, NW, NR)                                                                          \
-  if (del)                                                                                                        \
-    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, s, \
-                       L, lb, row_offset, ids, total, stamps, dbg);                                               \
-  else                                                                                                            \
+#define MBX_SCAN_SELECT_NW(KK, UU, NW, NR)                                                                       \
+  if (del && ir)                                                                                               \
+    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR, true>), dim3((unsigned)g), dim3(64 * NW), \
+                       0, s, L, lb, row_offset, ids, total, stamps, dbg);                                      \
+  else if (del)                                                                                                \
+    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \
+                       s, L, lb, row_offset, ids, total, stamps, dbg);                                         \
+  else if (ir)                                                                                                 \
+    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR, true>), dim3((unsigned)g),            \
+                       dim3(64 * NW), 0, s, L, lb, row_offset, ids, total, stamps, dbg);                       \
+  else                                                                                                         \
     hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \
                        s, L, lb, row_offset, ids, total, stamps, dbg)
 #define MBX_SCAN_SELECT(KK, UU)                  \

@@ -1,5 +1,5 @@
-"""Branch-free int terms (knob scan_int_range, default on): a COUNT scan whose
-terms are all int `column OP literal` compares evaluates each term as one
+"""Branch-free int terms (knob scan_int_range, default on): a scan (COUNT,
+BitSet, positions, aggregate) whose terms are all int `column OP literal` compares evaluates each term as one
 unsigned range test, ((uint32)(a - rlo) <= rspan) != rneg, built on the host
 from the operator and the literal (mbx_api.cpp int_range_of).  PredEval's
 integer compare (R/iterator/PredEval.java:131-162, TupleUtils.CompareTupleWithValue
@@ -55,6 +55,25 @@ def _count_both(m, ctx, t, cnf):
     return on, off
 
 
+def _all_outputs(m, ctx, t, ot, cnf, agg_col=2):
+    """BitSet (k_scan_fast BitSet mode), positions (the one-launch
+    k_scan_select) and an int aggregate with the knob on and off, each equal
+    to the oracle's"""
+    n_o, w_o, ids_o = oracle.filescan(ot, cnf)
+    agg_o = oracle.aggregate(ot, cnf, agg_col)
+    plan = ctx.compile(t, cnf)
+    for ir in (1, 0):
+        ctx.set_tuning("scan_int_range", ir)
+        bm = ctx.scan_bitmap(plan)
+        assert bm.count == n_o and np.array_equal(bm.download(), w_o), (ir, cnf)
+        assert np.array_equal(ctx.scan_select(plan), ids_o), (ir, cnf)
+        got = ctx.scan_aggregate(plan, agg_col)
+        assert got["count"] == agg_o["count"], (ir, cnf)
+        if agg_o["count"]:  # empty selections: identities are representation details
+            assert got == agg_o, (ir, cnf, got, agg_o)
+    ctx.set_tuning("scan_int_range", 1)
+
+
 @pytest.mark.parametrize("op", [LT, LE, GT, GE, EQ, NE, NOP])
 def test_every_operator_at_the_edges(m, ctx, op):
     cols = _table()
@@ -66,6 +85,8 @@ def test_every_operator_at_the_edges(m, ctx, op):
             want = oracle.filescan_count(ot, cnf)
             on, off = _count_both(m, ctx, t, cnf)
             assert on == off == want, (op, lit, cnf, on, off, want)
+            if lit in (IMIN, 0, IMAX):
+                _all_outputs(m, ctx, t, ot, cnf)
 
 
 def test_conjunctions_and_disjunctions(m, ctx):
@@ -87,6 +108,7 @@ def test_conjunctions_and_disjunctions(m, ctx):
         want = oracle.filescan_count(ot, cnf)
         on, off = _count_both(m, ctx, t, cnf)
         assert on == off == want, (cnf, on, off, want)
+        _all_outputs(m, ctx, t, ot, cnf)
 
 
 def test_deleted_rows_and_ragged_sizes(m, ctx):
@@ -103,3 +125,4 @@ def test_deleted_rows_and_ragged_sizes(m, ctx):
             want = oracle.filescan_count(ot, cnf)
             on, off = _count_both(m, ctx, t, cnf)
             assert on == off == want, (n, cnf, on, off, want)
+            _all_outputs(m, ctx, t, ot, cnf)
