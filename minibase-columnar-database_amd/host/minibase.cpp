@@ -721,6 +721,8 @@ ColumnarFileScan::ColumnarFileScan(const std::string& file_name, const std::vect
   if ((int)proj_list.size() != n_out_flds) throw FileScanException("ColumnarFileScan: n_out_flds");
   setup_jtuple(Jtuple_, in1, s1_sizes, proj_list);
   for (const auto& p : proj_list) proj_cols_.push_back(p.offset - 1);
+  types_ = f_.getAttributeTypes();
+  sizes_ = f_.getAttrSizes();
   CnfImage img = flatten(outFilter);
   mbx_cnf cnf = img.view();
   mbx_ctx* c = global::SystemDefs::ctx();
@@ -743,12 +745,10 @@ void ColumnarFileScan::next_batch() {
     chk<FileScanException>(mbx_cursor_open(c, f_.table(), sel_->get(), proj_cols_.data(), (int32_t)proj_cols_.size(),
                                            &cur_),
                            "ColumnarFileScan: materialise");
-  const auto types = f_.getAttributeTypes();
-  const auto sizes = f_.getAttrSizes();
   batch_.resize(proj_cols_.size());
   std::vector<void*> ptrs(proj_cols_.size());
   for (size_t j = 0; j < proj_cols_.size(); j++) {
-    batch_[j].resize((size_t)(Batch::kRows * col_width(types, sizes, proj_cols_[j])));
+    batch_[j].resize((size_t)(Batch::kRows * col_width(types_, sizes_, proj_cols_[j])));
     ptrs[j] = batch_[j].data();
   }
   batch_ids_.resize((size_t)Batch::kRows);
@@ -762,7 +762,7 @@ heap::Tuple* ColumnarFileScan::get_next() {
     next_batch();
     if (batch_n_ == 0) return nullptr;
   }
-  fill_row(Jtuple_, f_.getAttributeTypes(), f_.getAttrSizes(), proj_cols_, batch_, batch_i_);
+  fill_row(Jtuple_, types_, sizes_, proj_cols_, batch_, batch_i_);
   batch_i_++;
   return &Jtuple_;
 }

@@ -325,6 +325,8 @@ class ColumnarFileScan : public Iterator {
   columnar::BitSetPtr sel_;
   mbx_cursor* cur_ = nullptr;
   std::vector<int32_t> proj_cols_;
+  std::vector<AttrType> types_;  // the file's schema, read once (get_next runs per row)
+  std::vector<short> sizes_;
   std::vector<std::vector<uint8_t>> batch_;
   std::vector<int64_t> batch_ids_;
   int64_t batch_n_ = 0, batch_i_ = 0;
