@@ -81,7 +81,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.tiles_per_block = env_knob("MBX_TILES_PER_BLOCK", -1);
   t.force_generic = (int32_t)env_knob("MBX_FORCE_GENERIC", 0);
   t.scan_hoist = (int32_t)env_knob("MBX_SCAN_HOIST", 1);
-  t.scan_int_range = (int32_t)env_knob("MBX_SCAN_INT_RANGE", 1);
+  t.scan_int_range = (int32_t)env_knob("MBX_SCAN_INT_RANGE", 2);
   t.scan_ri = (int32_t)env_knob("MBX_SCAN_RI", 1);
   t.sink_lds = (int32_t)env_knob("MBX_SINK_LDS", 1);
   t.ticket_groups = (int32_t)env_knob("MBX_TICKET_GROUPS", -1);
@@ -579,6 +579,8 @@ static int32_t cmp_op_of(int32_t op) {
 
 // comp(lit, col) = -comp(col, lit): mirror the operator
 static void int_range_of(KTerm& kt);
+static void float_range_of(KTerm& kt);
+static void str_range_of(KTerm& kt);
 
 static int32_t flip(int32_t op) {
   switch (op) {
@@ -681,6 +683,7 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
           kt.op = kNever;
           kt.lhs = s0;
           kt.nan_lit = 1;
+          float_range_of(kt);  // empty: never true (it raises wherever reached)
           p->host.has_real = 1;
           p->host.terms[nterms++] = kt;
         } else if (!never && op_on(e.op, 0)) {
@@ -714,11 +717,13 @@ static int compile_into(mbx_ctx* c, const mbx_table* t, const mbx_cnf* cnf, mbx_
         if (ctype == MBX_ATTR_INTEGER) {
           kt.ilit = lit->integer;
           int_range_of(kt);
-        }
-        else if (real) kt.flit = lit->real;
-        else {
+        } else if (real) {
+          kt.flit = lit->real;
+          float_range_of(kt);
+        } else {
           int rc = add_pool_string(p, *lit, pool_used, kt);
           if (rc) return rc;
+          str_range_of(kt);
         }
       }
       if (ctype == MBX_ATTR_STRING && kt.rhs < 0 && kt.swords > 4) p->str_lit_fits16 = false;
@@ -761,6 +766,53 @@ static void int_range_of(KTerm& kt) {
   kt.rlo = (int32_t)lo;
   kt.rspan = (uint32_t)hi - (uint32_t)(int32_t)lo;
   kt.rneg = neg ? 1 : 0;
+  kt.rm31 = 0;
+}
+
+static void set_key_range(KTerm& kt, int64_t lo, int64_t hi, bool neg, uint32_t rm31) {
+  if (lo > hi) lo = INT32_MIN, hi = INT32_MAX, neg = true;  // empty
+  kt.rlo = (int32_t)lo;
+  kt.rspan = (uint32_t)(int32_t)hi - (uint32_t)(int32_t)lo;
+  kt.rneg = neg ? 1 : 0;
+  kt.rm31 = rm31;
+}
+
+// float `a OP lit` over the signed-ordered key of a (KTerm.rm31): the kernels'
+// cmp4<float> IEEE truth table for every non-NaN a (-0.0 == +0.0); a NaN row
+// that reaches the term raises whatever the range says (nan_lit: empty)
+static int32_t float_key(float f) {
+  uint32_t b;
+  memcpy(&b, &f, 4);
+  return (int32_t)(b ^ ((uint32_t)((int32_t)b >> 31) & 0x7fffffffu));
+}
+
+static void float_range_of(KTerm& kt) {
+  const int64_t ninf = float_key(-INFINITY), pinf = float_key(INFINITY);
+  const float lit = kt.flit;
+  if (kt.nan_lit || std::isnan(lit) || kt.op == kNever) return set_key_range(kt, 1, 0, false, 0x7fffffffu);
+  const int64_t elo = lit == 0.0f ? float_key(-0.0f) : float_key(lit);
+  const int64_t ehi = lit == 0.0f ? float_key(0.0f) : float_key(lit);
+  switch (kt.op) {
+    case kLT: return set_key_range(kt, ninf, elo - 1, false, 0x7fffffffu);
+    case kLE: return set_key_range(kt, ninf, ehi, false, 0x7fffffffu);
+    case kGT: return set_key_range(kt, ehi + 1, pinf, false, 0x7fffffffu);
+    case kGE: return set_key_range(kt, elo, pinf, false, 0x7fffffffu);
+    case kEQ: return set_key_range(kt, elo, ehi, false, 0x7fffffffu);
+    default: return set_key_range(kt, elo, ehi, true, 0x7fffffffu);  // kNE
+  }
+}
+
+// char(n) `s OP lit`: the compareTo sign c in {-1, 0, 1} against 0
+static void str_range_of(KTerm& kt) {
+  switch (kt.op) {
+    case kLT: return set_key_range(kt, -1, -1, false, 0);
+    case kLE: return set_key_range(kt, -1, 0, false, 0);
+    case kGT: return set_key_range(kt, 1, 1, false, 0);
+    case kGE: return set_key_range(kt, 0, 1, false, 0);
+    case kEQ: return set_key_range(kt, 0, 0, false, 0);
+    case kNE: return set_key_range(kt, 0, 0, true, 0);
+    default: return set_key_range(kt, 1, 0, false, 0);  // kNever
+  }
 }
 
 static int plan_variant(mbx_plan* p, int32_t agg_col, PlanVariant** out) {
@@ -931,11 +983,17 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
   L.seg_counts = seg_counts;
   L.words_wt = tu.scan_words_wt;
   L.int_range = 0;
-  if (tu.scan_int_range && !p->host.has_real && v.fast_ks == 0) {
-    bool ir = p->host.nterms >= 1;
-    for (int32_t i = 0; i < p->host.nterms; i++)
-      ir = ir && p->host.terms[i].kind == kInt && p->host.terms[i].rhs < 0;
-    L.int_range = ir ? 1 : 0;
+  if (tu.scan_int_range && p->host.nterms >= 1) {
+    bool ints = true, lits = true;
+    for (int32_t i = 0; i < p->host.nterms; i++) {
+      ints = ints && p->host.terms[i].kind == kInt;
+      lits = lits && p->host.terms[i].rhs < 0;
+    }
+    if (lits && ints && !p->host.has_real && v.fast_ks == 0) L.int_range = 1;
+    // typed range tests (float / char(16) terms too): COUNT and aggregate scans
+    // of up to kHoistTerms terms, knob value 2 or more
+    else if (lits && tu.scan_int_range >= 2 && mode != kModeBitmap && p->host.nterms <= kHoistTerms)
+      L.int_range = 2;
   }
   L.fin_mode = tu.fin_mode >= 0 ? tu.fin_mode : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
   if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))

@@ -61,12 +61,16 @@ struct KTerm {
   // raises (TupleUtils.java:61-69 falls through to the string branch).
   uint32_t req_below;  // all_conj & (conj_bit - 1)
   int32_t nan_lit;     // the literal is NaN (or a literal-vs-literal NaN term): raises whenever reached
-  // int `column OP literal` as one unsigned range test (the scan's branch-free
-  // term body, ScanLaunch.int_range): holds iff ((uint32)(a - rlo) <= rspan) != rneg
+  // `column OP literal` as one unsigned range test over a signed-ordered key
+  // (the scan's branch-free term body): holds iff ((uint32)(x - rlo) <= rspan)
+  // != rneg, x = the int value; a float's bits with the low 31 bits flipped
+  // when negative (x = a ^ ((a >> 31) & rm31), rm31 = 0x7fffffff: -0.0 and
+  // +0.0 become the adjacent keys -1 and 0, NaNs fall outside [-inf, +inf]);
+  // a string's compareTo sign against the literal (-1 / 0 / 1)
   int32_t rlo;
   uint32_t rspan;
   int32_t rneg;
-  int32_t rpad_;
+  uint32_t rm31;
 };
 
 // The compiled predicate (PredEval over one CNF) + optional aggregate column.
@@ -136,7 +140,8 @@ struct ScanLaunch {
                               //    (tiles_per_block x 32 B) and stored in one burst at the block's end
   int64_t* seg_counts;        // BitSet scans: the output bitmap's per-segment counts (one per block)
   int32_t words_wt;           // BitSet words stored write-through (sc1) instead of plain
-  int32_t int_range;          // every term an int literal compare: branch-free range-test body
+  int32_t int_range;          // branch-free range-test term body: 1 every term an int literal
+                              // compare, 2 literal compares of any type (int / float / char(16))
 };
 
 // dynamic LDS per block for the staged BitSet (4 blocks per CU: <= 128 KB of

@@ -712,10 +712,13 @@ __device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const u
 // own conjunct did (R/iterator/PredEval.java:164-175); KTerm.req_below.
 // WHOLE: the tile is one of the table's full tiles (the main loop's): no row
 // bound checks -- only the one partial tile needs them
-// IR: every term is an int `column OP literal` (ScanLaunch.int_range): the
+// IR = 1: every term is an int `column OP literal` (ScanLaunch.int_range): the
 // term body is one unsigned range test per row, no branch on the operator or
-// the comparison type (KTerm.rlo / rspan / rneg, mbx_api.cpp int_range_of)
-template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool RI = false, bool WHOLE = false, bool IR = false>
+// the comparison type (KTerm.rlo / rspan / rneg, mbx_api.cpp int_range_of).
+// IR = 2: literal terms of any type, one range test over a signed-ordered key
+// (KTerm.rm31: float bits; a char(16) term's compareTo sign); a float term
+// still tracks PredEval's NaN reach
+template <int K, int KS, int MODE, bool DEL, int TQ = 0, bool RI = false, bool WHOLE = false, int IR = 0>
 __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __restrict__ P, const TileRegs<K, KS>& D,
                                           int64_t t, int lane, int nterms, uint32_t all, int agg_slot, bool agg_real,
                                           Acc& acc, uint64_t& wave_count, const KTerm* th = nullptr,
@@ -732,7 +735,59 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
     const KTerm& T = TQ > 0 ? th[ti] : P->terms[ti];
     const int lhs = T.lhs;
     bool r[4];
-    if constexpr (IR) {
+    if constexpr (IR == 2) {
+      const uint32_t lo = (uint32_t)T.rlo, span = T.rspan;
+      const bool neg = T.rneg != 0;
+      if (KS > 0 && T.kind == kStr) {
+        uint32_t lit[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lit[i] = i < T.swords ? __builtin_bswap32(P->pool[T.soff + i]) : 0u;
+        int32_t c[4];
+        if (KS == 1 || lhs == K)
+          str16_cmp4(D.s[0], lit, c);
+        else
+          str16_cmp4(D.s[KS > 1 ? 1 : 0], lit, c);
+        bool rs[4];  // rs[j] is row 64j + lane (string slots load row-interleaved)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rs[j] = (((uint32_t)c[j] - lo) <= span) != neg;
+        if (RI) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] = rs[j];
+        } else {
+          const uint64_t w0 = __ballot(rs[0]), w1 = __ballot(rs[1]), w2 = __ballot(rs[2]), w3 = __ballot(rs[3]);
+          const int q = lane >> 4;
+          const uint64_t w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
+          const uint32_t nib = (uint32_t)(w >> ((lane & 15) * 4));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r[j] = (nib >> j) & 1u;
+        }
+      } else {
+        int32_t a[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
+#pragma unroll
+        for (int s = 1; s < K; ++s)
+          if (lhs == s) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
+          }
+        if (T.kind == kReal) {
+          const uint32_t below = T.req_below, own = T.conj_bit;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float f = __int_as_float(a[j]);
+            const bool reach = ((cb[j] & below) == below) && !(cb[j] & own);
+            nanr[j] = nanr[j] || (reach && (T.nan_lit || f != f));
+          }
+        }
+        const uint32_t rm = T.rm31;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t x = (uint32_t)a[j] ^ ((uint32_t)(a[j] >> 31) & rm);
+          r[j] = ((x - lo) <= span) != neg;
+        }
+      }
+    } else if constexpr (IR == 1) {
       int32_t a[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) a[j] = D.v[0][j];
@@ -992,7 +1047,7 @@ __device__ __forceinline__ void load_partial(TileRegs<K, KS>& D, int64_t t, int6
 // counts feed compaction).  A grid-stride interleave measured equal on MI355X
 // (DESIGN.md section 5).
 // TQ > 0: <= TQ literal terms hoisted into registers, term loop unrolled.
-template <int K, int KS, int MODE, bool DEL, int U, bool NT, int TQ = 0, bool RI = false, bool IR = false>
+template <int K, int KS, int MODE, bool DEL, int U, bool NT, int TQ = 0, bool RI = false, int IR = 0>
 __global__ __launch_bounds__(kBlock) void k_scan_fast(ScanLaunch L) {
   const KPlan* __restrict__ P = L.plan;
   const int lane = threadIdx.x & 63;
@@ -1784,7 +1839,7 @@ constexpr bool kDefaultNT = true;
 // is known -- no second launch, no re-read of the BitSet.  Plans of 1..4
 // 4-byte int literal terms (no float compare: no NaN reach), wave ranges of
 // <= kSelRegs x 16 tiles (tables up to ~134 M rows), <= kLookbackBlocks blocks.
-template <int K, bool DEL, int U, int TQ, int NW, int NR, bool IR = false>
+template <int K, bool DEL, int U, int TQ, int NW, int NR, int IR = 0>
 __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* __restrict__ lb, int64_t row_offset,
                                                          int64_t* __restrict__ ids, int64_t* __restrict__ total,
                                                          int64_t* __restrict__ stamps, int32_t dbg) {
@@ -2119,8 +2174,17 @@ static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   const unsigned lds = L.sink_lds ? (unsigned)(L.tiles_per_block * kWordsPerTile * sizeof(uint64_t)) : 0u;
   // int literal terms as branch-free range tests
   if constexpr (KS == 0) {
-    if (L.hoist_terms && L.int_range) {
-      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, TQ, RI, true>), grid, dim3(kBlock), lds, s, L);
+    if (L.hoist_terms && L.int_range == 1) {
+      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, TQ, RI, 1>), grid, dim3(kBlock), lds, s, L);
+      return;
+    }
+  }
+  // literal terms of any type as range tests over ordered keys, hoisted
+  // (COUNT / aggregate scans in the 4-rows-per-lane layout)
+  if constexpr (MODE != kModeBitmap && !RI) {
+    if (L.int_range == 2) {
+      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, kHoistTerms, RI, 2>), grid, dim3(kBlock), lds, s,
+                         L);
       return;
     }
   }
@@ -2359,13 +2423,13 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
   const int nr = wave_words <= 64 ? 1 : wave_words <= 128 ? 2 : wave_words <= 256 ? 4 : kSelRegs;
 #define MBX_SCAN_SELECT_NW(KK, UU, NW, NR)                                                                       \
   if (del && ir)                                                                                               \
-    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR, true>), dim3((unsigned)g), dim3(64 * NW), \
+    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR, 1>), dim3((unsigned)g), dim3(64 * NW), \
                        0, s, L, lb, row_offset, ids, total, stamps, dbg);                                      \
   else if (del)                                                                                                \
     hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \
                        s, L, lb, row_offset, ids, total, stamps, dbg);                                         \
   else if (ir)                                                                                                 \
-    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR, true>), dim3((unsigned)g),            \
+    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR, 1>), dim3((unsigned)g),            \
                        dim3(64 * NW), 0, s, L, lb, row_offset, ids, total, stamps, dbg);                       \
   else                                                                                                         \
     hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \

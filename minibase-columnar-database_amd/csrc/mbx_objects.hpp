@@ -45,7 +45,8 @@ struct MbxTuning {
   int64_t tiles_per_block = -1;   // MBX_TILES_PER_BLOCK: segment size of every scan / BitSet
   int32_t force_generic = 0;      // MBX_FORCE_GENERIC: plans compiled after this use k_scan_generic
   int32_t scan_hoist = 1;         // MBX_SCAN_HOIST: 0 reads terms from the plan per tile
-  int32_t scan_int_range = 1;     // MBX_SCAN_INT_RANGE: int literal terms as branch-free range tests
+  int32_t scan_int_range = 2;     // MBX_SCAN_INT_RANGE: literal terms as branch-free range tests --
+                                  // 0 off, 1 int-only plans, 2 (default) also float / char(16) terms
   int32_t scan_ri = 1;            // MBX_SCAN_RI: 0 never, 1 BitSet output only, 2 always
   int32_t sink_lds = 1;           // MBX_SINK_LDS: 0 never, 1 segments >= 128 tiles, 2 whenever it fits
   int32_t ticket_groups = -1;     // MBX_TICKET_GROUPS

@@ -47,11 +47,11 @@ def _table(n=70_001, seed=17):
 def _count_both(m, ctx, t, cnf):
     """(range form, branchy form) COUNT of one CNF"""
     plan = ctx.compile(t, cnf)
-    ctx.set_tuning("scan_int_range", 1)
+    ctx.set_tuning("scan_int_range", 2)
     on = ctx.scan_count(plan)
     ctx.set_tuning("scan_int_range", 0)
     off = ctx.scan_count(plan)
-    ctx.set_tuning("scan_int_range", 1)
+    ctx.set_tuning("scan_int_range", 2)
     return on, off
 
 
@@ -71,7 +71,7 @@ def _all_outputs(m, ctx, t, ot, cnf, agg_col=2):
         assert got["count"] == agg_o["count"], (ir, cnf)
         if agg_o["count"]:  # empty selections: identities are representation details
             assert got == agg_o, (ir, cnf, got, agg_o)
-    ctx.set_tuning("scan_int_range", 1)
+    ctx.set_tuning("scan_int_range", 2)
 
 
 @pytest.mark.parametrize("op", [LT, LE, GT, GE, EQ, NE, NOP])
