@@ -228,13 +228,32 @@ def main():
     plan = ctx.compile(table, cnf)
 
     comm = None
+    torch_pg = None  # fallback exchange: torch.distributed's own RCCL group
     if exchange and not same_device:
         uid = m.mbx.comm_unique_id() if rank == 0 else None
         if world > 1:
             box = [uid]
             dist.broadcast_object_list(box, src=0)
             uid = box[0]
-        comm = ctx.comm_init_rank(world, rank, uid)
+        ok = 1
+        try:
+            comm = ctx.comm_init_rank(world, rank, uid)
+        except m.MbxError as err:
+            if world == 1:
+                raise
+            ok = 0
+            print(f"rank {rank}: libmbx RCCL communicator failed ({err})", file=sys.stderr)
+        if world > 1:
+            # every rank takes the same exchange: libmbx's communicator if it
+            # came up everywhere, else torch.distributed's RCCL group (eager)
+            flag = torch.tensor([ok], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag[0]) == 0:
+                if comm is not None:
+                    comm.close()
+                    comm = None
+                torch_pg = dist.new_group(backend="nccl")
+                print(f"rank {rank}: exchange falls back to torch.distributed (nccl = RCCL)", file=sys.stderr)
 
     # correctness gate before timing: the kernel's count vs a torch reduction
     # of the same device columns; with the exchange, the global count vs the
@@ -278,6 +297,8 @@ def main():
                 comm.allreduce_count_async(base + 8 * FW * j, FW * (je - j))
                 if xs_kernel:
                     comm.allreduce_agg_async(dummy.data_ptr())
+            elif torch_pg is not None:
+                dist.all_reduce(counts[j:je], group=torch_pg)
             elif exchange:  # same-device rehearsal: gloo over host copies
                 gloo_works.extend(range(j, je))
 
@@ -295,6 +316,8 @@ def main():
     # HIP graphs of G steps each (the timed region replays them); captured
     # after the warm-up, which sized every scratch buffer
     G = args.graph_steps if (args.graph_steps > 0 and not gloo_works and not (exchange and comm is None)) else 0
+    if torch_pg is not None:
+        G = 0
     graphs = []
     if G:
         try:
@@ -397,7 +420,8 @@ def main():
                  else "RCCL all-reduce of every step's COUNT (one collective per query; libmbx mbx_comm, right "
                       "after the step's scan on the same stream)")
                 if comm is not None else None) or (
-            "gloo all-reduce (same-device rehearsal)" if exchange else "none")
+            "torch.distributed RCCL all-reduce per step (fallback: libmbx's communicator failed)" if torch_pg is not None
+            else None) or ("gloo all-reduce (same-device rehearsal)" if exchange else "none")
         out = {
             "metric": METRIC,
             "value": total_rows / t_max,
