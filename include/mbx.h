@@ -201,11 +201,12 @@ int mbx_scan_blocks(mbx_ctx *ctx, const mbx_plan *p, int64_t *blocks);
 int mbx_scan_bitmap(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap **out, int64_t *count);
 int mbx_scan_bitmap_async(mbx_ctx *ctx, const mbx_plan *p, mbx_bitmap *out);
 /* the get_next_tid() stream as ascending positions (TID.position, global:
- * row_offset added; SURVEY 8(b) mbx_scan_select): two launches, the BitSet
- * scan and the compaction over its segment counts (DESIGN.md section 5 has
- * the one-launch forms measured and not kept).  host_ids holds up to cap
- * positions; their device scratch is sized to the count and released before
- * the call returns. */
+ * row_offset added; SURVEY 8(b) mbx_scan_select): ONE launch (k_scan_select:
+ * BitSet scan, decoupled look-back, positions) for plans of 1-4 int literal
+ * terms on <= 4 four-byte columns (knob scan_select_fused), else two
+ * launches, the BitSet scan and the compaction over its segment counts
+ * (DESIGN.md section 3).  host_ids holds up to cap positions; their device
+ * scratch is sized to the count and released before the call returns. */
 int mbx_scan_select(mbx_ctx *ctx, const mbx_plan *p, int64_t *host_ids, int64_t cap, int64_t *n);
 /* enqueue only: BitSet into `out` (nbits = the table's rows), positions into
  * dev_ids (capacity: the selected rows, at most the table's rows), the count
