@@ -989,7 +989,8 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
       ints = ints && p->host.terms[i].kind == kInt;
       lits = lits && p->host.terms[i].rhs < 0;
     }
-    if (lits && ints && !p->host.has_real && v.fast_ks == 0) L.int_range = 1;
+    if (lits && ints && !p->host.has_real && v.fast_ks == 0)
+      L.int_range = (tu.scan_int_range == 3 || tu.scan_int_range == 4) ? tu.scan_int_range : 1;  // 3 / 4: U A/B
     // typed range tests (float / char(16) terms too): COUNT and aggregate scans
     // of up to kHoistTerms terms, knob value 2 or more
     else if (lits && tu.scan_int_range >= 2 && mode != kModeBitmap && p->host.nterms <= kHoistTerms)

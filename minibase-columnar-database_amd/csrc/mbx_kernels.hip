@@ -2173,8 +2173,18 @@ static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   constexpr int kU = K == 1 && KS == 0 ? 4 : kDefaultU;
   const unsigned lds = L.sink_lds ? (unsigned)(L.tiles_per_block * kWordsPerTile * sizeof(uint64_t)) : 0u;
   // int literal terms as branch-free range tests
+  if constexpr (KS == 0 && K == 2 && MODE == kModeCount) {  // diagnostic: U = 3 / 4 tiles in flight (knob 3 / 4)
+    if (L.hoist_terms && L.int_range == 3) {
+      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, 3, kDefaultNT, TQ, RI, 1>), grid, dim3(kBlock), lds, s, L);
+      return;
+    }
+    if (L.hoist_terms && L.int_range == 4) {
+      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, 4, kDefaultNT, TQ, RI, 1>), grid, dim3(kBlock), lds, s, L);
+      return;
+    }
+  }
   if constexpr (KS == 0) {
-    if (L.hoist_terms && L.int_range == 1) {
+    if (L.hoist_terms && (L.int_range == 1 || L.int_range == 3 || L.int_range == 4)) {
       hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, TQ, RI, 1>), grid, dim3(kBlock), lds, s, L);
       return;
     }
