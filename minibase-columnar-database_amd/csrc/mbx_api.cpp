@@ -997,6 +997,13 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
       L.int_range = 2;
   }
   L.fin_mode = tu.fin_mode >= 0 ? tu.fin_mode : (mode != kModeAgg ? kFinPackedCount : kFinWriteThrough);
+  // aggregates over more blocks than the chip holds at once (string-slot
+  // plans, ~4096 blocks): each block's drained write-through partial and
+  // ticket round trip hold its slot from the next block, four rounds per
+  // slot -- plain partial stores and a separate fold launch instead (C5 125 M
+  // rows: scan 472.7 -> 458.4 us + a 6 us fold, query 481 -> 471 us,
+  // profiles/r03/c5fin)
+  if (tu.fin_mode < 0 && mode == kModeAgg && grid_blocks(L.nrows, tpb) > kResidentBlocks) L.fin_mode = kFinSeparate;
   if (L.fin_mode == kFinPackedCount && !packed_count_fits(L.nrows, grid_blocks(L.nrows, tpb), L.ticket_groups))
     L.fin_mode = kFinWriteThrough;
   if ((L.fin_mode == kFinPackedCount || L.fin_mode == kFinSegOnly) && mode == kModeAgg) L.fin_mode = kFinWriteThrough;

@@ -18,6 +18,7 @@
 
 namespace mbx {
 
+constexpr int64_t kResidentBlocks = 1024;  // 256-thread blocks the chip holds at once (4 per CU)
 constexpr int kHoistTerms = 4;        // literal terms the fast scan hoists into registers
 constexpr int kTileRows = 256;       // rows per wave tile
 constexpr int kWordsPerTile = 4;     // bitmap words per tile
