@@ -32,6 +32,15 @@ scanned by all ranks / max-over-ranks wall time.  stdout carries only the
 JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
+
+Launch: with WORLD_SIZE unset and --gpus N > 1, this process is only a
+launcher: before anything touches a GPU it starts N rank processes of this
+same script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+MASTER_PORT in their env), relays rank 0's JSON line and exits with the
+first failing rank's status (the others are then stopped by PID).  Under an
+external torch.distributed.run, WORLD_SIZE must equal --gpus.
+--dry-launch: the ranks print their rank env as JSON and exit before
+importing torch (the launcher's CPU test, tests/test_bench_launch.py).
 """
 import argparse
 import json
@@ -67,7 +76,7 @@ def cpu_baseline(rows, min_seconds):
     count1 = oracle.filescan_count(t, cnf)          # one single-thread pass, for the record
     one = time.perf_counter() - t0
     passes, elapsed, count = 0, 0.0, None
-    while elapsed < min_seconds and passes < 50:
+    while elapsed < min_seconds and passes < 5000:
         t0 = time.perf_counter()
         count = oracle.filescan_count_mt(t, cnf, threads)
         elapsed += time.perf_counter() - t0
@@ -84,18 +93,62 @@ def cpu_baseline(rows, min_seconds):
     }
 
 
-def load_traffic(rows):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary
-    (profiles/*_pmc.json, written by tools/pmc_summary.py), or None."""
+def load_traffic(rows, count_mode):
+    """HBM bytes per launch of the C3 scan over a `rows`-row shard with the
+    given COUNT form ("finalize" | "frame"), from the committed rocprofv3 PMC
+    summary (profiles/c3_scan_pmc.json: one entry per shard size bench.py
+    runs at N = 1, 2, 4, 8; written by tools/pmc_summary.py), or None."""
     path = os.path.join(ROOT, "profiles", "c3_scan_pmc.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("rows") == rows:
-            return d.get("hbm_bytes_per_launch")
+        e = d.get("shards", {}).get(f"{rows}:{count_mode}")
+        return (e or {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, dry):
+    """Start n rank processes of this script (one per GPU; none of this
+    process's code has touched a GPU), relay rank 0's stdout (every rank's
+    with --dry-launch) and return the exit status: 0, or the first failing
+    rank's status, after the remaining ranks were stopped by their PIDs."""
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = subprocess.PIPE if (r == 0 or dry) else sys.stderr
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, stdout=out))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench launcher: rank {procs.index(p)} exited with {rc}; stopping the others",
+                      file=sys.stderr)
+                for q in live:
+                    q.kill()
+        time.sleep(0.05)
+    for p in procs:
+        if p.stdout is not None:
+            data = p.stdout.read()
+            if data:
+                os.write(1, data)
+    return status
 
 
 def read_probe(ctx, table, ext, torch, reps=30):
@@ -181,12 +234,29 @@ def main():
                          "auto: frame with an exchange, finalize without")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="ranks print their rank env as JSON and exit before importing torch (launcher test)")
     args = ap.parse_args()
-    out_fd = quiet_stdout()
+    if args.gpus < 1:
+        print(f"bench: --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
+
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.dry_launch))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"bench: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_launch:
+        env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world, "gpus": args.gpus,
+                          "torch_imported": "torch" in sys.modules, "env": env}), flush=True)
+        return
+    out_fd = quiet_stdout()
 
     import torch
     import torch.distributed as dist
@@ -268,6 +338,21 @@ def main():
     # no-return atomics and the all-reduce sums whole frames -- the launch ends
     # without the finalize's dependent atomic round trips
     frames = args.count == "frame" or (args.count == "auto" and exchange)
+    if frames:
+        # a frame slot's 12-bit arrival field sums every rank's arrivals: it
+        # must stay < 4096 (mbx_count_frame_fits); otherwise the in-launch
+        # finalize (one int64 per rank, summed exactly) is used
+        nb = ctx.scan_blocks(plan)
+        if world > 1:
+            tb = torch.tensor([nb], dtype=torch.int64)
+            dist.all_reduce(tb, op=dist.ReduceOp.MAX)
+            nb = int(tb[0])
+        if not m.mbx.count_frame_fits(nb, world):
+            if args.count == "frame":
+                raise SystemExit(f"bench: {world} ranks x {nb} blocks overflow a count frame")
+            frames = False
+            print(f"rank {rank}: {world} ranks x {nb} blocks overflow a count frame; in-launch finalize",
+                  file=sys.stderr)
     FW = m.mbx.COUNT_FRAME_WORDS if frames else 1
     counts = torch.zeros((steps + warmup, FW), dtype=torch.int64, device="cuda")
     ext = torch.cuda.ExternalStream(ctx.stream)
@@ -464,8 +549,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
-                "traffic": load_traffic(n),
-                "traffic_unit": "HBM bytes per launch (rocprofv3 PMC, profiles/c3_scan_pmc.json)",
+                "traffic": load_traffic(n, "frame" if frames else "finalize"),
+                "traffic_unit": "HBM bytes per launch of rank 0's shard scan (rocprofv3 PMC, "
+                                "profiles/c3_scan_pmc.json, same rows and COUNT form)",
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 # secondary denominator: the best read rate of the
@@ -476,7 +562,9 @@ def main():
             },
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if not args.no_cpu_baseline:
+            # rank 0, after the timed region, over rank 0's shard (the other
+            # ranks wait at the closing barrier)
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
         os.write(out_fd, (json.dumps(out) + "\n").encode())
 

@@ -195,6 +195,10 @@ int mbx_scan_count_async(mbx_ctx *ctx, const mbx_plan *p, int64_t *dev_count);
 #define MBX_COUNT_FRAME_WORDS 512
 int mbx_scan_count_frame_async(mbx_ctx *ctx, const mbx_plan *p, int64_t *dev_frame);
 int mbx_count_frame_decode(const int64_t *host_frame, int64_t *count, int64_t *nan_blocks, int64_t *arrivals);
+/* 1 when the frames of nranks ranks whose scans have at most nblocks blocks
+ * each sum exactly (every slot's summed arrivals and NaN blocks < 4096),
+ * else 0 (then combine in-launch-finalized counts instead) */
+int mbx_count_frame_fits(int64_t nblocks, int32_t nranks);
 /* blocks of this plan's COUNT launch (= the arrivals one frame records) */
 int mbx_scan_blocks(mbx_ctx *ctx, const mbx_plan *p, int64_t *blocks);
 /* the selection as a device BitSet (the get_next_tid() stream as positions) */

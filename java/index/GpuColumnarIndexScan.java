@@ -20,7 +20,8 @@ import iterator.TupleUtils;
 
 /**
  * Drop-in for ColumnarIndexScan (R/index/ColumnarIndexScan.java:79-330): same
- * constructor, getOutputPositions(), get_next() in nextSetBit order.
+ * constructors (the projecting one, :79-182, and the bitmap-only one BitMapQuery
+ * uses, :185-268), getOutputPositions(), get_next() in nextSetBit order.
  * Bitmap-index CNFs run as ONE kernel launch (Native.cnfCursorOpen,
  * k_cnf_select) over the value BitSets of every term -- OR within a
  * conjunct, AND across, AND NOT cf.md -- that also writes the positions and
@@ -41,7 +42,9 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
   private final AttrType[] outTypes;
   private final int[] outIdx, projTypes;
   private final short[] projSizes;
-  private final boolean fused;
+  private final boolean fused, projecting;
+  public FldSpec[] perm_mat;
+  private BitSet positions;                // getOutputPositions()'s BitSet, formed on first use
   private long[] ids;
   private Object[] batch;
   private int n, i;
@@ -50,8 +53,32 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
                               final String[] indNames, AttrType[] types, short[] str_sizes, int noInFlds,
                               int noOutFlds, int[] out_indexes, FldSpec[] outFlds, CondExpr[] selects,
                               final boolean indexOnly) throws Exception {
+    this(true, columnarFile, fldNums, indexTypes, indNames, types, str_sizes, noInFlds, noOutFlds, out_indexes,
+         outFlds, selects, indexOnly);
+  }
+
+  /**
+   * The bitmap-only form (:185-268) BitMapQuery uses for getOutputPositions()
+   * (R/input/BitMapQuery.java:244,339): the CNF's BitSet, no projection.  As
+   * in the reference, get_next() fails on a selected row (its out_indexes is
+   * null, :292) with IndexException, and getTupleSize() with the
+   * NullPointerException of its null Jtuple.
+   */
+  public GpuColumnarIndexScan(Columnarfile columnarFile, final int[] fldNums, IndexType[] indexTypes,
+                              final String[] indNames, AttrType[] types, short[] str_sizes, int noInFlds,
+                              CondExpr[] selects) throws Exception {
+    this(false, columnarFile, fldNums, indexTypes, indNames, types, str_sizes, noInFlds, 0, null, null, selects,
+         false);
+  }
+
+  private GpuColumnarIndexScan(boolean projecting, Columnarfile columnarFile, int[] fldNums, IndexType[] indexTypes,
+                               String[] indNames, AttrType[] types, short[] str_sizes, int noInFlds, int noOutFlds,
+                               int[] out_indexes, FldSpec[] outFlds, CondExpr[] selects, boolean indexOnly)
+      throws Exception {
+    this.projecting = projecting;
     outTypes = new AttrType[noOutFlds];
-    TupleUtils.setup_op_tuple(Jtuple, outTypes, types, noInFlds, str_sizes, outFlds, noOutFlds);
+    if (projecting) TupleUtils.setup_op_tuple(Jtuple, outTypes, types, noInFlds, str_sizes, outFlds, noOutFlds);
+    perm_mat = outFlds;
     ctx = GpuContext.ctx();
     table = GpuTables.get(columnarFile.get_fileName());
     nbits = tableRows(table);
@@ -78,18 +105,22 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
       for (int k = 0; k < cnfOffsets.length; k++) cnfOffsets[k] = offs.get(k);
       deleted = Native.bitmapUpload(ctx, nbits, columnarFile.getMarkedDeleted().getBitSet().toLongArray());
       try {
-        // CNF + positions + projected rows: one kernel, any CNF shape
-        cursor = Native.cnfCursorOpen(ctx, table, cnfBitmaps, cnfOffsets, deleted, outIdx);
+        if (projecting)   // CNF + positions + projected rows: one kernel, any CNF shape
+          cursor = Native.cnfCursorOpen(ctx, table, cnfBitmaps, cnfOffsets, deleted, outIdx);
+        else              // the BitSet alone: one k_bitmap_cnf launch
+          output = Native.bitmapCnf(ctx, nbits, cnfBitmaps, cnfOffsets, deleted);
       } catch (Exception e) {
         close();
         throw e;
       }
     } else {
-      ColumnarIndexScan ref = new ColumnarIndexScan(columnarFile, fldNums, indexTypes, indNames, types, str_sizes,
-                                                    noInFlds, noOutFlds, out_indexes, outFlds, selects, indexOnly);
+      ColumnarIndexScan ref = projecting
+          ? new ColumnarIndexScan(columnarFile, fldNums, indexTypes, indNames, types, str_sizes, noInFlds, noOutFlds,
+                                  out_indexes, outFlds, selects, indexOnly)
+          : new ColumnarIndexScan(columnarFile, fldNums, indexTypes, indNames, types, str_sizes, noInFlds, selects);
       output = Native.bitmapUpload(ctx, nbits, ref.getOutputPositions().toLongArray());
       ref.close();
-      cursor = Native.cursorOpen(ctx, table, output, outIdx);
+      if (projecting) cursor = Native.cursorOpen(ctx, table, output, outIdx);
     }
   }
 
@@ -120,8 +151,18 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
     return true;
   }
 
-  public BitSet getOutputPositions() throws Exception {
-    return BitSet.valueOf(Native.bitmapDownload(ctx, gpuSelection()));                       // (:270)
+  /** the CNF's BitSet (:270-272): the same object on every call, as the reference's outputPositions */
+  public BitSet getOutputPositions() {
+    if (positions == null) {
+      try {
+        positions = BitSet.valueOf(Native.bitmapDownload(ctx, gpuSelection()));
+      } catch (Exception e) {
+        // the reference's getOutputPositions() declares no checked exception: a
+        // device failure here surfaces unchecked, carrying mbx_last_error()
+        throw new IllegalStateException("GPU ColumnarIndexScan: " + e.getMessage(), e);
+      }
+    }
+    return positions;
   }
 
   public long gpuSelection() throws Exception {
@@ -138,6 +179,14 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
   }
 
   public Tuple get_next() throws Exception {
+    if (!projecting) {
+      // the reference's bitmap-only form walks a null out_indexes at the
+      // first remaining position (:287-307); a scan with none returns null
+      if (cursor == 0) cursor = Native.cursorOpen(ctx, table, gpuSelection(), outIdx);
+      if (Native.cursorCount(cursor) > 0)
+        throw new IndexException(new NullPointerException("outIndexes"), "IndexScan.java: Heapfile error");
+      return null;
+    }
     if (i == n) {
       Object[] r = Native.cursorNext(cursor, 65536, projTypes, projSizes);
       if (r == null) return null;
@@ -175,7 +224,7 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
 
   public void restart() throws iterator.FileScanException {
     try {
-      Native.cursorRestart(cursor);
+      if (cursor != 0) Native.cursorRestart(cursor);                    // currentBitMapPos = 0 (:321-323)
     } catch (Exception e) {
       throw new iterator.FileScanException(e, "restart failed");
     }
@@ -183,6 +232,7 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
   }
 
   public int getTupleSize() {
+    if (!projecting) throw new NullPointerException("ColumnarIndexScan: the bitmap-only form has no Jtuple");
     return Jtuple.size();
   }
 }

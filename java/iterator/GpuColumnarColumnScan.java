@@ -10,7 +10,7 @@ import heap.Tuple;
 
 /**
  * Drop-in for ColumnarColumnScan (R/iterator/ColumnarColumnScan.java:39-211):
- * same constructor, get_next / get_next_tid / close contract.  The CondExpr's
+ * same constructors (projecting and delete-query), get_next / get_next_tid / close contract.  The CondExpr's
  * field 1 is column colNo (the reference evaluates PredEval on a one-field
  * tuple of that column, :55-77), so the CNF is compiled against the staged
  * table with field 1 renumbered to colNo + 1; the predicate, the deleted-row
@@ -27,6 +27,8 @@ public class GpuColumnarColumnScan extends Iterator implements GpuSelection {
   private long selection, cursor;
   private final Tuple Jtuple = new Tuple();
   private final int fieldCount;
+  private final boolean deleteQuery;
+  public FldSpec[] perm_mat;
   private final int[] outIdx, projTypes;
   private final short[] projSizes;
   private long[] ids;
@@ -35,11 +37,30 @@ public class GpuColumnarColumnScan extends Iterator implements GpuSelection {
 
   public GpuColumnarColumnScan(Columnarfile columnarfile, int colNo, int n_out_flds, int[] out_indexes,
                                FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
+    this(false, columnarfile, colNo, n_out_flds, out_indexes, proj_list, outFilter);
+  }
+
+  /**
+   * The delete-query form (:91-132): no projection, for get_next_tid()
+   * (DeleteQuery -> markTupleDeleted).  Its get_next() on a selected row
+   * fails with the NullPointerException the reference's null outIndexes
+   * raises (:166).
+   */
+  public GpuColumnarColumnScan(Columnarfile columnarfile, int colNo, CondExpr[] outFilter) throws Exception {
+    this(true, columnarfile, colNo, 0, null, null, outFilter);
+  }
+
+  private GpuColumnarColumnScan(boolean deleteQuery, Columnarfile columnarfile, int colNo, int n_out_flds,
+                                int[] out_indexes, FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
+    this.deleteQuery = deleteQuery;
     AttrType[] in1 = columnarfile.getAttributeTypes();
     fieldCount = columnarfile.getFieldCount();
-    AttrType[] jtypes = new AttrType[n_out_flds];
-    TupleUtils.setup_op_tuple(Jtuple, jtypes, in1, (short) fieldCount, columnarfile.getStringSizes(), proj_list,
-                              n_out_flds);
+    if (!deleteQuery) {
+      AttrType[] jtypes = new AttrType[n_out_flds];
+      TupleUtils.setup_op_tuple(Jtuple, jtypes, in1, (short) fieldCount, columnarfile.getStringSizes(), proj_list,
+                                n_out_flds);
+    }
+    perm_mat = proj_list;
     ctx = GpuContext.ctx();
     table = GpuTables.get(columnarfile.get_fileName());
     outIdx = new int[n_out_flds];
@@ -58,6 +79,11 @@ public class GpuColumnarColumnScan extends Iterator implements GpuSelection {
       close();
       throw new FileScanException(e, "GPU column scan failed");
     }
+  }
+
+  /** shows what input fields go where in the output tuple (:134-137) */
+  public FldSpec[] show() {
+    return perm_mat;
   }
 
   /** a copy of the CNF whose field-1 symbols name column colNo of the file */
@@ -90,6 +116,7 @@ public class GpuColumnarColumnScan extends Iterator implements GpuSelection {
 
   public Tuple get_next() throws Exception {
     if (!fill()) return null;
+    if (deleteQuery) throw new NullPointerException("ColumnarColumnScan: the delete-query form has no out_indexes");
     for (int k = 0; k < outIdx.length; k++) {
       switch (projTypes[k]) {
         case AttrType.attrInteger: Jtuple.setIntFld(k + 1, ((int[]) batch[k])[i]); break;
@@ -117,16 +144,12 @@ public class GpuColumnarColumnScan extends Iterator implements GpuSelection {
     }
   }
 
+  /** ColumnarColumnScan does not override Iterator.restart() (R/iterator/Iterator.java:134-136): a no-op */
   public void restart() throws FileScanException {
-    try {
-      Native.cursorRestart(cursor);
-    } catch (Exception e) {
-      throw new FileScanException(e, "restart failed");
-    }
-    n = i = 0;
   }
 
+  /** nor Iterator.getTupleSize() (:138-140): -1 */
   public int getTupleSize() {
-    return Jtuple.size();
+    return -1;
   }
 }

@@ -8,8 +8,8 @@ import global.TID;
 import heap.Tuple;
 
 /**
- * Drop-in for ColumnarFileScan (R/iterator/ColumnarFileScan.java:51-188): same
- * constructor, same get_next / get_next_tid / close / restart contract and
+ * Drop-in for ColumnarFileScan (R/iterator/ColumnarFileScan.java:51-216): same
+ * constructors (the projecting one and the delete-query one), same get_next / get_next_tid / close / restart contract and
  * the same shared Jtuple.  The predicate (PredEval over the CondExpr[]), the
  * deleted-row skip and the projection run as MI355X kernels; rows come back
  * in batches of BATCH through a device cursor, in position order.
@@ -27,15 +27,37 @@ public class GpuColumnarFileScan extends Iterator implements GpuSelection {
   private final int[] proj, projTypes;
   private final short[] projSizes;
   private final short len_in1;
+  private final boolean deleteQuery;
+  public FldSpec[] perm_mat;
   private long[] ids;
   private Object[] batch;
   private int n, i;
 
   public GpuColumnarFileScan(String file_name, AttrType[] in1, short[] s1_sizes, short len_in1, int n_out_flds,
                              FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
+    this(false, file_name, in1, s1_sizes, len_in1, n_out_flds, proj_list, outFilter);
+  }
+
+  /**
+   * The delete-query form (:101-135): no projection, for get_next_tid()
+   * (DeleteQuery -> markTupleDeleted).  As in the reference, it has no output
+   * tuple: get_next() on a selected row and getTupleSize() fail with the
+   * NullPointerException the reference's null Jtuple raises (:167, :214).
+   */
+  public GpuColumnarFileScan(String file_name, AttrType[] in1, short[] s1_sizes, short len_in1,
+                             CondExpr[] outFilter) throws Exception {
+    this(true, file_name, in1, s1_sizes, len_in1, 0, null, outFilter);
+  }
+
+  private GpuColumnarFileScan(boolean deleteQuery, String file_name, AttrType[] in1, short[] s1_sizes,
+                              short len_in1, int n_out_flds, FldSpec[] proj_list, CondExpr[] outFilter)
+      throws Exception {
+    this.deleteQuery = deleteQuery;
     this.len_in1 = len_in1;
     outTypes = new AttrType[n_out_flds];
-    TupleUtils.setup_op_tuple(Jtuple, outTypes, in1, len_in1, s1_sizes, proj_list, n_out_flds);  // :66-71
+    if (!deleteQuery)
+      TupleUtils.setup_op_tuple(Jtuple, outTypes, in1, len_in1, s1_sizes, proj_list, n_out_flds);  // :66-71
+    perm_mat = proj_list;
     ctx = GpuContext.ctx();
     table = GpuTables.get(file_name);
     // per-column char(n) sizes: s1_sizes lists the string columns' sizes in order
@@ -61,6 +83,11 @@ public class GpuColumnarFileScan extends Iterator implements GpuSelection {
     }
   }
 
+  /** shows what input fields go where in the output tuple (:139-142) */
+  public FldSpec[] show() {
+    return perm_mat;
+  }
+
   private boolean fill() throws Exception {
     if (i < n) return true;
     Object[] r = Native.cursorNext(cursor, BATCH, projTypes, projSizes);
@@ -74,6 +101,7 @@ public class GpuColumnarFileScan extends Iterator implements GpuSelection {
 
   public Tuple get_next() throws Exception {
     if (!fill()) return null;
+    if (deleteQuery) throw new NullPointerException("ColumnarFileScan: the delete-query form has no output tuple");
     for (int k = 0; k < outTypes.length; k++) {
       switch (outTypes[k].attrType) {
         case AttrType.attrInteger: Jtuple.setIntFld(k + 1, ((int[]) batch[k])[i]); break;
@@ -127,6 +155,7 @@ public class GpuColumnarFileScan extends Iterator implements GpuSelection {
   }
 
   public int getTupleSize() {
+    if (deleteQuery) throw new NullPointerException("ColumnarFileScan: the delete-query form has no output tuple");
     return Jtuple.size();
   }
 }

@@ -50,7 +50,8 @@ public class GpuColumnarNestedLoopJoins extends Iterator implements GlobalConst 
                                     int n_out_flds, int amt_of_mem) throws Exception {
     if (!(outerItr instanceof GpuSelection) || !(innerItr instanceof GpuSelection))
       throw new NestedLoopException("GpuColumnarNestedLoopJoins: outerItr / innerItr must be GPU scans "
-                                    + "(GpuColumnarFileScan, GpuColumnarColumnScan, GpuColumnarIndexScan)");
+                                    + "(GpuColumnarFileScan, GpuColumnarColumnScan, GpuColumnarColumnsScan, "
+                                    + "GpuColumnarIndexScan)");
     outerFile = outerColumnarFile;
     innerFile = innerColumnarFile;
     Jtypes = new AttrType[n_out_flds];

@@ -6,7 +6,7 @@ package iterator;
  * R/iterator/ColumnarNestedLoopJoins.java:48-66): the iterator's rows as a
  * device BitSet over its staged table, and which file column each field of
  * its output tuple holds.  Implemented by GpuColumnarFileScan,
- * GpuColumnarColumnScan and GpuColumnarIndexScan.
+ * GpuColumnarColumnScan, GpuColumnarColumnsScan and GpuColumnarIndexScan.
  */
 public interface GpuSelection {
   /** the staged table (mbx_table handle) the selection's positions index */

@@ -1125,6 +1125,12 @@ extern "C" int mbx_scan_count_frame_async(mbx_ctx* c, const mbx_plan* pc, int64_
                       true, true);
 }
 
+extern "C" int mbx_count_frame_fits(int64_t nblocks, int32_t nranks) {
+  if (nblocks < 0 || nranks <= 0) return 0;
+  const int64_t per_slot = (nblocks + kFrameSlots - 1) / kFrameSlots;
+  return per_slot <= kFrameMaxArrivalsPerSlot && per_slot * nranks < 4096 ? 1 : 0;
+}
+
 extern "C" int mbx_count_frame_decode(const int64_t* frame, int64_t* count, int64_t* nan_blocks, int64_t* arrivals) {
   NOTNULL(frame);
   NOTNULL(count);

@@ -921,8 +921,10 @@ void ColumnarColumnScan::close() {
     closeFlag = true;
   }
 }
-void ColumnarColumnScan::restart() { inner_->restart(); }
-int ColumnarColumnScan::getTupleSize() { return inner_->getTupleSize(); }
+// ColumnarColumnScan does not override Iterator.restart() / getTupleSize()
+// (R/iterator/Iterator.java:134-140): a no-op and -1
+void ColumnarColumnScan::restart() {}
+int ColumnarColumnScan::getTupleSize() { return -1; }
 
 }  // namespace iterator
 
@@ -1098,8 +1100,9 @@ void ColumnIndexScan::close() {
   rows_.close();
   closeFlag = true;
 }
-void ColumnIndexScan::restart() { rows_.restart(); }
-int ColumnIndexScan::getTupleSize() { return Jtuple_.size(); }
+// nor does ColumnIndexScan (R/index/ColumnIndexScan.java:28-740): Iterator's no-op and -1
+void ColumnIndexScan::restart() {}
+int ColumnIndexScan::getTupleSize() { return -1; }
 
 ColumnarIndexScan::ColumnarIndexScan(columnar::Columnarfile* cf, const std::vector<int>& fldNums,
                                      const std::vector<IndexType>& indexTypes,

@@ -82,6 +82,7 @@ EXPORTS = [
     "mbx_abi_version", "mbx_last_error", "mbx_device_count", "mbx_init", "mbx_free", "mbx_sync", "mbx_stream",
     "mbx_table_stage", "mbx_table_wrap", "mbx_table_free", "mbx_table_info", "mbx_plan_compile", "mbx_plan_free",
     "mbx_scan_count", "mbx_scan_count_async", "mbx_scan_count_frame_async", "mbx_count_frame_decode",
+    "mbx_count_frame_fits",
     "mbx_scan_blocks", "mbx_scan_bitmap", "mbx_scan_bitmap_async", "mbx_scan_select",
     "mbx_scan_select_async", "mbx_scan_aggregate",
     "mbx_scan_aggregate_async", "mbx_bitmap_alloc", "mbx_bitmap_upload", "mbx_bitmap_download", "mbx_bitmap_info",
@@ -147,6 +148,7 @@ def lib():
         "mbx_scan_count_async": ([V, V, V], ctypes.c_int),
         "mbx_scan_count_frame_async": ([V, V, V], ctypes.c_int),
         "mbx_count_frame_decode": ([V, P(I64), P(I64), P(I64)], ctypes.c_int),
+        "mbx_count_frame_fits": ([I64, ctypes.c_int32], ctypes.c_int),
         "mbx_scan_blocks": ([V, V, P(I64)], ctypes.c_int),
         "mbx_scan_bitmap": ([V, V, P(V), P(I64)], ctypes.c_int),
         "mbx_scan_bitmap_async": ([V, V, V], ctypes.c_int),
@@ -679,6 +681,11 @@ def count_frame_decode(frame):
     n, nan, arr = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     _chk(lib().mbx_count_frame_decode(f.ctypes.data, ctypes.byref(n), ctypes.byref(nan), ctypes.byref(arr)))
     return n.value, nan.value, arr.value
+
+
+def count_frame_fits(nblocks, nranks):
+    """mbx_count_frame_fits: nranks frames of <= nblocks-block scans sum exactly."""
+    return bool(lib().mbx_count_frame_fits(int(nblocks), int(nranks)))
 
 
 def comm_unique_id():

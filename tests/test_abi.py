@@ -78,22 +78,7 @@ def test_jni_glue_covers_the_java_side_and_calls_only_the_boundary():
     calls = set(re.findall(r"\b(mbx_[a-z_0-9]+)\s*\(", re.sub(r"/\*.*?\*/", "", glue, flags=re.S)))
     undeclared = sorted(calls - set(declared_functions()))
     assert not undeclared, undeclared
-    # the Java drop-ins keep the reference constructors' parameter lists
-    fs = open(os.path.join(root, "java", "iterator", "GpuColumnarFileScan.java")).read()
-    assert re.search(r"GpuColumnarFileScan\(String file_name, AttrType\[\] in1, short\[\] s1_sizes, short len_in1, "
-                     r"int n_out_flds,\s+FldSpec\[\] proj_list, CondExpr\[\] outFilter\)", fs)
-    # R/iterator/ColumnarColumnScan.java:39-45
-    cs = open(os.path.join(root, "java", "iterator", "GpuColumnarColumnScan.java")).read()
-    assert re.search(r"GpuColumnarColumnScan\(Columnarfile columnarfile, int colNo, int n_out_flds, int\[\] out_indexes,"
-                     r"\s+FldSpec\[\] proj_list, CondExpr\[\] outFilter\)", cs)
-    # R/iterator/ColumnarNestedLoopJoins.java:48-65
-    nl = open(os.path.join(root, "java", "iterator", "GpuColumnarNestedLoopJoins.java")).read()
-    sig = re.sub(r"\s+", " ", nl[nl.index("public GpuColumnarNestedLoopJoins("):nl.index("throws Exception {")])
-    assert sig.strip() == ("public GpuColumnarNestedLoopJoins(Columnarfile outerColumnarFile, Columnarfile "
-                           "innerColumnarFile, AttrType in1[], int in1_len, short[] t1_str_sizes, AttrType in2[], "
-                           "int in2_len, short[] t2_str_sizes, Iterator outerItr, Iterator innerItr, CondExpr[] "
-                           "outFilter, CondExpr[] rightFilter, CondExpr[] joinFilter, FldSpec[] proj_list, int "
-                           "n_out_flds, int amt_of_mem)")
+    # the drop-ins' constructor / method / field lists: tests/test_java_api.py
     # every native the Java drop-ins call is declared by Native.java
     called = set()
     for d, _, files in os.walk(os.path.join(root, "java")):

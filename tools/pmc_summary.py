@@ -7,7 +7,8 @@
                 reports half the bytes of a wide coalesced streaming read, so
                 hbm read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE * 1024 as is.
 
-usage: pmc_summary.py --kernel-substr k_scan_fast --rows N --out profiles/c3_scan_pmc.json DIR [DIR...]
+usage: pmc_summary.py --kernel-substr k_scan_fast --rows N --algo-bytes B --out F [--key ROWS:MODE] DIR [DIR...]
+  --key merges the summary into F["shards"][key] (bench.py load_traffic) instead of overwriting F.
 """
 import argparse
 import csv
@@ -33,6 +34,7 @@ def main():
     ap.add_argument("--rows", type=int, required=True)
     ap.add_argument("--algo-bytes", type=int, required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--key", default=None, help="ROWS:MODE entry of the shards map to write")
     args = ap.parse_args()
 
     kt = [r for r in rows_of(args.dirs, "kernel_trace.csv") if args.kernel_substr in r.get("Kernel_Name", "")]
@@ -59,8 +61,18 @@ def main():
         "traffic_over_algorithmic": (hbm / args.algo_bytes) if hbm else None,
         "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 FETCH_SIZE halves wide streaming reads)",
     }
+    if args.key:
+        try:
+            with open(args.out) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            doc = {}
+        doc.setdefault("shards", {})[args.key] = summary
+        summary_out = doc
+    else:
+        summary_out = summary
     with open(args.out, "w") as f:
-        json.dump(summary, f, indent=1)
+        json.dump(summary_out, f, indent=1)
     print(json.dumps(summary))
 
 
