@@ -30,7 +30,7 @@ public final class GpuShardedScan implements AutoCloseable {
   public GpuShardedScan(String columnarFile) throws Exception {
     final int n = GpuContext.devices();
     name = columnarFile;
-    db = GpuTables.dbHandle();                    // the buffer pool is flushed first
+    db = GpuTables.dbHandle();                    // dirty unpinned frames flushed first
     nrows = Native.dbColumnarRows(db, columnarFile);
     ctxs = new long[n];
     tables = new long[n];

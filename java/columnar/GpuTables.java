@@ -1,21 +1,36 @@
 package columnar;
 
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
+import java.util.BitSet;
 import java.util.HashMap;
 import java.util.IdentityHashMap;
 import java.util.Map;
 
 import bitmap.BitMapFile;
+import bufmgr.GpuFlush;
+import global.AttrType;
+import global.Convert;
 import global.GpuContext;
 import global.Native;
+import global.RID;
 import global.SystemDefs;
+import heap.Heapfile;
+import heap.Scan;
+import heap.Tuple;
 
 /**
  * HBM images of Columnarfiles and BitMapFiles, staged once per file and kept
  * until the file changes (tables are scanned many times, DESIGN.md section 2).
  * A Columnarfile is staged straight from the DB file (mbx_db_stage: pages ->
  * HBM -> GPU page decoder, the reference's positions kept, cf.md and holes
- * as deleted rows); the buffer pool is flushed first so the file on disk is
- * current.
+ * as deleted rows) after the dirty UNPINNED frames of the buffer pool were
+ * flushed one by one (bufmgr.GpuFlush; never flushAllPages, which throws
+ * PagePinnedException when a reference iterator holds a pin,
+ * R/bufmgr/BufMgr.java:349-400).  If a dirty frame is pinned, its bytes are not
+ * on disk yet: the Columnarfile is then lifted through the buffer pool
+ * instead (heap.Scan per column, decoded into direct ByteBuffers,
+ * Native.tableStage) -- the JVM's own view, pinned pages included.
  */
 public final class GpuTables {
   private static String dbPath;
@@ -34,25 +49,101 @@ public final class GpuTables {
     dbPath = path;
   }
 
+  private static int dirtyPinned;   // dirty frames the last flush had to leave in the pool
+
   private static long db() throws Exception {
     if (dbPath == null) throw new IllegalStateException("GpuTables.open(dbPath) first");
-    SystemDefs.JavabaseBM.flushAllPages();               // the pages the JVM still holds dirty
+    dirtyPinned = GpuFlush.flushUnpinned(SystemDefs.JavabaseBM);
     if (db == 0) db = Native.dbOpen(dbPath);
     return db;
   }
 
-  /** the DB file handle (buffer pool flushed first): sharded scans stage their row ranges from it */
+  /**
+   * The DB file handle (dirty unpinned frames flushed first): sharded scans
+   * stage their row ranges straight from it, so a dirty frame still pinned
+   * (an insert in progress) makes the file stale for them: FileScanException.
+   */
   public static synchronized long dbHandle() throws Exception {
-    return db();
+    long d = db();
+    if (dirtyPinned != 0)
+      throw new iterator.FileScanException(null, "GpuTables: " + dirtyPinned
+          + " dirty buffer frame(s) pinned; the DB file is not current for row-range staging");
+    return d;
   }
 
   public static synchronized long get(String columnarFile) throws Exception {
     Long t = tables.get(columnarFile);
     if (t == null) {
-      t = Native.dbStage(GpuContext.ctx(), db(), columnarFile);
+      long d = db();
+      t = dirtyPinned == 0 ? Native.dbStage(GpuContext.ctx(), d, columnarFile) : stageDecoded(columnarFile);
       tables.put(columnarFile, t);
     }
     return t;
+  }
+
+  /**
+   * A Columnarfile lifted through the buffer pool: every column heapfile
+   * walked with heap.Scan (R/heap/Scan.java:84-113), each record placed at its
+   * position (Heapfile.findPosition, R/heap/Heapfile.java:262-273) in a direct
+   * ByteBuffer in host order -- int / float as their 4 big-endian bytes read
+   * with Convert.getIntValue (R/global/Convert.java:18-37; a float keeps its
+   * bits), char(n) as the record's writeUTF payload zero-padded to n bytes.
+   * Positions some column lacks (holes) and cf.md's marks are deleted rows,
+   * as TupleScan skips them (R/columnar/TupleScan.java:55-89).
+   */
+  static long stageDecoded(String name) throws Exception {
+    Columnarfile f = new Columnarfile(name);
+    final AttrType[] types = f.getAttributeTypes();
+    final short[] sizes = f.getAttrSizes();
+    final int nc = f.getFieldCount();
+    final Heapfile[] hfs = f.getHeapfiles();
+    int nrows = 0;
+    for (int c = 0; c < nc; c++) {
+      Scan s = hfs[c].openScan();
+      RID rid = new RID();
+      try {
+        while (s.getNext(rid) != null) nrows = Math.max(nrows, hfs[c].findPosition(rid) + 1);
+      } finally {
+        s.closescan();
+      }
+    }
+    int[] t = new int[nc];
+    short[] w = new short[nc];
+    ByteBuffer[] cols = new ByteBuffer[nc];
+    BitSet present = new BitSet();
+    present.set(0, nrows);
+    for (int c = 0; c < nc; c++) {
+      t[c] = types[c].attrType;
+      w[c] = t[c] == AttrType.attrString ? sizes[c] : 4;
+      ByteBuffer b = ByteBuffer.allocateDirect(Math.max(1, nrows * w[c])).order(ByteOrder.nativeOrder());
+      BitSet have = new BitSet(nrows);
+      Scan s = hfs[c].openScan();
+      RID rid = new RID();
+      try {
+        Tuple tu;
+        while ((tu = s.getNext(rid)) != null) {
+          int p = hfs[c].findPosition(rid);
+          byte[] rec = tu.getTupleByteArray();
+          if (t[c] == AttrType.attrString) {
+            int len = ((rec[0] & 0xff) << 8) | (rec[1] & 0xff);
+            for (int k = 0; k < w[c]; k++) b.put(p * w[c] + k, k < len ? rec[2 + k] : 0);
+          } else {
+            b.putInt(p * 4, Convert.getIntValue(0, rec));
+          }
+          have.set(p);
+        }
+      } finally {
+        s.closescan();
+      }
+      present.and(have);
+      cols[c] = b;
+    }
+    BitSet deleted = (BitSet) f.getMarkedDeleted().getBitSet().clone();
+    BitSet holes = new BitSet();
+    holes.set(0, nrows);
+    holes.andNot(present);
+    deleted.or(holes);
+    return Native.tableStage(GpuContext.ctx(), t, w, nrows, cols, deleted.toLongArray(), 0);
   }
 
   /** a BitMapFile's BitSet on the device (uploaded from the engine's own copy) */
