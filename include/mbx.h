@@ -287,6 +287,14 @@ int mbx_cursor_open(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *sel, con
 int mbx_cursor_count(const mbx_cursor *c, int64_t *count);
 int mbx_cursor_next(mbx_cursor *c, int64_t max_rows, int64_t *host_ids, void *const *host_out,
                     int64_t *n);
+/* The same batch without a copy: *ids and cols[j] (an array of nproj
+ * pointers the caller provides) point into the cursor's pinned batch buffer
+ * -- positions, then each projected column in the mbx_materialize host
+ * layout -- valid until the next mbx_cursor_next / _next_view / _restart /
+ * _close on this cursor.  A batch crosses PCIe as one copy (packed on the
+ * device), so a caller that consumes rows in place (Iterator.get_next filling
+ * its Jtuple, the JNI glue filling int[] / String[]) touches each byte once. */
+int mbx_cursor_next_view(mbx_cursor *c, int64_t max_rows, const int64_t **ids, const void **cols, int64_t *n);
 int mbx_cursor_restart(mbx_cursor *c); /* Iterator.restart() */
 int mbx_cursor_close(mbx_cursor *c);   /* Iterator.close(), idempotent via free */
 /* Delivery is double buffered: mbx_cursor_next returns batch k from pinned

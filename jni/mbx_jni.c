@@ -703,11 +703,14 @@ static jobject column_array(JNIEnv *env, jint type, jshort size, const void *buf
       memcpy(tmp, (const char *)buf + r * size, (size_t)size);
       tmp[size] = 0;
       jstring js = (*env)->NewStringUTF(env, tmp);
+      if (!js) break; /* OutOfMemoryError pending */
       (*env)->SetObjectArrayElement(env, sa, (jsize)r, js);
       (*env)->DeleteLocalRef(env, js);
     }
     free(tmp);
-    col = sa;
+    col = sa && tmp && !(*env)->ExceptionCheck(env) ? sa : NULL;
+    if (sa && sa != col) (*env)->DeleteLocalRef(env, sa);
+    if (!col && !(*env)->ExceptionCheck(env)) throw_chain(env, kChain, "cursor rows: host allocation");
   }
   return col;
 }
@@ -715,7 +718,9 @@ static jobject column_array(JNIEnv *env, jint type, jshort size, const void *buf
 /* The next <= max_rows rows: {long[] positions, Object[] columns}, a column
  * per projected field as int[] / float[] / String[] (types / sizes: the
  * projected columns' AttrType and char(n) size); null at the end of the
- * stream (get_next() returning null). */
+ * stream (get_next() returning null).  The batch is read in place from the
+ * cursor's pinned buffer (mbx_cursor_next_view): one copy into the Java
+ * arrays, none in between. */
 JNIEXPORT jobjectArray JNICALL Java_global_Native_cursorNext(JNIEnv *env, jclass cls, jlong cur, jint max_rows,
                                                             jintArray types, jshortArray sizes) {
   (void)cls;
@@ -726,38 +731,33 @@ JNIEXPORT jobjectArray JNICALL Java_global_Native_cursorNext(JNIEnv *env, jclass
   }
   jint *t = np > 0 ? (*env)->GetIntArrayElements(env, types, NULL) : NULL;
   jshort *s = np > 0 ? (*env)->GetShortArrayElements(env, sizes, NULL) : NULL;
-  int64_t *ids = (int64_t *)malloc(sizeof(int64_t) * (size_t)max_rows);
-  void **bufs = (void **)calloc((size_t)(np > 0 ? np : 1), sizeof(void *));
-  int bad = !ids || !bufs || (np > 0 && (!t || !s));
-  for (jsize j = 0; !bad && j < np; j++) {
-    const size_t w = t[j] == MBX_ATTR_STRING ? (size_t)s[j] : 4;
-    bufs[j] = malloc(w * (size_t)max_rows);
-    bad = !bufs[j];
-  }
+  const void **bufs = (const void **)calloc((size_t)(np > 0 ? np : 1), sizeof(void *));
+  const int64_t *ids = NULL;
   jobjectArray res = NULL;
   int64_t n = 0;
-  if (bad) {
+  if (!bufs || (np > 0 && (!t || !s))) {
     throw_chain(env, kChain, "cursorNext: host allocation");
-  } else if (!check(env, mbx_cursor_next(P(mbx_cursor, cur), max_rows, ids, bufs, &n), kFileScan) && n > 0) {
+  } else if (!check(env, mbx_cursor_next_view(P(mbx_cursor, cur), max_rows, &ids, bufs, &n), kFileScan) && n > 0) {
     jclass objc = (*env)->FindClass(env, "java/lang/Object");
-    jclass strc = (*env)->FindClass(env, "java/lang/String");
-    jobjectArray cols = (*env)->NewObjectArray(env, np, objc, NULL);
-    jlongArray jids = (*env)->NewLongArray(env, (jsize)n);
+    jclass strc = objc ? (*env)->FindClass(env, "java/lang/String") : NULL;
+    jobjectArray cols = strc ? (*env)->NewObjectArray(env, np, objc, NULL) : NULL;
+    jlongArray jids = cols ? (*env)->NewLongArray(env, (jsize)n) : NULL;
     if (jids) (*env)->SetLongArrayRegion(env, jids, 0, (jsize)n, (const jlong *)ids);
-    for (jsize j = 0; cols && j < np; j++) {
+    for (jsize j = 0; jids && j < np; j++) {
       jobject col = column_array(env, t[j], s[j], bufs[j], n, strc);
+      if (!col) break;
       (*env)->SetObjectArrayElement(env, cols, j, col);
       (*env)->DeleteLocalRef(env, col);
     }
-    res = (*env)->NewObjectArray(env, 2, objc, NULL);
-    if (res) {
-      (*env)->SetObjectArrayElement(env, res, 0, jids);
-      (*env)->SetObjectArrayElement(env, res, 1, cols);
+    if (jids && !(*env)->ExceptionCheck(env)) {
+      res = (*env)->NewObjectArray(env, 2, objc, NULL);
+      if (res) {
+        (*env)->SetObjectArrayElement(env, res, 0, jids);
+        (*env)->SetObjectArrayElement(env, res, 1, cols);
+      }
     }
   }
-  for (jsize j = 0; bufs && j < np; j++) free(bufs[j]);
   free(bufs);
-  free(ids);
   if (t) (*env)->ReleaseIntArrayElements(env, types, t, JNI_ABORT);
   if (s) (*env)->ReleaseShortArrayElements(env, sizes, s, JNI_ABORT);
   return res;
@@ -1088,6 +1088,10 @@ JNIEXPORT jobjectArray JNICALL Java_global_Native_gather(JNIEnv *env, jclass cls
     out = objc ? (*env)->NewObjectArray(env, np, objc, NULL) : NULL;
     for (jsize j = 0; out && j < np; j++) {
       jobject col = column_array(env, t[j], s[j], bufs[j], n, strc);
+      if (!col) {
+        out = NULL;
+        break;
+      }
       (*env)->SetObjectArrayElement(env, out, j, col);
       (*env)->DeleteLocalRef(env, col);
     }

@@ -1782,19 +1782,44 @@ extern "C" int mbx_cursor_count(const mbx_cursor* kc, int64_t* count) {
   return MBX_OK;
 }
 
-// enqueue the device -> pinned copies of rows [from, from + n) into pin[b]
+// bytes per row of projected column j in the host layout (mbx_materialize's)
+static int64_t host_width(const mbx_cursor* k, size_t j) {
+  const TCol& tc = k->t->cols[(size_t)k->proj[j]];
+  return tc.attr_type == MBX_ATTR_STRING ? (int64_t)tc.size : 4;
+}
+
+static int64_t align16(int64_t v) { return (v + 15) & ~int64_t(15); }
+
+// host / staging layout of an n-row batch: n positions, then each projected
+// column's n rows, every part 16-byte aligned; returns the batch's bytes
+static int64_t batch_layout(const mbx_cursor* k, int64_t n, int64_t* off) {
+  int64_t o = align16(n * (int64_t)sizeof(int64_t));
+  for (size_t j = 0; j < k->outs.size(); j++) {
+    off[j] = o;
+    o = align16(o + n * host_width(k, j));
+  }
+  return o;
+}
+
+// enqueue rows [from, from + n) into pin[b]: one pack kernel into the device
+// staging region, one device -> pinned copy, one event
 static int cursor_fetch(mbx_cursor* k, int b, int64_t from, int64_t n) {
   mbx_ctx* c = k->ctx;
-  uint8_t* dst = k->pin[b];
-  HIPCHK(hipMemcpyAsync(dst, k->ids + from, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-  dst += (size_t)k->batch_rows * sizeof(int64_t);
-  int64_t bytes = n * (int64_t)sizeof(int64_t);
+  int64_t off[kMaxProj];
+  const int64_t bytes = batch_layout(k, n, off);
+  CursorPack P;
+  memset(&P, 0, sizeof(P));
+  P.ncols = (int32_t)k->outs.size();
   for (size_t j = 0; j < k->outs.size(); j++) {
-    const int64_t w = col_bytes(k->t, k->proj[j]);
-    HIPCHK(hipMemcpyAsync(dst, (uint8_t*)k->outs[j] + from * w, (size_t)(n * w), hipMemcpyDeviceToHost, c->stream));
-    dst += (size_t)(k->batch_rows * w);
-    bytes += n * w;
+    const TCol& tc = k->t->cols[(size_t)k->proj[j]];
+    P.col[j].src = (const uint8_t*)k->outs[j];
+    P.col[j].src_stride = tc.stride_w * 4;
+    P.col[j].width = (int32_t)host_width(k, j);
+    P.col[j].is_string = tc.attr_type == MBX_ATTR_STRING;
+    P.col[j].dst_off = off[j];
   }
+  HIPCHK(launch_cursor_pack(k->ids, from, n, P, k->stage, c->stream));
+  HIPCHK(hipMemcpyAsync(k->pin[b], k->stage, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipEventRecord(k->ev[b], c->stream));
   k->d2h_bytes += bytes;
   return MBX_OK;
@@ -1815,11 +1840,13 @@ static void cursor_release_pinned(mbx_cursor* k) {
     k->ev[b] = nullptr;
     k->pin[b] = nullptr;
   }
+  if (k->stage) hipFree(k->stage);
+  k->stage = nullptr;
   k->batch_rows = 0;
 }
 
-extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_ids, void* const* host_out,
-                               int64_t* n) {
+// the next <= max_rows rows as pointers into the pinned batch buffer
+static int cursor_next_view(mbx_cursor* k, int64_t max_rows, const int64_t** ids, const void** cols, int64_t* n) {
   NOTNULL(k);
   NOTNULL(n);
   *n = 0;
@@ -1830,23 +1857,26 @@ extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_id
   mbx_ctx* c = k->ctx;
   int rc = set_device(c);
   if (rc) return rc;
-  const mbx_table* t = k->t;
-  // pinned batch buffers, sized to the largest batch asked for so far
+  // pinned batch buffers + the device staging region, sized to the largest
+  // batch asked for so far
   const int64_t rows = max_rows < k->count ? max_rows : k->count;
   if (k->batch_rows < rows) {
     if ((rc = cursor_drain(k))) return rc;
     cursor_release_pinned(k);
-    int64_t row_bytes = (int64_t)sizeof(int64_t);
-    for (size_t j = 0; j < k->outs.size(); j++) row_bytes += col_bytes(t, k->proj[j]);
+    int64_t off[kMaxProj];
+    const int64_t bytes = batch_layout(k, rows, off);
     for (int b = 0; b < 2; b++) {
-      HIPCHK(hipHostMalloc((void**)&k->pin[b], (size_t)(rows * row_bytes), hipHostMallocDefault));
+      HIPCHK(hipHostMalloc((void**)&k->pin[b], (size_t)bytes, hipHostMallocDefault));
       HIPCHK(hipEventCreateWithFlags(&k->ev[b], hipEventDisableTiming));
     }
+    HIPCHK(hipMalloc((void**)&k->stage, (size_t)bytes));
     k->batch_rows = rows;
   }
   int b;
+  int64_t laid = take;  // rows the buffer's layout was packed for
   if (k->pf_start == k->next && k->pf_n >= take) {
-    b = k->pf_buf;  // this batch is already on its way
+    b = k->pf_buf;  // this batch is already on its way (perhaps with more rows)
+    laid = k->pf_n;
     k->pf_start = -1;
   } else {
     if ((rc = cursor_drain(k))) return rc;
@@ -1863,22 +1893,31 @@ extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_id
     k->pf_n = m;
     k->pf_buf = b ^ 1;
   }
-  const uint8_t* src = k->pin[b];
-  if (host_ids) memcpy(host_ids, src, (size_t)take * sizeof(int64_t));
-  src += (size_t)k->batch_rows * sizeof(int64_t);
-  for (size_t j = 0; j < k->outs.size(); j++) {
-    const TCol& tc = t->cols[(size_t)k->proj[j]];
-    const int64_t w = (int64_t)tc.stride_w * 4;
-    if (host_out && host_out[j]) {
-      if (tc.attr_type == MBX_ATTR_STRING)
-        unpack_rows(tc, src, take, host_out[j]);
-      else
-        memcpy(host_out[j], src, (size_t)(take * w));
-    }
-    src += (size_t)(k->batch_rows * w);
-  }
+  int64_t off[kMaxProj];
+  batch_layout(k, laid, off);
+  if (ids) *ids = (const int64_t*)k->pin[b];
+  for (size_t j = 0; cols && j < k->outs.size(); j++) cols[j] = k->pin[b] + off[j];
   k->next += take;
   *n = take;
+  return MBX_OK;
+}
+
+extern "C" int mbx_cursor_next_view(mbx_cursor* k, int64_t max_rows, const int64_t** ids, const void** cols,
+                                    int64_t* n) {
+  return cursor_next_view(k, max_rows, ids, cols, n);
+}
+
+extern "C" int mbx_cursor_next(mbx_cursor* k, int64_t max_rows, int64_t* host_ids, void* const* host_out,
+                               int64_t* n) {
+  NOTNULL(k);
+  const int64_t* vids = nullptr;
+  const void* vcols[kMaxProj];
+  if (k->outs.size() > (size_t)kMaxProj) return fail(MBX_E_UNSUPPORTED, "cursor_next: %zu columns", k->outs.size());
+  int rc = cursor_next_view(k, max_rows, &vids, vcols, n);
+  if (rc || *n == 0) return rc;
+  if (host_ids) memcpy(host_ids, vids, (size_t)*n * sizeof(int64_t));
+  for (size_t j = 0; host_out && j < k->outs.size(); j++)
+    if (host_out[j]) memcpy(host_out[j], vcols[j], (size_t)(*n * host_width(k, j)));
   return MBX_OK;
 }
 

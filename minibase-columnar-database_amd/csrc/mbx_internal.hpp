@@ -359,4 +359,23 @@ hipError_t launch_index_build(const KCol& col, int64_t nrows, const uint64_t* de
                               int32_t nvalues,
                               int32_t value_words, uint64_t* const* outs, int64_t words_per_block, hipStream_t s);
 
+// cursor delivery (mbx_cursor.hip): rows [from, from + n) of a cursor's
+// positions + projected columns packed into one staging region in the host
+// layout; column j at dst + col[j].dst_off, width bytes per row
+struct CursorPackCol {
+  const uint8_t* src;
+  int64_t dst_off;
+  int32_t src_stride;  // bytes per device row
+  int32_t width;       // bytes per host row (4, or n for char(n))
+  int32_t is_string;
+  int32_t pad_;
+};
+struct CursorPack {
+  CursorPackCol col[kMaxProj];
+  int32_t ncols;
+  int32_t pad_;
+};
+hipError_t launch_cursor_pack(const int64_t* ids, int64_t from, int64_t n, const CursorPack& P, uint8_t* dst,
+                              hipStream_t s);
+
 }  // namespace mbx

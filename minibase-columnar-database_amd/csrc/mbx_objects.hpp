@@ -143,8 +143,11 @@ struct mbx_cursor {
   std::vector<int32_t> proj;
   // double-buffered delivery (mbx_cursor_next): while the caller consumes
   // batch k, batch k+1 is already on its way into the other pinned buffer.
-  // A pinned batch = ids (batch_rows x 8 B), then each column's device rows.
+  // A batch is packed on the device (k_cursor_pack into `stage`) in the host
+  // layout -- positions, then each projected column, 16-byte aligned -- and
+  // crosses PCIe as ONE copy into pin[b].
   uint8_t* pin[2] = {nullptr, nullptr};
+  uint8_t* stage = nullptr;  // device staging region of one batch
   hipEvent_t ev[2] = {nullptr, nullptr};
   int64_t batch_rows = 0;   // rows a pinned buffer holds
   int64_t pf_start = -1;    // first row of the batch in flight into pin[pf_buf] (-1: none)

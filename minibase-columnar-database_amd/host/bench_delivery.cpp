@@ -84,32 +84,49 @@ Loop drain(It& it) {
   return r;
 }
 
-void emit(const char* cfg, const char* mode, int64_t nrows, double ctor_ms, const Loop& l, double batches_ms) {
+struct Batches {
+  int64_t rows;
+  double ms;
+  int64_t bytes;
+};
+
+void emit(const char* cfg, const char* mode, int64_t nrows, double ctor_ms, const Loop& l,
+          const std::vector<Batches>& bo) {
   printf("{\"config\": \"%s\", \"cursor\": \"%s\", \"table_rows\": %lld, \"rows_delivered\": %lld, "
          "\"ctor_ms\": %.3f, \"get_next_loop_ms\": %.3f, \"delivered_rows_per_s\": %.4g, \"ns_per_row\": %.2f, "
-         "\"cursor_batches_only_ms\": %.3f, \"checksum\": %lld}\n",
+         "\"checksum\": %lld, \"cursor_batches_only\": [",
          cfg, mode, (long long)nrows, (long long)l.rows, ctor_ms, l.ms, l.rows / (l.ms * 1e-3),
-         l.ms * 1e6 / (double)(l.rows > 0 ? l.rows : 1), batches_ms, (long long)l.checksum);
+         l.ms * 1e6 / (double)(l.rows > 0 ? l.rows : 1), (long long)l.checksum);
+  for (size_t i = 0; i < bo.size(); i++)
+    printf("%s{\"batch_rows\": %lld, \"ms\": %.3f, \"d2h_bytes\": %lld, \"gbs\": %.2f}", i ? ", " : "",
+           (long long)bo[i].rows, bo[i].ms, (long long)bo[i].bytes, bo[i].bytes / (bo[i].ms * 1e-3) / 1e9);
+  printf("]}\n");
   fflush(stdout);
 }
 
-// the cursor's batches alone (mbx_cursor_next into caller buffers, no
-// Jtuple fill): the part of the loop that is device -> host copy
-double batches_only(mbx_cursor* c, int ncols) {
-  std::vector<int64_t> ids(8192);
-  std::vector<std::vector<int32_t>> cols((size_t)ncols, std::vector<int32_t>(8192));
-  std::vector<void*> p((size_t)ncols);
-  for (int j = 0; j < ncols; j++) p[(size_t)j] = cols[(size_t)j].data();
-  mbx_cursor_restart(c);
-  const double t0 = now_ms();
-  int64_t n = 0;
-  do {
-    if (mbx_cursor_next(c, 8192, ids.data(), p.data(), &n) < 0) {
-      fprintf(stderr, "cursor_next: %s\n", mbx_last_error());
-      exit(1);
-    }
-  } while (n > 0);
-  return now_ms() - t0;
+// the cursor's batches alone (mbx_cursor_next_view, rows left in the pinned
+// buffer, no Jtuple fill): the part of the loop that is device -> host
+// delivery, at a few batch sizes; bytes = what crossed PCIe
+std::vector<Batches> batches_only(mbx_cursor* c) {
+  std::vector<Batches> out;
+  const void* cols[16];
+  for (int64_t rows : {8192, 65536, 65536, 262144, 262144}) {  // the first pass at a new size allocates
+    const int64_t* ids = nullptr;
+    int64_t n = 0, b0 = 0, b1 = 0, d = 0;
+    mbx_cursor_restart(c);
+    mbx_cursor_stats(c, &d, &b0);
+    const double t0 = now_ms();
+    do {
+      if (mbx_cursor_next_view(c, rows, &ids, cols, &n) < 0) {
+        fprintf(stderr, "cursor_next_view: %s\n", mbx_last_error());
+        exit(1);
+      }
+    } while (n > 0);
+    const double ms = now_ms() - t0;
+    mbx_cursor_stats(c, &d, &b1);
+    out.push_back({rows, ms, b1 - b0});
+  }
+  return out;
 }
 
 }  // namespace
@@ -162,7 +179,7 @@ int main(int argc, char** argv) {
           fprintf(stderr, "cursor_open: %s\n", mbx_last_error());
           return 1;
         }
-        const double bo2 = batches_only(c2cur, 4);
+        const auto bo2 = batches_only(c2cur);
         mbx_cursor_close(c2cur);
         fs.close();
         emit("C2", mode, n2, ctor2, l2, bo2);
@@ -203,7 +220,7 @@ int main(int argc, char** argv) {
           fprintf(stderr, "cnf_cursor_open: %s\n", mbx_last_error());
           return 1;
         }
-        const double bo = batches_only(cur, 2);
+        const auto bo = batches_only(cur);
         mbx_cursor_close(cur);
         is.close();
         emit("C4", mode, n4, ctor4, l4, bo);

@@ -588,10 +588,6 @@ CnfImage flatten(CondExpr* const* filter, int remap_from, int remap_to) {
 // ---- result batches shared by the scans: project `proj` columns of the
 // selection on the GPU, hand them out row by row
 
-struct Batch {
-  static constexpr int64_t kRows = CursorBatches::kRows;
-};
-
 static void setup_jtuple(heap::Tuple& J, const std::vector<AttrType>& in1, const std::vector<short>& s_sizes,
                          const std::vector<FldSpec>& proj) {
   // TupleUtils.setup_op_tuple (R/iterator/TupleUtils.java:295-341)
@@ -615,31 +611,6 @@ static int64_t col_width(const std::vector<AttrType>& types, const std::vector<s
   return types[(size_t)col].attrType == AttrType::attrString ? sizes[(size_t)col] : 4;
 }
 
-static void fill_row(heap::Tuple& J, const std::vector<AttrType>& types, const std::vector<short>& sizes,
-                     const std::vector<int32_t>& cols, const std::vector<std::vector<uint8_t>>& batch, int64_t i) {
-  for (size_t j = 0; j < cols.size(); j++) {
-    const int c = cols[j];
-    const int64_t w = col_width(types, sizes, c);
-    const uint8_t* p = batch[j].data() + i * w;
-    switch (types[(size_t)c].attrType) {
-      case AttrType::attrInteger: {
-        int32_t v;
-        memcpy(&v, p, 4);
-        J.setIntFld((int)j + 1, v);
-        break;
-      }
-      case AttrType::attrReal: {
-        float v;
-        memcpy(&v, p, 4);
-        J.setFloFld((int)j + 1, v);
-        break;
-      }
-      default:
-        J.setStrFld((int)j + 1, std::string((const char*)p, strnlen((const char*)p, (size_t)w)));
-    }
-  }
-}
-
 void CursorBatches::reset(mbx_cursor* c, const std::vector<AttrType>& types, const std::vector<short>& sizes,
                           const std::vector<int32_t>& cols) {
   close();
@@ -647,15 +618,14 @@ void CursorBatches::reset(mbx_cursor* c, const std::vector<AttrType>& types, con
   types_ = types;
   sizes_ = sizes;
   cols_ = cols;
-  batch_.assign(cols.size(), {});
   kind_.assign(cols.size(), 0);
   width_.assign(cols.size(), 0);
   for (size_t j = 0; j < cols.size(); j++) {
     kind_[j] = types[(size_t)cols[j]].attrType;
     width_[j] = col_width(types, sizes, cols[j]);
-    batch_[j].resize((size_t)(kRows * width_[j]));
   }
-  ids_.assign((size_t)kRows, 0);
+  vcols_.assign(cols.size(), nullptr);
+  vids_ = nullptr;
   n_ = i_ = 0;
 }
 
@@ -668,9 +638,7 @@ int64_t CursorBatches::count() const {
 bool CursorBatches::next() {
   if (!cur_) return false;
   if (i_ >= n_) {
-    std::vector<void*> ptrs(cols_.size());
-    for (size_t j = 0; j < cols_.size(); j++) ptrs[j] = batch_[j].data();
-    chk<FileScanException>(mbx_cursor_next(cur_, kRows, ids_.data(), ptrs.data(), &n_), "get_next");
+    chk<FileScanException>(mbx_cursor_next_view(cur_, kRows, &vids_, vcols_.data(), &n_), "get_next");
     i_ = 0;
     if (n_ == 0) return false;
   }
@@ -681,7 +649,7 @@ bool CursorBatches::next() {
 void CursorBatches::fill(heap::Tuple& J) const {
   const int64_t i = i_ - 1;
   for (size_t j = 0; j < cols_.size(); j++) {
-    const uint8_t* p = batch_[j].data() + i * width_[j];
+    const uint8_t* p = (const uint8_t*)vcols_[j] + i * width_[j];
     switch (kind_[j]) {
       case AttrType::attrInteger: {
         int32_t v;
@@ -739,49 +707,33 @@ int64_t ColumnarFileScan::resultCount() const {
   return n;
 }
 
-void ColumnarFileScan::next_batch() {
-  mbx_ctx* c = global::SystemDefs::ctx();
-  if (!cur_)
-    chk<FileScanException>(mbx_cursor_open(c, f_.table(), sel_->get(), proj_cols_.data(), (int32_t)proj_cols_.size(),
-                                           &cur_),
-                           "ColumnarFileScan: materialise");
-  batch_.resize(proj_cols_.size());
-  std::vector<void*> ptrs(proj_cols_.size());
-  for (size_t j = 0; j < proj_cols_.size(); j++) {
-    batch_[j].resize((size_t)(Batch::kRows * col_width(types_, sizes_, proj_cols_[j])));
-    ptrs[j] = batch_[j].data();
-  }
-  batch_ids_.resize((size_t)Batch::kRows);
-  chk<FileScanException>(mbx_cursor_next(cur_, Batch::kRows, batch_ids_.data(), ptrs.data(), &batch_n_),
-                         "ColumnarFileScan: get_next");
-  batch_i_ = 0;
+void ColumnarFileScan::open_rows() {
+  mbx_cursor* cur = nullptr;
+  chk<FileScanException>(mbx_cursor_open(global::SystemDefs::ctx(), f_.table(), sel_->get(), proj_cols_.data(),
+                                         (int32_t)proj_cols_.size(), &cur),
+                         "ColumnarFileScan: materialise");
+  rows_.reset(cur, types_, sizes_, proj_cols_);
 }
 
 heap::Tuple* ColumnarFileScan::get_next() {
-  if (batch_i_ >= batch_n_) {
-    next_batch();
-    if (batch_n_ == 0) return nullptr;
-  }
-  fill_row(Jtuple_, types_, sizes_, proj_cols_, batch_, batch_i_);
-  batch_i_++;
+  if (!rows_.open()) open_rows();
+  if (!rows_.next()) return nullptr;
+  rows_.fill(Jtuple_);
   return &Jtuple_;
 }
 
 global::TID ColumnarFileScan::get_next_tid() {
   global::TID tid;
   tid.numRIDs = f_.getFieldCount();
-  if (batch_i_ >= batch_n_) {
-    next_batch();
-    if (batch_n_ == 0) return tid;  // position -1: end of scan (null in Java)
-  }
-  tid.position = batch_ids_[(size_t)batch_i_++];
+  if (!rows_.open()) open_rows();
+  if (!rows_.next()) return tid;  // position -1: end of scan (null in Java)
+  tid.position = rows_.position();
   return tid;
 }
 
 void ColumnarFileScan::close() {
   if (!closeFlag) {
-    if (cur_) mbx_cursor_close(cur_);
-    cur_ = nullptr;
+    rows_.close();
     sel_.reset();
     if (plan_) mbx_plan_free(plan_);
     plan_ = nullptr;
@@ -789,10 +741,7 @@ void ColumnarFileScan::close() {
   }
 }
 
-void ColumnarFileScan::restart() {
-  if (cur_) chk<FileScanException>(mbx_cursor_restart(cur_), "restart");
-  batch_n_ = batch_i_ = 0;
-}
+void ColumnarFileScan::restart() { rows_.restart(); }
 
 int ColumnarFileScan::getTupleSize() { return Jtuple_.size(); }
 

@@ -270,8 +270,7 @@ namespace iterator {
 // double-buffered delivery; fill() writes the current row into Jtuple.
 class CursorBatches {
  public:
-  // rows per batch: 64 Ki rows keep the per-batch copy calls (one per column
-  // + the positions) well below the per-row Jtuple fill (bench_delivery)
+  // rows per batch (one packed device -> pinned copy each, bench_delivery)
   static constexpr int64_t kRows = 65536;
   CursorBatches() = default;
   ~CursorBatches() { close(); }
@@ -283,7 +282,7 @@ class CursorBatches {
   bool open() const { return cur_ != nullptr; }
   int64_t count() const;
   bool next();                  // the next row; false at the end of the stream
-  int64_t position() const { return ids_[(size_t)i_ - 1]; }
+  int64_t position() const { return vids_[i_ - 1]; }
   void fill(heap::Tuple& J) const;
   void restart();
   void close();
@@ -295,8 +294,10 @@ class CursorBatches {
   std::vector<int32_t> cols_;
   std::vector<int> kind_;    // per projected column: its AttrType code
   std::vector<int64_t> width_;  // per projected column: bytes per row in the batch
-  std::vector<std::vector<uint8_t>> batch_;
-  std::vector<int64_t> ids_;
+  // the current batch in the cursor's pinned buffer (mbx_cursor_next_view:
+  // rows are read in place, valid until the next batch)
+  const int64_t* vids_ = nullptr;
+  std::vector<const void*> vcols_;
   int64_t n_ = 0, i_ = 0;
 };
 
@@ -315,21 +316,17 @@ class ColumnarFileScan : public Iterator {
   columnar::BitSetPtr selection() const { return sel_; }
 
  private:
-  void fill(int64_t row);
-  void next_batch();
+  void open_rows();
   columnar::Columnarfile f_;
   std::vector<AttrType> in1_;
   std::vector<FldSpec> perm_mat_;
   heap::Tuple Jtuple_;
   mbx_plan* plan_ = nullptr;
   columnar::BitSetPtr sel_;
-  mbx_cursor* cur_ = nullptr;
   std::vector<int32_t> proj_cols_;
   std::vector<AttrType> types_;  // the file's schema, read once (get_next runs per row)
   std::vector<short> sizes_;
-  std::vector<std::vector<uint8_t>> batch_;
-  std::vector<int64_t> batch_ids_;
-  int64_t batch_n_ = 0, batch_i_ = 0;
+  CursorBatches rows_;           // opened at the first get_next / get_next_tid
 };
 
 // R/iterator/ColumnarColumnsScan.java:39-257: a CNF over the tuple of the

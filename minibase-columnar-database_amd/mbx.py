@@ -88,7 +88,7 @@ EXPORTS = [
     "mbx_scan_aggregate_async", "mbx_bitmap_alloc", "mbx_bitmap_upload", "mbx_bitmap_download", "mbx_bitmap_info",
     "mbx_bitmap_free", "mbx_bitmap_combine", "mbx_bitmap_cnf", "mbx_bitmap_cnf_async", "mbx_cnf_materialize_async", "mbx_bitmap_index_build",
     "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
-    "mbx_cursor_next", "mbx_cursor_restart", "mbx_cursor_close", "mbx_cursor_stats", "mbx_cnf_cursor_open", "mbx_cnf_cursor_launch",
+    "mbx_cursor_next", "mbx_cursor_next_view", "mbx_cursor_restart", "mbx_cursor_close", "mbx_cursor_stats", "mbx_cnf_cursor_open", "mbx_cnf_cursor_launch",
     "mbx_probe_read", "mbx_set_tuning",
     "mbx_diag_select_stamps", "mbx_dev_alloc", "mbx_dev_free", "mbx_dev_download", "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
     "mbx_comm_info", "mbx_comm_wait", "mbx_comm_allreduce_count_async", "mbx_comm_scan_count_async",
@@ -172,6 +172,7 @@ def lib():
         "mbx_cursor_open": ([V, V, V, P(I32), I32, P(V)], ctypes.c_int),
         "mbx_cursor_count": ([V, P(I64)], ctypes.c_int),
         "mbx_cursor_next": ([V, I64, V, P(V), P(I64)], ctypes.c_int),
+        "mbx_cursor_next_view": ([V, I64, P(V), P(V), P(I64)], ctypes.c_int),
         "mbx_cursor_restart": ([V], ctypes.c_int),
         "mbx_cursor_close": ([V], ctypes.c_int),
         "mbx_cursor_stats": ([V, P(I64), P(I64)], ctypes.c_int),

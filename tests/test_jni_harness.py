@@ -367,7 +367,7 @@ def test_db_file_staging_equals_the_decoded_array_path(jvm, ctx, tmp_path):
             res.append((jvm.call("scanCount", I64, J(ctx), J(p)), list(oracle.words_to_positions(words_of(jvm, ctx, bm)))))
             jvm.call("bitmapFree", None, J(bm))
             jvm.call("planFree", None, J(p))
-        n_o, _, ids_o = oracle.filescan(oracle.Table(cols, deleted=words), cnf)
+        n_o, _, ids_o = oracle.filescan(oracle.Table(cols, deleted_words=words), cnf)
         assert res[0] == res[1] == (n_o, list(ids_o))
     with pytest.raises(JavaException) as e:
         jvm.call("dbStage", I64, J(ctx), J(dbh), (V, jvm.string("nosuchfile")))

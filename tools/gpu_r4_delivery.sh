@@ -1,0 +1,15 @@
+# Round 4: the packed one-copy cursor (k_cursor_pack + mbx_cursor_next_view):
+# the full GPU suite, then bench_delivery (C2 / C4 delivered rows through the
+# C++ drop-ins' get_next, batch-only copies at 8 Ki / 64 Ki / 256 Ki rows)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r4_delivery}
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+mkdir -p /tmp/mbx_delivery && rm -f /tmp/mbx_delivery/db
+timeout -k 10 420 minibase-columnar-database_amd/host/bench_delivery /tmp/mbx_delivery 10000000 100000000 3 > $OUT/delivery.jsonl 2> $OUT/delivery.err || { echo DELIVERY_FAIL; tail -20 $OUT/delivery.err; exit 1; }
+rm -rf /tmp/mbx_delivery
+cat $OUT/delivery.jsonl
+echo DELIVERY_OK

@@ -29,4 +29,6 @@ MBX_BENCH_SAME_DEVICE=1 timeout -k 10 300 python3 bench.py --gpus 2 --steps 20 -
 cat $OUT/bench_n2_same_device.json
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $OUT/bench_n1.json 2> $OUT/bench_n1.err || { echo N1_FAIL; tail -30 $OUT/bench_n1.err; exit 1; }
 cat $OUT/bench_n1.json
+timeout -k 10 600 python -u -m pytest tests/test_jni_harness.py tests/test_bench_launch.py -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_jni.log 2>&1 || { echo JNI_TESTS_FAIL; tail -40 $OUT/pytest_jni.log; exit 1; }
+tail -3 $OUT/pytest_jni.log
 echo R4_SHARD_PMC_OK
