@@ -168,6 +168,16 @@ int mbx_table_wrap(mbx_ctx *ctx, const mbx_col_desc *cols, int32_t ncols, int64_
                    int64_t row_offset, mbx_table **out);
 int mbx_table_free(mbx_table *t);
 int mbx_table_info(const mbx_table *t, int64_t *nrows, int64_t *row_offset, int32_t *ncols);
+/* Column group (no reference counterpart; a physical layout choice of the
+ * executor): a device-built, table-owned row-interleaved copy of 2..4 of the
+ * table's 4-byte columns (cols, 0-based; each column in at most one group).
+ * Late materialisation that projects grouped columns (mbx_cursor_open,
+ * mbx_materialize*, mbx_cnf_cursor_open, mbx_cnf_materialize_async with
+ * <= 4 four-byte columns) gathers them from the group, so one row's values
+ * share a line: fewer HBM lines for a sparse selection.  Results are
+ * identical; scans keep reading the columns.  Costs ncols x 4 bytes x nrows
+ * of HBM. */
+int mbx_table_group(mbx_ctx *ctx, mbx_table *t, const int32_t *cols, int32_t ncols);
 
 /* ---- predicates: PredEval.Eval over one tuple (R/iterator/PredEval.java:25-183),
  * compiled once for one table.  Type rules follow the reference: the

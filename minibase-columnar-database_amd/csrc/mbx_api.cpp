@@ -82,6 +82,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.force_generic = (int32_t)env_knob("MBX_FORCE_GENERIC", 0);
   t.scan_hoist = (int32_t)env_knob("MBX_SCAN_HOIST", 1);
   t.scan_int_range = (int32_t)env_knob("MBX_SCAN_INT_RANGE", 2);
+  if (t.scan_int_range < 0 || t.scan_int_range > 2) t.scan_int_range = 2;
   t.scan_ri = (int32_t)env_knob("MBX_SCAN_RI", 1);
   t.sink_lds = (int32_t)env_knob("MBX_SINK_LDS", 1);
   t.ticket_groups = (int32_t)env_knob("MBX_TICKET_GROUPS", -1);
@@ -89,6 +90,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.join_plain = (int32_t)env_knob("MBX_JOIN_PLAIN", 0);
   t.distinct_lds_probes = (int32_t)env_knob("MBX_DISTINCT_LDS_PROBES", -1);
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
+  if (((t.select_dbg & 3) | ((t.select_dbg >> 4) & 7)) & ~kDiagDbg) t.select_dbg = 0;  // A/B forms: -DMBX_DIAG
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
   t.cursor_prefetch = (int32_t)env_knob("MBX_CURSOR_PREFETCH", 1);
   t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 1);
@@ -279,14 +281,23 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   if (!strcmp(knob, "tiles_per_block")) t.tiles_per_block = value;
   else if (!strcmp(knob, "force_generic")) t.force_generic = v;
   else if (!strcmp(knob, "scan_hoist")) t.scan_hoist = v;
-  else if (!strcmp(knob, "scan_int_range")) t.scan_int_range = v;
+  else if (!strcmp(knob, "scan_int_range")) {
+    if (v < 0 || v > 2) return fail(MBX_E_INVALID, "mbx_set_tuning: scan_int_range %d (0, 1 or 2)", v);
+    t.scan_int_range = v;
+  }
   else if (!strcmp(knob, "scan_ri")) t.scan_ri = v;
   else if (!strcmp(knob, "sink_lds")) t.sink_lds = v;
   else if (!strcmp(knob, "ticket_groups")) t.ticket_groups = v;
   else if (!strcmp(knob, "fin_mode")) t.fin_mode = v;
   else if (!strcmp(knob, "join_plain")) t.join_plain = v;
   else if (!strcmp(knob, "distinct_lds_probes")) t.distinct_lds_probes = v;
-  else if (!strcmp(knob, "select_dbg")) t.select_dbg = v;
+  else if (!strcmp(knob, "select_dbg")) {
+    // k_select_ids takes bits 0-1, the one-launch selections bits 4-6: A/B
+    // forms a production build compiles out (kDiagDbg)
+    if (((v & 3) | ((v >> 4) & 7)) & ~kDiagDbg)
+      return fail(MBX_E_UNSUPPORTED, "mbx_set_tuning: select_dbg %d needs a -DMBX_DIAG build", v);
+    t.select_dbg = v;
+  }
   else if (!strcmp(knob, "gather_fused")) t.gather_fused = v;
   else if (!strcmp(knob, "select_blocks")) t.select_blocks = v < 1 ? 1024 : (int32_t)v;
   else if (!strcmp(knob, "cursor_prefetch")) t.cursor_prefetch = v;
@@ -393,8 +404,50 @@ extern "C" int mbx_table_free(mbx_table* t) {
   hipStreamSynchronize(t->ctx->stream);
   for (auto& c : t->cols)
     if (c.owned) hipFree(c.dev);
+  for (auto& g : t->groups) hipFree(g.dev);
   if (t->owns_deleted) hipFree(t->deleted);
   delete t;
+  return MBX_OK;
+}
+
+// Column group: a row-interleaved copy of 2..4 four-byte columns (row r's
+// values side by side), built on the device and owned by the table.  The
+// narrow gathers of a late materialisation (k_select_ids<4>, k_cnf_select)
+// read a grouped column from the group, so the projected values of one row
+// share a 128-byte line: a sparse gather (1 % of rows) touches ~15 % of the
+// group's lines instead of ~28 % of every column's.
+extern "C" int mbx_table_group(mbx_ctx* c, mbx_table* t, const int32_t* cols, int32_t ncols) {
+  NOTNULL(c);
+  NOTNULL(t);
+  NOTNULL(cols);
+  if (ncols < 2 || ncols > 4) return fail(MBX_E_INVALID, "table_group: %d columns (2..4)", ncols);
+  if (c->capturing) return fail(MBX_E_INVALID, "table_group: inside a graph capture (it allocates)");
+  const uint32_t* src[4];
+  for (int32_t k = 0; k < ncols; k++) {
+    if (cols[k] < 0 || cols[k] >= (int32_t)t->cols.size())
+      return fail(MBX_E_RANGE, "table_group: column %d outside 0..%zu", cols[k], t->cols.size() - 1);
+    if (t->cols[(size_t)cols[k]].stride_w != 1)
+      return fail(MBX_E_INVALID, "table_group: column %d is not a 4-byte column", cols[k]);
+    for (int32_t j = 0; j < k; j++)
+      if (cols[j] == cols[k]) return fail(MBX_E_INVALID, "table_group: column %d twice", cols[k]);
+    for (const TGroup& g : t->groups)
+      for (int32_t gc : g.cols)
+        if (gc == cols[k]) return fail(MBX_E_INVALID, "table_group: column %d is already grouped", cols[k]);
+    src[k] = (const uint32_t*)t->cols[(size_t)cols[k]].dev;
+  }
+  int rc = set_device(c);
+  if (rc) return rc;
+  TGroup g;
+  g.cols.assign(cols, cols + ncols);
+  const size_t bytes = sizeof(uint32_t) * (size_t)ncols * (size_t)(t->nrows > 0 ? t->nrows : 1);
+  if (hipMalloc(&g.dev, bytes) != hipSuccess) return fail(MBX_E_NOMEM, "table_group: %zu bytes", bytes);
+  hipError_t e = launch_group_build(src, ncols, t->nrows, g.dev, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    hipFree(g.dev);
+    return fail(MBX_E_DEVICE, "table_group: %s", hipGetErrorString(e));
+  }
+  t->groups.push_back(g);
   return MBX_OK;
 }
 
@@ -990,7 +1043,7 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
       lits = lits && p->host.terms[i].rhs < 0;
     }
     if (lits && ints && !p->host.has_real && v.fast_ks == 0)
-      L.int_range = (tu.scan_int_range == 3 || tu.scan_int_range == 4) ? tu.scan_int_range : 1;  // 3 / 4: U A/B
+      L.int_range = 1;
     // typed range tests (float / char(16) terms too): COUNT and aggregate scans
     // of up to kHoistTerms terms, knob value 2 or more
     else if (lits && tu.scan_int_range >= 2 && mode != kModeBitmap && p->host.nterms <= kHoistTerms)
@@ -1195,12 +1248,14 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
                            int32_t nproj, int64_t row_offset, int64_t* dev_ids, void* const* dev_out,
                            int64_t* dev_total);
 
-// BitSet + ascending positions: the BitSet scan, then k_select_ids over its
-// segment counts.  One-launch forms measured slower: round F's (each block
-// summing the lower segments' counts) and round 2's decoupled look-back
-// (C2 10M rows 22-24 vs 19.8 us; 100M rows equal): polling predecessors
-// while the scan saturates HBM costs 2-11 us per block.
-// dev_ids holds every row's position.
+// BitSet + ascending positions.  Default (tuning scan_select_fused = 1): ONE
+// launch, k_scan_select -- the scan writes the BitSet words and each block
+// finds its output offset by decoupled look-back, then emits its positions --
+// for plans of 1..4 int literal terms on 4-byte columns whose segments fit
+// (scan_select_fusable).  Every other plan (float / string terms, symbol-vs-
+// symbol terms, scan_select_fused = 0) takes the two-launch form: the BitSet
+// scan, then k_select_ids over its segment counts.  dev_ids holds every row's
+// position.
 static int scan_select_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int64_t* dev_ids, int64_t* dev_count,
                             int32_t* dev_nan) {
   if (c->tune.scan_select_fused && b->nbits == p->t->nrows) {
@@ -1590,6 +1645,23 @@ int mbx::index_build_encoded(mbx_ctx* c, const mbx_table* t, int32_t col, const 
 
 // ---------------------------------------------------- late materialisation
 
+// a projected column as the gathers read it: its device rows, plus the
+// column group holding it (mbx_table_group) for the narrow 4-byte gathers
+static ProjCol proj_col(const mbx_table* t, int32_t col) {
+  ProjCol p;
+  const TCol& tc = t->cols[(size_t)col];
+  p.base = tc.dev;
+  p.stride_w = tc.stride_w;
+  for (const TGroup& g : t->groups)
+    for (size_t k = 0; k < g.cols.size(); k++)
+      if (g.cols[k] == col) {
+        p.gbase = g.dev + k;
+        p.gstride = (int32_t)g.cols.size();
+        return p;
+      }
+  return p;
+}
+
 static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel, const int32_t* proj,
                            int32_t nproj, int64_t row_offset, int64_t* dev_ids, void* const* dev_out,
                            int64_t* dev_total) {
@@ -1600,9 +1672,7 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
     if (!t) return fail(MBX_E_INVALID, "materialize: projection without a table");
     if (proj[j] < 0 || proj[j] >= (int32_t)t->cols.size())
       return fail(MBX_E_RANGE, "materialize: column %d outside 0..%zu", proj[j], t->cols.size() - 1);
-    pc[j].base = t->cols[(size_t)proj[j]].dev;
-    pc[j].stride_w = t->cols[(size_t)proj[j]].stride_w;
-    pc[j].pad_ = 0;
+    pc[j] = proj_col(t, proj[j]);
   }
   if (t && sel->nbits != t->nrows) return fail(MBX_E_INVALID, "materialize: bitmap/table size mismatch");
   if (!dev_total) dev_total = c->dcount + 1;
@@ -1643,9 +1713,8 @@ static int cnf_proj_args(const mbx_table* t, const int32_t* proj, int32_t nproj,
       return fail(MBX_E_RANGE, "cnf_materialize: column %d outside 0..%zu", proj[j], t->cols.size() - 1);
     const TCol& tc = t->cols[(size_t)proj[j]];
     if (!dev_out[j]) return fail(MBX_E_INVALID, "cnf_materialize: dev_out[%d] null", j);
-    pc[j].base = tc.dev;
-    pc[j].stride_w = tc.stride_w;
-    pc[j].pad_ = 0;
+    (void)tc;
+    pc[j] = proj_col(t, proj[j]);
   }
   return MBX_OK;
 }
@@ -2001,13 +2070,11 @@ extern "C" int mbx_cnf_cursor_launch(mbx_ctx* c, const mbx_table* t, const mbx_b
   }
   ProjCol pc[kMaxProj];
   for (int32_t j = 0; j < nproj; j++) {
-    pc[j].base = t->cols[(size_t)proj[j]].dev;
-    pc[j].stride_w = t->cols[(size_t)proj[j]].stride_w;
-    pc[j].pad_ = 0;
+    pc[j] = proj_col(t, proj[j]);
   }
   e = launch_cnf_materialize(C, deleted ? deleted->words : nullptr, (t->nrows + 63) >> 6, t->nrows, c->lookback,
                              t->row_offset, k->ids, pc, k->outs.data(), nproj, k->dcount, c->stream, nullptr,
-                             c->tune.select_dbg >> 4);
+                             c->tune.select_dbg >> 4, bound);
   if (e != hipSuccess) {
     mbx_cursor_close(k);
     return fail(MBX_E_DEVICE, "cnf_cursor: %s", hipGetErrorString(e));

@@ -30,6 +30,17 @@ constexpr int kMaxStrWords = 64;     // 256-byte strings
 constexpr int kMaxPoolWords = 512;
 constexpr int kMaxBitmaps = 64;      // bitmaps in one CNF launch
 constexpr int kMaxProj = 16;
+// select_dbg kernel bits that exist only for A/B measurements: skip the
+// prefix loads / the look-back wait (wrong output by design), skip the
+// emission, the back-off and plain-load poll forms.  A production build
+// compiles them out (the kernels mask dbg with kDiagDbg); -DMBX_DIAG keeps
+// them.  Stamps, the write-through flip and the every-predecessor look-back
+// (tables of >= 2^32 rows take it) stay in every build.
+#ifdef MBX_DIAG
+constexpr int32_t kDiagDbg = ~0;
+#else
+constexpr int32_t kDiagDbg = ~(1 | 2 | 4);
+#endif
 
 enum ColKind : int32_t { kInt = 0, kReal = 1, kStr = 2 };
 
@@ -188,7 +199,8 @@ constexpr int kFrameSlotStride = 16;  // int64 words per slot line
 struct ProjCol {
   const void* base;
   int32_t stride_w;
-  int32_t pad_;
+  int32_t gstride = 0;           // > 0: a 4-byte column also in a column group (mbx_table_group):
+  const void* gbase = nullptr;   // its value of row r at ((const uint32_t*)gbase)[r * gstride]
 };
 
 struct BitmapCnf {
@@ -324,7 +336,8 @@ hipError_t launch_finalize(const Partial* partials, int64_t nblocks, int32_t agg
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
-                                  int64_t* stamps = nullptr, int32_t dbg = 0);
+                                  int64_t* stamps = nullptr, int32_t dbg = 0,
+                                  int64_t cap = INT64_MAX);
 constexpr int64_t kLookbackWords = 1 + 2 * 1024;  // epoch, per-block counts, per-block inclusive prefixes
 // BitSet + positions + COUNT of a plan in one launch (k_scan_select): plans of
 // 1..4 int literal terms on 4-byte columns, tables whose segments fit the
@@ -375,6 +388,9 @@ struct CursorPack {
   int32_t ncols;
   int32_t pad_;
 };
+// column group (mbx_table_group): out[r * ncols + k] = cols[k][r]
+hipError_t launch_group_build(const uint32_t* const* cols, int32_t ncols, int64_t nrows, uint32_t* out,
+                              hipStream_t s);
 hipError_t launch_cursor_pack(const int64_t* ids, int64_t from, int64_t n, const CursorPack& P, uint8_t* dst,
                               hipStream_t s);
 

@@ -541,7 +541,23 @@ struct Gather4 {
   const int32_t* col[4];
   uint32_t* out[4];
   int32_t n;  // projected columns (0: positions only)
+  int64_t cap = INT64_MAX;  // rows the outputs (and positions) hold
+  // words between rows of col[g]: 1 for a column, the group's width when the
+  // column is read from a column group (its row's projected values share a line)
+  int32_t stride[4] = {1, 1, 1, 1};
 };
+
+// the narrow gather's source of a projected 4-byte column: its column group
+// when it has one, else the column
+__device__ __host__ inline void gather4_source(Gather4& G, int g, const ProjCol& pc) {
+  if (pc.gstride > 0) {
+    G.col[g] = (const int32_t*)pc.gbase;
+    G.stride[g] = pc.gstride;
+  } else {
+    G.col[g] = (const int32_t*)pc.base;
+    G.stride[g] = 1;
+  }
+}
 
 // Any projection (ColumnarIndexScan's out_indexes with char(n) columns, or
 // more than 4 columns): template argument G4 == kWide.  Column g's rows are
@@ -553,6 +569,7 @@ struct GatherW {
   uint32_t* out[kMaxProj];
   int32_t sw[kMaxProj];
   int32_t n;
+  int64_t cap = INT64_MAX;  // rows the outputs (and positions) hold
 };
 
 // An output store of the compaction: plain, or write-through (`sc1`: the
@@ -617,8 +634,8 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
 #pragma unroll
         for (int g = 0; g < G4; ++g)
           if (g < G.n) {
-            v0[g] = (uint32_t)G.col[g][p0];
-            v1[g] = (uint32_t)G.col[g][p1];
+            v0[g] = (uint32_t)G.col[g][p0 * G.stride[g]];
+            v1[g] = (uint32_t)G.col[g][p1 * G.stride[g]];
           }
         if (ids) {
           put(&ids[off + i0], row_offset + p0, wt);
@@ -650,7 +667,7 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
         } else {
 #pragma unroll
           for (int g = 0; g < G4; ++g)
-            if (g < G.n) put(&G.out[g][o], (uint32_t)G.col[g][p], wt);
+            if (g < G.n) put(&G.out[g][o], (uint32_t)G.col[g][p * G.stride[g]], wt);
         }
       }
     }
@@ -1392,9 +1409,11 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
                                                        int64_t row_offset, int64_t* __restrict__ ids,
                                                        int64_t* __restrict__ total, int32_t dbg,
                                                        int64_t* __restrict__ stamps, Gather4 G) {
-  // dbg (diagnostic A/B, mbx_set_tuning "select_dbg"): bit 0 skips the
-  // prefix loads, bit 1 the emission; stamps: per block wall_clock64() at
-  // start / words + prefix in / after the block barrier / end
+  // dbg (diagnostic A/B, mbx_set_tuning "select_dbg"; -DMBX_DIAG builds
+  // only): bit 0 skips the prefix loads, bit 1 the emission; stamps: per
+  // block wall_clock64() at start / words + prefix in / after the block
+  // barrier / end
+  dbg &= kDiagDbg;
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
   __shared__ int64_t wcount[kWaves];
   __shared__ int64_t wpre[kWaves];
@@ -1586,6 +1605,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
                                             int32_t dbg, int64_t* __restrict__ segc, int64_t nseg, int64_t* wcount,
                                             int64_t* wpre, uint16_t (*stage)[32 * 64],
                                             uint64_t* __restrict__ words_out = nullptr) {
+  dbg &= kDiagDbg;  // bits 0-2: A/B poll forms, -DMBX_DIAG builds only
   int64_t* const inc = lb + 1 + kLookbackBlocks;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
   // wave 0 loads the look-back's first window (the 64 predecessors) BEFORE
   // this block stores its own flag: vmcnt counts loads and stores in issue
@@ -1644,7 +1664,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
           const int64_t p = a0 * 64 + st[i];
 #pragma unroll
           for (int g = 0; g < G4; ++g)
-            if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p];
+            if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p * G.stride[g]];
         }
       }
     }
@@ -1690,9 +1710,13 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       if (dbg & 8) inc[j] = epoch << 32;
     }
   }
+  // a block whose rows would end past the outputs' capacity writes none of
+  // them: the caller sees *total > cap and fails, with nothing out of bounds
+  const bool fits = off + bc <= G.cap;
   for (int k = 0; k < wave; ++k) off += wcount[k];
   const bool wt = (G4 == 0) != ((dbg & 32) != 0);
-  if (cached) {
+  if (!fits) {
+  } else if (cached) {
     // the prefetched rows, then the rest of the staged ones, then the steps
     // that did not fit the stage one by one
 #pragma unroll
@@ -2177,18 +2201,8 @@ static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   constexpr int kU = K == 1 && KS == 0 ? 4 : kDefaultU;
   const unsigned lds = L.sink_lds ? (unsigned)(L.tiles_per_block * kWordsPerTile * sizeof(uint64_t)) : 0u;
   // int literal terms as branch-free range tests
-  if constexpr (KS == 0 && K == 2 && MODE == kModeCount) {  // diagnostic: U = 3 / 4 tiles in flight (knob 3 / 4)
-    if (L.hoist_terms && L.int_range == 3) {
-      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, 3, kDefaultNT, TQ, RI, 1>), grid, dim3(kBlock), lds, s, L);
-      return;
-    }
-    if (L.hoist_terms && L.int_range == 4) {
-      hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, 4, kDefaultNT, TQ, RI, 1>), grid, dim3(kBlock), lds, s, L);
-      return;
-    }
-  }
   if constexpr (KS == 0) {
-    if (L.hoist_terms && (L.int_range == 1 || L.int_range == 3 || L.int_range == 4)) {
+    if (L.hoist_terms && L.int_range == 1) {
       hipLaunchKernelGGL((k_scan_fast<K, KS, MODE, DEL, kU, kDefaultNT, TQ, RI, 1>), grid, dim3(kBlock), lds, s, L);
       return;
     }
@@ -2330,7 +2344,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
   Gather4 G{};
   if (nproj > 0 && all4 && fuse_gather) {
     for (int j = 0; j < nproj; ++j) {
-      G.col[j] = (const int32_t*)proj[j].base;
+      gather4_source(G, j, proj[j]);
       G.out[j] = (uint32_t*)out[j];
     }
     G.n = nproj;
@@ -2358,7 +2372,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
-                                  int64_t* stamps, int32_t dbg) {
+                                  int64_t* stamps, int32_t dbg, int64_t cap) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   if (nproj < 0 || nproj > kMaxProj) return hipErrorInvalidValue;
   // <= 4 four-byte columns: values prefetched in registers (Gather4); any
@@ -2370,7 +2384,7 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   for (int j = 0; j < nproj; ++j) {
     if (proj[j].stride_w < 1) return hipErrorInvalidValue;
     if (narrow) {
-      G.col[j] = (const int32_t*)proj[j].base;
+      gather4_source(G, j, proj[j]);
       G.out[j] = (uint32_t*)out[j];
     }
     W.col[j] = (const uint32_t*)proj[j].base;
@@ -2379,6 +2393,7 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   }
   G.n = narrow ? nproj : 0;
   W.n = nproj;
+  G.cap = W.cap = cap;
   // <= kLookbackBlocks blocks: one poll load per thread per 256 predecessors
   const int64_t wpb = (nwords + kLookbackBlocks - 1) / kLookbackBlocks;
   const int64_t g = (nwords + wpb - 1) / wpb;

@@ -60,10 +60,10 @@ struct MbxTuning {
   int32_t scan_select_waves = 16; // MBX_SCAN_SELECT_WAVES: waves per k_scan_select block (4 or 16)
   int32_t scan_words_wt = 1;      // MBX_SCAN_WORDS_WT: BitSet scan words stored write-through
   int32_t comm_same_stream = 1;   // MBX_COMM_SAME_STREAM: collectives on the context stream (0: the exchange stream)
-  int32_t select_dbg = 0;         // MBX_SELECT_DBG: diagnostic k_select_ids variants (bit 0 no prefix,
-                                  // bit 1 no emission: wrong output), bit 3 per-block stamps, bits 4-5
-                                  // k_cnf_select look-back variants (16 back-off, 32 no wait: wrong output,
-                                  // 128 every-predecessor poll instead of the chained look-back)
+  int32_t select_dbg = 0;         // MBX_SELECT_DBG: bit 3 per-block stamps, 128 every-predecessor poll
+                                  // instead of the chained look-back, 512 write-through flip; -DMBX_DIAG
+                                  // builds only: k_select_ids bit 0 no prefix / bit 1 no emission, the
+                                  // one-launch selections' 16 back-off / 32 no wait / 64 plain-load polls
 };
 constexpr int64_t kMaxStampBlocks = 65536;
 
@@ -94,11 +94,18 @@ struct TCol {
   bool owned = false;
 };
 
+// a column group (mbx_table_group): row r of column cols[k] at dev[r * cols.size() + k]
+struct TGroup {
+  std::vector<int32_t> cols;
+  uint32_t* dev = nullptr;
+};
+
 struct mbx_table {
   mbx_ctx* ctx = nullptr;
   int64_t nrows = 0;
   int64_t row_offset = 0;
   std::vector<TCol> cols;
+  std::vector<TGroup> groups;  // owned
   uint64_t* deleted = nullptr;
   bool owns_deleted = false;
   bool aligned16 = true;

@@ -298,4 +298,37 @@ hipError_t launch_present_merge(const uint64_t* present0, const uint64_t* other,
   return hipGetLastError();
 }
 
+// Column group (mbx_table_group): out[r * ncols + k] = cols[k][r].  One
+// thread per row; loads coalesce per column, the row's stores are adjacent.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_group_build(const uint32_t* __restrict__ c0,
+                                                        const uint32_t* __restrict__ c1,
+                                                        const uint32_t* __restrict__ c2,
+                                                        const uint32_t* __restrict__ c3, int64_t nrows,
+                                                        uint32_t* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * kBlock) {
+    uint32_t* o = out + r * N;
+    o[0] = c0[r];
+    o[1] = c1[r];
+    if constexpr (N > 2) o[2] = c2[r];
+    if constexpr (N > 3) o[3] = c3[r];
+  }
+}
+
+hipError_t launch_group_build(const uint32_t* const* cols, int32_t ncols, int64_t nrows, uint32_t* out,
+                              hipStream_t s) {
+  if (nrows <= 0) return hipSuccess;
+  const int64_t want = (nrows + kBlock - 1) / kBlock;
+  const unsigned g = (unsigned)(want < 8192 ? want : 8192);
+  const uint32_t* c2 = ncols > 2 ? cols[2] : nullptr;
+  const uint32_t* c3 = ncols > 3 ? cols[3] : nullptr;
+  if (ncols == 2)
+    hipLaunchKernelGGL(k_group_build<2>, dim3(g), dim3(kBlock), 0, s, cols[0], cols[1], c2, c3, nrows, out);
+  else if (ncols == 3)
+    hipLaunchKernelGGL(k_group_build<3>, dim3(g), dim3(kBlock), 0, s, cols[0], cols[1], c2, c3, nrows, out);
+  else
+    hipLaunchKernelGGL(k_group_build<4>, dim3(g), dim3(kBlock), 0, s, cols[0], cols[1], c2, c3, nrows, out);
+  return hipGetLastError();
+}
+
 }  // namespace mbx

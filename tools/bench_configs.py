@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--c4-rows", type=int, default=100_000_000, help="global rows")
     ap.add_argument("--c4-positions", action="store_true",
                     help="C4 query also writes the selected positions (default: the projected rows only)")
+    ap.add_argument("--c4-group", action="store_true",
+                    help="C4: the projected c0, c1 also staged as a column group (mbx_table_group, 8-byte rows)")
     ap.add_argument("--c4-two-call", action="store_true",
                     help="C4 query as mbx_bitmap_cnf_async + mbx_materialize_async (default: one launch)")
     ap.add_argument("--c5-rows", default="125000000,1000000000", help="global rows, comma separated")
@@ -212,6 +214,8 @@ def main():
         bm2 = ctx.index_build(t, 2, [("int", v) for v in range(10)])
         bm3 = ctx.index_build(t, 3, [("int", v) for v in range(10)])
         a, b = bm2[3], bm3[7]
+        if args.c4_group:
+            ctx.group(t, [0, 1])
         out = ctx.bitmap_alloc(n)
         cap = max(1, n // 50)
         ids = torch.zeros(cap, dtype=torch.int64, device="cuda")
@@ -279,6 +283,7 @@ def main():
         byts = 2 * N / 8 + glob * 8 + (glob * 8 if mode != "projection" else 0) + (2 * N / 8 if mode == "two_call"
                                                                                     else 0)
         emit({"config": "C4", "rows": N, "gpus": world, "rows_per_gpu": n, "selected": glob,
+              "layout": "column group (c0, c1) for the gather" if args.c4_group else "columns",
               "ms_per_query": ms, "rows_per_s": N / ms * 1e3, "algorithmic_gbs": byts / ms / 1e6,
               "query": {"projection": "one launch (mbx_cnf_materialize_async): projected rows c0, c1",
                         "positions": "one launch (mbx_cnf_materialize_async): positions + c0, c1",
