@@ -102,7 +102,11 @@ public class GpuShardedColumnarIndexScan extends Iterator {
         mine.add(del);
         long[] h = new long[bms.size()];
         for (int k = 0; k < h.length; k++) h[k] = bms.get(k);
-        long[] r = Native.cnfCursorLaunch(ctx, s.table(g), h, offs, del, outIdx);   // all GPUs in flight
+        // launch only: the cursor's capacity bound comes from the slices' counts,
+        // which Native.dbBitmapStageRange fixed at staging (mbx_bitmap_upload
+        // counts every upload), so no shard waits for its launch before the
+        // next shard's is enqueued -- all GPUs in flight
+        long[] r = Native.cnfCursorLaunch(ctx, s.table(g), h, offs, del, outIdx);
         cursors[g] = r[0];
         dcounts[g] = r[1];
       }
