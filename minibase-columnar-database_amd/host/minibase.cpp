@@ -180,42 +180,31 @@ namespace heap {
 
 void Tuple::setHdr(const std::vector<global::AttrType>& types, const std::vector<short>& str_sizes) {
   types_ = types;
+  kinds_.clear();
+  for (const auto& t : types) kinds_.push_back(t.attrType);
   str_sizes_ = str_sizes;
   ints_.assign(types.size(), 0);
   reals_.assign(types.size(), 0.0f);
   strs_.assign(types.size(), std::string());
 }
 
-void Tuple::check(int fldNo, int type) const {
+void Tuple::bad_field(int fldNo, int type) const {
   if (fldNo < 1 || fldNo > (int)types_.size())
     throw iterator::FieldNumberOutOfBoundException("Tuple: field number " + std::to_string(fldNo) + " out of bound");
-  if (types_[(size_t)fldNo - 1].attrType != type)
-    throw iterator::UnknowAttrType("Tuple: field " + std::to_string(fldNo) + " has another type");
-}
-
-int Tuple::getIntFld(int f) const {
-  check(f, global::AttrType::attrInteger);
-  return ints_[(size_t)f - 1];
-}
-float Tuple::getFloFld(int f) const {
-  check(f, global::AttrType::attrReal);
-  return reals_[(size_t)f - 1];
+  throw iterator::UnknowAttrType("Tuple: field " + std::to_string(fldNo) + " has another type (" +
+                                 std::to_string(type) + " asked)");
 }
 std::string Tuple::getStrFld(int f) const {
   check(f, global::AttrType::attrString);
   return strs_[(size_t)f - 1];
 }
-void Tuple::setIntFld(int f, int v) {
-  check(f, global::AttrType::attrInteger);
-  ints_[(size_t)f - 1] = v;
-}
-void Tuple::setFloFld(int f, float v) {
-  check(f, global::AttrType::attrReal);
-  reals_[(size_t)f - 1] = v;
-}
 void Tuple::setStrFld(int f, const std::string& v) {
   check(f, global::AttrType::attrString);
   strs_[(size_t)f - 1] = v;
+}
+void Tuple::setStrFld(int f, const char* p, size_t n) {
+  check(f, global::AttrType::attrString);
+  strs_[(size_t)f - 1].assign(p, n);
 }
 
 int Tuple::size() const {
@@ -635,38 +624,13 @@ int64_t CursorBatches::count() const {
   return n;
 }
 
-bool CursorBatches::next() {
+bool CursorBatches::next_batch() {
   if (!cur_) return false;
-  if (i_ >= n_) {
-    chk<FileScanException>(mbx_cursor_next_view(cur_, kRows, &vids_, vcols_.data(), &n_), "get_next");
-    i_ = 0;
-    if (n_ == 0) return false;
-  }
+  chk<FileScanException>(mbx_cursor_next_view(cur_, kRows, &vids_, vcols_.data(), &n_), "get_next");
+  i_ = 0;
+  if (n_ == 0) return false;
   i_++;
   return true;
-}
-
-void CursorBatches::fill(heap::Tuple& J) const {
-  const int64_t i = i_ - 1;
-  for (size_t j = 0; j < cols_.size(); j++) {
-    const uint8_t* p = (const uint8_t*)vcols_[j] + i * width_[j];
-    switch (kind_[j]) {
-      case AttrType::attrInteger: {
-        int32_t v;
-        memcpy(&v, p, 4);
-        J.setIntFld((int)j + 1, v);
-        break;
-      }
-      case AttrType::attrReal: {
-        float v;
-        memcpy(&v, p, 4);
-        J.setFloFld((int)j + 1, v);
-        break;
-      }
-      default:
-        J.setStrFld((int)j + 1, std::string((const char*)p, strnlen((const char*)p, (size_t)width_[j])));
-    }
-  }
 }
 
 void CursorBatches::restart() {

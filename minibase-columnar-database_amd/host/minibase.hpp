@@ -22,6 +22,7 @@
 #include <memory>
 #include <set>
 #include <stdexcept>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -103,16 +104,37 @@ namespace heap {
 class Tuple {
  public:
   void setHdr(const std::vector<global::AttrType>& types, const std::vector<short>& str_sizes);
-  int getIntFld(int fldNo) const;
-  float getFloFld(int fldNo) const;
+  // the accessors run once per field per delivered row: inline, with the
+  // reference's field-number / type checks (FieldNumberOutOfBoundException,
+  // UnknowAttrType) thrown out of line
+  int getIntFld(int fldNo) const {
+    check(fldNo, global::AttrType::attrInteger);
+    return ints_[(size_t)fldNo - 1];
+  }
+  float getFloFld(int fldNo) const {
+    check(fldNo, global::AttrType::attrReal);
+    return reals_[(size_t)fldNo - 1];
+  }
   std::string getStrFld(int fldNo) const;
-  void setIntFld(int fldNo, int v);
-  void setFloFld(int fldNo, float v);
+  void setIntFld(int fldNo, int v) {
+    check(fldNo, global::AttrType::attrInteger);
+    ints_[(size_t)fldNo - 1] = v;
+  }
+  void setFloFld(int fldNo, float v) {
+    check(fldNo, global::AttrType::attrReal);
+    reals_[(size_t)fldNo - 1] = v;
+  }
   void setStrFld(int fldNo, const std::string& v);
-  short noOfFlds() const { return (short)types_.size(); }
+  void setStrFld(int fldNo, const char* p, size_t n);  // no temporary std::string
+  short noOfFlds() const { return (short)kinds_.size(); }
   int size() const;  // header + fields, as Tuple.size() with setHdr's layout
  private:
-  void check(int fldNo, int type) const;
+  void check(int fldNo, int type) const {
+    if (__builtin_expect(fldNo < 1 || fldNo > (int)kinds_.size() || kinds_[(size_t)fldNo - 1] != type, 0))
+      bad_field(fldNo, type);
+  }
+  [[noreturn]] void bad_field(int fldNo, int type) const;
+  std::vector<int> kinds_;  // types_[i].attrType
   std::vector<global::AttrType> types_;
   std::vector<short> str_sizes_;
   std::vector<int32_t> ints_;
@@ -281,13 +303,43 @@ class CursorBatches {
              const std::vector<int32_t>& cols);
   bool open() const { return cur_ != nullptr; }
   int64_t count() const;
-  bool next();                  // the next row; false at the end of the stream
+  // the next row; false at the end of the stream (a new batch every kRows rows)
+  bool next() {
+    if (i_ < n_) {
+      i_++;
+      return true;
+    }
+    return next_batch();
+  }
   int64_t position() const { return vids_[i_ - 1]; }
-  void fill(heap::Tuple& J) const;
+  // the current row into J's fields 1..n (Projection.Project's copy)
+  void fill(heap::Tuple& J) const {
+    const int64_t i = i_ - 1;
+    for (size_t j = 0; j < kind_.size(); j++) {
+      const uint8_t* p = (const uint8_t*)vcols_[j] + i * width_[j];
+      switch (kind_[j]) {
+        case AttrType::attrInteger: {
+          int32_t v;
+          memcpy(&v, p, 4);
+          J.setIntFld((int)j + 1, v);
+          break;
+        }
+        case AttrType::attrReal: {
+          float v;
+          memcpy(&v, p, 4);
+          J.setFloFld((int)j + 1, v);
+          break;
+        }
+        default:
+          J.setStrFld((int)j + 1, (const char*)p, strnlen((const char*)p, (size_t)width_[j]));
+      }
+    }
+  }
   void restart();
   void close();
 
  private:
+  bool next_batch();
   mbx_cursor* cur_ = nullptr;
   std::vector<AttrType> types_;
   std::vector<short> sizes_;
