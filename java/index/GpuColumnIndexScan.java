@@ -136,7 +136,7 @@ public class GpuColumnIndexScan extends Iterator {
     if (i < n) return true;
     if (drained) return false;
     started = true;
-    Object[] r = Native.cursorNext(cursor, 65536, projTypes, projSizes);
+    Object[] r = Native.cursorNext(cursor, 262144, projTypes, projSizes);
     if (r == null) return false;
     ids = (long[]) r[0];
     batch = (Object[]) r[1];

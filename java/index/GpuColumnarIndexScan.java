@@ -188,7 +188,7 @@ public class GpuColumnarIndexScan extends Iterator implements iterator.GpuSelect
       return null;
     }
     if (i == n) {
-      Object[] r = Native.cursorNext(cursor, 65536, projTypes, projSizes);
+      Object[] r = Native.cursorNext(cursor, 262144, projTypes, projSizes);
       if (r == null) return null;
       ids = (long[]) r[0];
       batch = (Object[]) r[1];

@@ -25,7 +25,7 @@ import heap.Tuple;
  * two columns differ.
  */
 public class GpuColumnarColumnsScan extends Iterator implements GpuSelection {
-  static final int BATCH = 65536;   // rows per cursor batch
+  static final int BATCH = 262144;  // rows per cursor batch (profiles/r04/b)
 
   private final long ctx, table, plan;
   private long selection, cursor;

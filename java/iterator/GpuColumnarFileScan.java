@@ -18,7 +18,7 @@ import heap.Tuple;
  * R/columnar/Columnarfile.java:812-830) read only the position.
  */
 public class GpuColumnarFileScan extends Iterator implements GpuSelection {
-  static final int BATCH = 65536;   // rows per cursor batch (bench_delivery: 64 Ki keeps the copy calls small)
+  static final int BATCH = 262144;  // rows per cursor batch: one packed copy each, 42 vs 24 GB/s at 64 Ki (profiles/r04/b)
 
   private final long ctx, table, plan;
   private long selection, cursor;
