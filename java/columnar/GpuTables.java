@@ -146,6 +146,16 @@ public final class GpuTables {
     return Native.tableStage(GpuContext.ctx(), t, w, nrows, cols, deleted.toLongArray(), 0);
   }
 
+  /**
+   * Stage (if needed) a Columnarfile and add a column group over 2..4 of its
+   * 4-byte columns (0-based): index / file scans projecting them gather one
+   * 128-byte line per selected row (DESIGN.md section 2).  Lives with the
+   * staged table (dropped by invalidate).
+   */
+  public static synchronized void group(String columnarFile, int[] cols) throws Exception {
+    Native.tableGroup(GpuContext.ctx(), get(columnarFile), cols);
+  }
+
   /** a BitMapFile's BitSet on the device (uploaded from the engine's own copy) */
   public static synchronized long bitmap(BitMapFile f, long nbits) throws Exception {
     Long b = bitmaps.get(f);

@@ -43,6 +43,8 @@ public final class Native {
   public static native long dbBitmapStageRange(long ctx, long db, String bitMapFile, long bitBegin, long nbits)
       throws Exception;
   public static native long tableRowOffset(long table) throws Exception;
+  /** a row-interleaved copy of 2..4 four-byte columns the sparse gathers read (mbx_table_group) */
+  public static native void tableGroup(long ctx, long table, int[] cols) throws Exception;
   /** the Columnarfile's positions (highest position + 1) from its directory (mbx_db_columnar_info) */
   public static native long dbColumnarRows(long db, String columnarFile) throws Exception;
 

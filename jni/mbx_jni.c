@@ -357,6 +357,17 @@ JNIEXPORT jlong JNICALL Java_global_Native_tableRowOffset(JNIEnv *env, jclass cl
   return row_offset;
 }
 
+/* column group: a row-interleaved copy of 2..4 four-byte columns (mbx_table_group) */
+JNIEXPORT void JNICALL Java_global_Native_tableGroup(JNIEnv *env, jclass cls, jlong ctx, jlong t, jintArray cols) {
+  (void)cls;
+  const jsize n = cols ? (*env)->GetArrayLength(env, cols) : 0;
+  jint *c = n > 0 ? (*env)->GetIntArrayElements(env, cols, NULL) : NULL;
+  const int rc = (n > 0 && !c) ? MBX_E_NOMEM
+                               : mbx_table_group(P(mbx_ctx, ctx), P(mbx_table, t), (const int32_t *)c, (int32_t)n);
+  if (c) (*env)->ReleaseIntArrayElements(env, cols, c, JNI_ABORT);
+  check(env, rc, kFileScan);
+}
+
 /* ---- plans and scans ----------------------------------------------------- */
 
 JNIEXPORT jlong JNICALL Java_global_Native_planCompile(JNIEnv *env, jclass cls, jlong ctx, jlong table,

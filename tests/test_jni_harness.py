@@ -256,6 +256,33 @@ def test_golden_index_queries_through_the_cnf_cursor(jvm, ctx, mini):
 
 
 @pytest.mark.gpu
+def test_table_group_through_the_glue(jvm, ctx):
+    """Native.tableGroup (GpuTables.group): C, D grouped, every golden
+    indexes_query's C, D rows unchanged; a bad group -> FileScanException"""
+    rows = helpers.load_minidata()
+    cols = helpers.minidata_columns(rows)
+    t = stage(jvm, ctx, cols)
+    jvm.call("tableGroup", None, J(ctx), J(t), (V, jvm.array("I", [2, 3])))
+    with pytest.raises(JavaException) as e:
+        jvm.call("tableGroup", None, J(ctx), J(t), (V, jvm.array("I", [0, 1])))   # char(25) columns
+    assert e.value.cls == "iterator/FileScanException"
+    regs = value_bitmaps(jvm, ctx, cols, len(rows))
+    for g in GOLD["indexes_query"]:
+        conj = helpers.index_conjuncts(regs, helpers.golden_cnf(g["cnf"]), helpers.MINI_TYPES)
+        bms = [h for c in conj for h in c]
+        offs = np.cumsum([0] + [len(c) for c in conj])
+        cur = jvm.call("cnfCursorOpen", I64, J(ctx), J(t), (V, jvm.array("J", bms)), (V, jvm.array("I", offs)), J(0),
+                       (V, jvm.array("I", [2, 3])))
+        _, got = drain(jvm, cur, [1, 1], [4, 4], batch=1000)
+        jvm.call("cursorClose", None, J(cur))
+        assert got == [r[2:] for r in g["rows"]], g["line"]
+    for reg in regs.values():
+        for h in reg.values():
+            jvm.call("bitmapFree", None, J(h))
+    jvm.call("tableFree", None, J(t))
+
+
+@pytest.mark.gpu
 def test_errors_map_to_the_reference_exceptions(jvm, ctx, mini):
     _, _, t = mini
     with pytest.raises(JavaException) as e:
