@@ -87,6 +87,9 @@ static void tuning_from_env(MbxTuning& t) {
   t.sink_lds = (int32_t)env_knob("MBX_SINK_LDS", 1);
   t.ticket_groups = (int32_t)env_knob("MBX_TICKET_GROUPS", -1);
   t.fin_mode = (int32_t)env_knob("MBX_FIN_MODE", -1);
+#ifndef MBX_DIAG
+  if (t.fin_mode == kFinFences || t.fin_mode == kFinSegOnly) t.fin_mode = -1;  // A/B forms: -DMBX_DIAG
+#endif
   t.join_plain = (int32_t)env_knob("MBX_JOIN_PLAIN", 0);
   t.distinct_lds_probes = (int32_t)env_knob("MBX_DISTINCT_LDS_PROBES", -1);
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
@@ -288,7 +291,15 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "scan_ri")) t.scan_ri = v;
   else if (!strcmp(knob, "sink_lds")) t.sink_lds = v;
   else if (!strcmp(knob, "ticket_groups")) t.ticket_groups = v;
-  else if (!strcmp(knob, "fin_mode")) t.fin_mode = v;
+  else if (!strcmp(knob, "fin_mode")) {
+#ifndef MBX_DIAG
+    // kFinFences (plain stores + fences) and kFinSegOnly forced on a COUNT
+    // scan (no count) exist for A/B measurements only
+    if (v == kFinFences || v == kFinSegOnly)
+      return fail(MBX_E_UNSUPPORTED, "mbx_set_tuning: fin_mode %d needs a -DMBX_DIAG build", v);
+#endif
+    t.fin_mode = v;
+  }
   else if (!strcmp(knob, "join_plain")) t.join_plain = v;
   else if (!strcmp(knob, "distinct_lds_probes")) t.distinct_lds_probes = v;
   else if (!strcmp(knob, "select_dbg")) {

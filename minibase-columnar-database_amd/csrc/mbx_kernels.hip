@@ -402,7 +402,8 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
         store_count_sc1(L.partials + blockIdx.x, p);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       is_last = arrive(L.ticket, L.ticket_groups);
-    } else if (L.ticket) {
+#ifdef MBX_DIAG
+    } else if (L.ticket) {  // kFinFences: plain stores + release / acquire fences (the A/B reference form)
       L.partials[blockIdx.x] = p;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -412,6 +413,7 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+#endif
     } else {
       L.partials[blockIdx.x] = p;
     }
@@ -419,10 +421,13 @@ __device__ __forceinline__ void block_reduce_store(Acc a, const ScanLaunch& L) {
   if (!L.ticket) return;
   __syncthreads();
   if (is_last) {
-    if (L.fin_mode == kFinWriteThrough)
-      finalize_block<true, !FULL>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
-    else
+#ifdef MBX_DIAG
+    if (L.fin_mode != kFinWriteThrough) {
       finalize_block<false>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
+      return;
+    }
+#endif
+    finalize_block<true, !FULL>(L.partials, gridDim.x, L.agg_kind, L.agg_out, L.count_out, L.nan_out);
   }
 }
 

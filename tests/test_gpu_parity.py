@@ -678,6 +678,22 @@ def test_c5_full_table_1b_rows(ctx, m):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("knob,value", [
+    ("fin_mode", 1),         # plain stores + fences
+    ("fin_mode", 4),         # segment words only, forced on a COUNT scan
+    ("scan_int_range", 3),   # the removed unsigned range forms
+    ("select_dbg", 1),       # compaction A/B bits
+    ("select_dbg", 16),
+])
+def test_ab_only_knob_values_are_compiled_out(m, ctx, knob, value, tune):
+    """The A/B-only kernel forms exist in -DMBX_DIAG builds only: the
+    production library refuses the knob values that would select them
+    (MBX_E_UNSUPPORTED / MBX_E_INVALID) instead of silently running another form."""
+    with pytest.raises(m.MbxError) as e:
+        tune(knob, value)
+    assert e.value.code in (m.E_UNSUPPORTED, m.E_INVALID)
+
+
 @pytest.mark.parametrize("groups,tpb,fin", [
     ("32", "0", None),     # default: 32 group words + the top word
     ("1", "0", None),      # one flat packed word (~1000 arrivals)

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--variants", default="0,1,2,3,4,5,6")
     ap.add_argument("--tpb", default="0,24,48,96,191,382")
     ap.add_argument("--generic", action="store_true")
-    ap.add_argument("--fin", default="0", help="MBX_FIN_MODE values: 0 write-through, 1 fences, 2 separate")
+    ap.add_argument("--fin", default="0", help="MBX_FIN_MODE values: 0 write-through, 2 separate (1 fences: -DMBX_DIAG builds)")
     ap.add_argument("--groups", default="32", help="MBX_TICKET_GROUPS values (0/1: one flat ticket)")
     args = ap.parse_args()
 
