@@ -182,6 +182,8 @@ void Tuple::setHdr(const std::vector<global::AttrType>& types, const std::vector
   types_ = types;
   kinds_.clear();
   for (const auto& t : types) kinds_.push_back(t.attrType);
+  int_prefix_ = 0;
+  while (int_prefix_ < (int)kinds_.size() && kinds_[(size_t)int_prefix_] == global::AttrType::attrInteger) int_prefix_++;
   str_sizes_ = str_sizes;
   ints_.assign(types.size(), 0);
   reals_.assign(types.size(), 0.0f);
@@ -613,6 +615,8 @@ void CursorBatches::reset(mbx_cursor* c, const std::vector<AttrType>& types, con
     kind_[j] = types[(size_t)cols[j]].attrType;
     width_[j] = col_width(types, sizes, cols[j]);
   }
+  all_int_ = !cols.empty();
+  for (int k : kind_) all_int_ = all_int_ && k == AttrType::attrInteger;
   vcols_.assign(cols.size(), nullptr);
   vids_ = nullptr;
   n_ = i_ = 0;
@@ -677,13 +681,6 @@ void ColumnarFileScan::open_rows() {
                                          (int32_t)proj_cols_.size(), &cur),
                          "ColumnarFileScan: materialise");
   rows_.reset(cur, types_, sizes_, proj_cols_);
-}
-
-heap::Tuple* ColumnarFileScan::get_next() {
-  if (!rows_.open()) open_rows();
-  if (!rows_.next()) return nullptr;
-  rows_.fill(Jtuple_);
-  return &Jtuple_;
 }
 
 global::TID ColumnarFileScan::get_next_tid() {
@@ -1156,13 +1153,6 @@ void ColumnarIndexScan::open_cursor() {
   mbx_cursor* c = fused_ ? cnf_cursor(*f_, lists_, outIndexes_, "ColumnarIndexScan")
                          : bitset_cursor(*f_, output_, outIndexes_, "ColumnarIndexScan");
   rows_.reset(c, f_->getAttributeTypes(), f_->getAttrSizes(), pc);
-}
-
-heap::Tuple* ColumnarIndexScan::get_next() {
-  open_cursor();
-  if (!rows_.next()) return nullptr;
-  rows_.fill(Jtuple_);
-  return &Jtuple_;
 }
 
 global::TID ColumnarIndexScan::get_next_tid() {

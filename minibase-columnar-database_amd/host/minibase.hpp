@@ -126,6 +126,14 @@ class Tuple {
   }
   void setStrFld(int fldNo, const std::string& v);
   void setStrFld(int fldNo, const char* p, size_t n);  // no temporary std::string
+  // fields 1..n from row i of n int columns (Projection.Project's copy of an
+  // all-int projection): one range check against the header's leading int
+  // fields instead of one per field
+  void setIntFlds(const int32_t* const* cols, int64_t i, int n) {
+    if (__builtin_expect(n > int_prefix_, 0)) bad_field(int_prefix_ + 1, global::AttrType::attrInteger);
+    int32_t* d = ints_.data();
+    for (int j = 0; j < n; j++) d[j] = cols[j][i];
+  }
   short noOfFlds() const { return (short)kinds_.size(); }
   int size() const;  // header + fields, as Tuple.size() with setHdr's layout
  private:
@@ -135,6 +143,7 @@ class Tuple {
   }
   [[noreturn]] void bad_field(int fldNo, int type) const;
   std::vector<int> kinds_;  // types_[i].attrType
+  int int_prefix_ = 0;      // leading attrInteger fields
   std::vector<global::AttrType> types_;
   std::vector<short> str_sizes_;
   std::vector<int32_t> ints_;
@@ -316,6 +325,10 @@ class CursorBatches {
   // the current row into J's fields 1..n (Projection.Project's copy)
   void fill(heap::Tuple& J) const {
     const int64_t i = i_ - 1;
+    if (all_int_) {
+      J.setIntFlds(reinterpret_cast<const int32_t* const*>(vcols_.data()), i, (int)vcols_.size());
+      return;
+    }
     for (size_t j = 0; j < kind_.size(); j++) {
       const uint8_t* p = (const uint8_t*)vcols_[j] + i * width_[j];
       switch (kind_[j]) {
@@ -347,6 +360,7 @@ class CursorBatches {
   std::vector<int32_t> cols_;
   std::vector<int> kind_;    // per projected column: its AttrType code
   std::vector<int64_t> width_;  // per projected column: bytes per row in the batch
+  bool all_int_ = false;        // every projected column is attrInteger (fill's bulk copy)
   // the current batch in the cursor's pinned buffer (mbx_cursor_next_view:
   // rows are read in place, valid until the next batch)
   const int64_t* vids_ = nullptr;
@@ -360,7 +374,14 @@ class ColumnarFileScan : public Iterator {
   ColumnarFileScan(const std::string& file_name, const std::vector<AttrType>& in1,
                    const std::vector<short>& s1_sizes, short len_in1, int n_out_flds,
                    const std::vector<FldSpec>& proj_list, CondExpr* const* outFilter);
-  heap::Tuple* get_next() override;
+  // per delivered row: inline, and final so a caller holding the concrete
+  // class calls it directly
+  heap::Tuple* get_next() final {
+    if (__builtin_expect(!rows_.open(), 0)) open_rows();
+    if (!rows_.next()) return nullptr;
+    rows_.fill(Jtuple_);
+    return &Jtuple_;
+  }
   global::TID get_next_tid();
   void close() override;
   void restart() override;
@@ -501,7 +522,12 @@ class ColumnarIndexScan : public iterator::Iterator {
                     CondExpr* const* selects, bool indexOnly);
   // the CNF's BitSet (on the one-launch path it is formed on first request)
   columnar::BitSetPtr getOutputPositions();
-  heap::Tuple* get_next() override;
+  heap::Tuple* get_next() final {  // per delivered row: inline (ColumnarFileScan::get_next)
+    if (__builtin_expect(!rows_.open(), 0)) open_cursor();
+    if (!rows_.next()) return nullptr;
+    rows_.fill(Jtuple_);
+    return &Jtuple_;
+  }
   global::TID get_next_tid();
   void close() override;
   void restart() override;

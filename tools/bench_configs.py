@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--configs", default="C2,C4,C5")
+    ap.add_argument("--c2-stamps", action="store_true", help="C2: per-block stamps of each one-launch form")
     ap.add_argument("--c4-rows", type=int, default=100_000_000, help="global rows")
     ap.add_argument("--c4-positions", action="store_true",
                     help="C4 query also writes the selected positions (default: the projected rows only)")
@@ -170,19 +171,47 @@ def main():
         wpos = torch.nonzero(cols[0] < 104858).flatten()
         # both forms, interleaved: the BitSet scan + compaction (two launches)
         # and k_scan_select (one launch, knob scan_select_fused)
+        # and the one launch with its dry tail pass under the first loads
+        # (knob scan_select_warm)
         forms = {}
+        variants = {0: (0, 0), 1: (1, 0), "warm": (1, 1)}
         for rep in range(3):
-            for fused in (0, 1):
+            for key, (fused, warm) in variants.items():
                 ctx.set_tuning("scan_select_fused", fused)
+                ctx.set_tuning("scan_select_warm", warm)
                 ids.zero_()
                 torch.cuda.synchronize()
-                forms.setdefault(fused, []).append(kernel_ms(step, args.steps, args.warmup))
+                forms.setdefault(key, []).append(kernel_ms(step, args.steps, args.warmup))
                 got = int(cnt.item())
-                assert got == want, (fused, got, want)
-                assert bool((ids[:got] == wpos).all()), fused
+                assert got == want, (key, got, want)
+                assert bool((ids[:got] == wpos).all()), key
+        stamps = {}
+        if args.c2_stamps:
+            # per-block wall_clock64() stamps (start / count published / offset
+            # known / end, select_dbg bit 3) of one launch of each one-launch form
+            ntiles = -(-n // 256)
+            tpb = max(4, -(-ntiles // 1024))
+            nb = -(-(-(-ntiles // tpb)) // 4)  # 16-wave blocks of 4 BitSet segments
+            for key in (1, "warm"):
+                ctx.set_tuning("scan_select_fused", 1)
+                ctx.set_tuning("scan_select_warm", variants[key][1])
+                ctx.set_tuning("select_dbg", 8)
+                step()
+                ctx.sync()
+                st = np.zeros(4 * nb, dtype=np.int64)
+                M._chk(L.mbx_diag_select_stamps(ctx.h, st.ctypes.data, nb))
+                st = st.reshape(nb, 4).astype(np.float64) / 100.0  # 100 MHz wall clock -> us
+                st -= st[:, 0].min()
+                pct = lambda x: [round(float(v), 2) for v in np.percentile(x, [0, 10, 50, 90, 100])]
+                stamps[str(key)] = {"blocks": nb, "s1_pct": pct(st[:, 1]), "s2_pct": pct(st[:, 2]),
+                                    "s3_pct": pct(st[:, 3]), "s2_s1_pct": pct(st[:, 2] - st[:, 1]),
+                                    "s3_s2_pct": pct(st[:, 3] - st[:, 2])}
+                ctx.set_tuning("select_dbg", 0)
         fused_default = int(os.environ.get("MBX_SCAN_SELECT_FUSED", "1") or 0)
+        warm_default = int(os.environ.get("MBX_SCAN_SELECT_WARM", "0") or 0)
         ctx.set_tuning("scan_select_fused", fused_default)
-        ms = sorted(forms[fused_default])[1]  # the median of the three interleaved rounds
+        ctx.set_tuning("scan_select_warm", warm_default)
+        ms = sorted(forms["warm" if fused_default and warm_default else fused_default])[1]  # median of 3 rounds
         # the same queries replayed from a HIP graph of 10 (mbx_graph_*: no host launches between them)
         ctx.sync()
         ctx.graph_begin()
@@ -197,6 +226,7 @@ def main():
         emit({"config": "C2", "rows": n, "gpus": 1, "selected": got, "ms_per_query": ms, "rows_per_s": n / ms * 1e3,
               "form": "one launch (k_scan_select)" if fused_default else "two launches (BitSet scan + k_select_ids)",
               "ms_per_query_two_launch": forms[0], "ms_per_query_one_launch": forms[1],
+              "ms_per_query_one_launch_warm": forms["warm"], "stamps_us": stamps,
               "graph_replay_ms_per_query": graph_ms,
               "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
               "scan_gbs": (n * 4 + n / 8) / scan_ms / 1e6})

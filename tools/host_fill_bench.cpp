@@ -32,7 +32,21 @@ int main() {
       sum += J.getIntFld(1);
     }
     const double ns = std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
-    printf("{\"rows\": %lld, \"ns_per_row\": %.2f, \"checksum\": %lld}\n", (long long)n, ns / n, (long long)sum);
+    printf("{\"form\": \"setIntFld\", \"rows\": %lld, \"ns_per_row\": %.2f, \"checksum\": %lld}\n", (long long)n,
+           ns / n, (long long)sum);
+  }
+  const int32_t* cp[ncols];
+  for (int c = 0; c < ncols; c++) cp[c] = cols[c].data();
+  for (int rep = 0; rep < 5; rep++) {
+    int64_t sum = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int64_t i = 0; i < n; i++) {
+      J.setIntFlds(cp, i, ncols);
+      sum += J.getIntFld(1);
+    }
+    const double ns = std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - t0).count();
+    printf("{\"form\": \"setIntFlds\", \"rows\": %lld, \"ns_per_row\": %.2f, \"checksum\": %lld}\n", (long long)n,
+           ns / n, (long long)sum);
   }
   return 0;
 }
