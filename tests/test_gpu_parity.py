@@ -691,7 +691,7 @@ def test_ab_only_knob_values_are_compiled_out(m, ctx, knob, value, tune):
     (MBX_E_UNSUPPORTED / MBX_E_INVALID) instead of silently running another form."""
     with pytest.raises(m.MbxError) as e:
         tune(knob, value)
-    assert e.value.code in (m.E_UNSUPPORTED, m.E_INVALID)
+    assert e.value.code in (m.mbx.E_UNSUPPORTED, m.mbx.E_INVALID)
 
 
 @pytest.mark.parametrize("groups,tpb,fin", [
