@@ -1278,7 +1278,8 @@ static int scan_select_into(mbx_ctx* c, mbx_plan* p, mbx_bitmap* b, int64_t* dev
     if (rc) return rc;
     const int64_t tpb = b->wpb / kWordsPerTile;
     if (c->tune.scan_ri != 0 && p->all_literal &&
-        scan_select_fusable(p->t->nrows, tpb, v->fast_k, v->fast_ks, p->host.nterms, p->host.has_real) &&
+        scan_select_fusable(p->t->nrows, tpb, v->fast_k, v->fast_ks, p->host.nterms, p->host.has_real,
+                            c->tune.scan_select_waves) &&
         grid_blocks(p->t->nrows, tpb) == b->nseg) {
       const FusedSelect f{dev_ids, dev_count};
       return enqueue_scan(c, p, *v, kModeBitmap, b->words, c->partials, tpb, dev_count, nullptr, dev_nan, b->segc, &f);

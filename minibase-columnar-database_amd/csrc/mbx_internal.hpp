@@ -344,7 +344,7 @@ constexpr int64_t kLookbackWords = 1 + 2 * 1024;  // epoch, per-block counts, pe
 // one-launch form (scan_select_fusable); L as for a kModeBitmap scan (its
 // out_words / seg_counts: the BitSet and its segment counts)
 bool scan_select_fusable(int64_t nrows, int64_t tiles_per_block, int32_t fast_k, int32_t fast_ks, int32_t nterms,
-                         int32_t has_real);
+                         int32_t has_real, int32_t waves);
 hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offset, int64_t* ids, int64_t* total,
                               hipStream_t s, int64_t* stamps, int32_t dbg, int32_t waves, int32_t warm);
 hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,

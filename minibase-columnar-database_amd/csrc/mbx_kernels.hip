@@ -2465,9 +2465,12 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
 }
 
 bool scan_select_fusable(int64_t nrows, int64_t tiles_per_block, int32_t fast_k, int32_t fast_ks, int32_t nterms,
-                         int32_t has_real) {
+                         int32_t has_real, int32_t waves) {
   const int64_t ntiles = (nrows + kTileRows - 1) / kTileRows;
-  const int64_t nb = ntiles == 0 ? 1 : (ntiles + tiles_per_block - 1) / tiles_per_block;
+  const int64_t nseg = ntiles == 0 ? 1 : (ntiles + tiles_per_block - 1) / tiles_per_block;
+  // look-back flags per block: a 16-wave block holds 4 segments
+  const int64_t spb = waves == 16 ? 16 / kWaves : 1;
+  const int64_t nb = (nseg + spb - 1) / spb;
   return fast_k >= 1 && fast_k <= 4 && fast_ks == 0 && !has_real && nterms >= 1 && nterms <= kHoistTerms &&
          nrows > 0 && nb <= kLookbackBlocks && (tiles_per_block + kWaves - 1) / kWaves <= 16 * kSelRegs &&
          nrows < (int64_t(1) << 32);

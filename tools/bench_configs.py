@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--configs", default="C2,C4,C5")
     ap.add_argument("--c2-stamps", action="store_true", help="C2: per-block stamps of each one-launch form")
+    ap.add_argument("--c2-tpb", default="", help="C2: comma list of tiles_per_block to sweep (one launch)")
     ap.add_argument("--c4-rows", type=int, default=100_000_000, help="global rows")
     ap.add_argument("--c4-positions", action="store_true",
                     help="C4 query also writes the selected positions (default: the projected rows only)")
@@ -230,6 +231,27 @@ def main():
               "graph_replay_ms_per_query": graph_ms,
               "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
               "scan_gbs": (n * 4 + n / 8) / scan_ms / 1e6})
+        # segment size sweep (knob tiles_per_block, read by the BitSet's
+        # allocation): smaller segments = more waves per CU and more blocks
+        # in the look-back
+        for tpb in [int(x) for x in args.c2_tpb.split(",") if x]:
+            ctx.set_tuning("tiles_per_block", tpb)
+            bmt = ctx.bitmap_alloc(n)
+            res = {}
+            for rep in range(3):
+                for warm in (0, 1):
+                    ctx.set_tuning("scan_select_fused", 1)
+                    ctx.set_tuning("scan_select_warm", warm)
+                    ids.zero_()
+                    torch.cuda.synchronize()
+                    f = lambda: M._chk(L.mbx_scan_select_async(ctx.h, plan.h, bmt.h, ids.data_ptr(), cnt.data_ptr()))
+                    res.setdefault(warm, []).append(kernel_ms(f, args.steps, args.warmup))
+                    got = int(cnt.item())
+                    assert got == want and bool((ids[:got] == wpos).all()), (tpb, warm)
+            emit({"config": "C2-tpb", "tiles_per_block": tpb, "ms_one_launch": res[0], "ms_one_launch_warm": res[1]})
+            del bmt
+            ctx.set_tuning("tiles_per_block", 0)
+        ctx.set_tuning("scan_select_warm", warm_default)
         del cols, t, plan, bm, ids
         torch.cuda.empty_cache()
 

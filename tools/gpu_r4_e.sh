@@ -10,7 +10,7 @@ OUT=gpurun_out/${TAG:-r4_e}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_scan_select_fused.py tests/test_gpu_parity.py -k "fused or ab_only or finalize" -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
-timeout -k 10 300 python3 tools/bench_configs.py --configs C2 --c2-stamps > $OUT/c2.jsonl 2> $OUT/c2.err || { echo C2_FAIL; tail -20 $OUT/c2.err; exit 1; }
+timeout -k 10 300 python3 tools/bench_configs.py --configs C2 --c2-stamps --c2-tpb 10,13,20,26,39 > $OUT/c2.jsonl 2> $OUT/c2.err || { echo C2_FAIL; tail -20 $OUT/c2.err; exit 1; }
 cut -c1-900 $OUT/c2.jsonl
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/c2_kt -o c --output-format csv -- python3 tools/bench_configs.py --configs C2 > $OUT/c2_kt.jsonl 2> $OUT/c2_kt.err || { echo C2_KT_FAIL; tail -20 $OUT/c2_kt.err; exit 1; }
 find $OUT/c2_kt -name '*kernel_stats.csv' -exec cp {} $OUT/c2_kernel_stats.csv \;
