@@ -1609,10 +1609,10 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
                                             int64_t* __restrict__ total, const GT& G, int64_t* __restrict__ stamps,
                                             int32_t dbg, int64_t* __restrict__ segc, int64_t nseg, int64_t* wcount,
                                             int64_t* wpre, uint16_t (*stage)[32 * 64],
-                                            uint64_t* __restrict__ words_out = nullptr, bool dry = false) {
-  // dry: the warm-up pass of k_scan_select<WARM> -- the same instructions
-  // over the LDS only (no flag, poll or output access: the caller passes null
-  // outputs), so the CU's instruction cache holds this code before it counts
+                                            uint64_t* __restrict__ words_out = nullptr, int32_t fs = 1) {
+  // fs: int64 words between two blocks' count flags (1, or 16 = one 128-byte
+  // line per flag for the polling form: the polls of every block do not queue
+  // on the same few lines); the chained form needs 1
   dbg &= kDiagDbg;  // bits 0-2: A/B poll forms, -DMBX_DIAG builds only
   int64_t* const inc = lb + 1 + kLookbackBlocks;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
   // wave 0 loads the look-back's first window (the 64 predecessors) BEFORE
@@ -1621,7 +1621,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // that store's write-through round trip (and for any BitSet word stores
   // before it -- k_scan_select stores its words at the end, words_out)
   int64_t in0 = 0, a0f = epoch << 32;
-  if ((dbg & 8) && wave == 0 && blockIdx.x > 0 && !dry) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
+  if ((dbg & 8) && wave == 0 && blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
   if (lane == 0) wcount[wave] = c;
@@ -1631,8 +1631,9 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // the count is published by wave 1, not by the polling wave 0: each wave
   // has its own vmcnt, and a wave's wait for a poll also waits for every
   // store it issued before (the flag's write-through round trip)
-  if (threadIdx.x == 64 && !dry) {
-    __hip_atomic_store(&lb[1 + blockIdx.x], (epoch << 32) | bc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 64) {
+    __hip_atomic_store(&lb[1 + (int64_t)blockIdx.x * fs], (epoch << 32) | bc, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
     if (stamps) stamps[4 * blockIdx.x + 1] = wall_clock64();
   }
   // look-back: the predecessors' counts, all polls of a thread in flight together
@@ -1641,12 +1642,12 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
 #pragma unroll
   for (int k = 0; k < kLookbackBlocks / kThreads; ++k) {
     const int64_t j = (int64_t)k * kThreads + threadIdx.x;
-    if ((dbg & 8) || j >= (int64_t)blockIdx.x || dry)
+    if ((dbg & 8) || j >= (int64_t)blockIdx.x)
       v[k] = epoch << 32;
     else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
-      v[k] = __builtin_nontemporal_load(&lb[1 + j]);
+      v[k] = __builtin_nontemporal_load(&lb[1 + j * fs]);
     else
-      v[k] = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // meanwhile: stage the wave's leading steps together, load the first
   // kPrefetch x 64 rows' values
@@ -1666,7 +1667,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     }
     if constexpr (G4 != kWide) {
 #pragma unroll
-      for (int k = 0; k < kPrefetch && !dry; ++k) {
+      for (int k = 0; k < kPrefetch; ++k) {
         const uint32_t i = (uint32_t)lane + 64u * k;
         if (i < tot) {
           const int64_t p = a0 * 64 + st[i];
@@ -1682,7 +1683,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     // chained form: wave 0 walks back over its predecessors, 64 per round,
     // stops at the nearest one whose inclusive prefix is published and adds
     // the counts after it; other waves contribute 0
-    if (wave == 0 && !dry) pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
+    if (wave == 0) pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
   } else {
 #pragma unroll
   for (int k = 0; k < kLookbackBlocks / kThreads; ++k) {
@@ -1692,7 +1693,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
         __builtin_amdgcn_s_sleep(16);
       else
         __builtin_amdgcn_s_sleep(1);
-      v[k] = __hip_atomic_load(&lb[1 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     pre += v[k] & 0xffffffffll;
   }
@@ -1704,9 +1705,9 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
   for (int k = 0; k < NW; ++k) off += wpre[k];
-  if ((dbg & 8) && threadIdx.x == 0 && !dry)
+  if ((dbg & 8) && threadIdx.x == 0)
     __hip_atomic_store(&inc[blockIdx.x], (epoch << 32) | (off + bc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (blockIdx.x == gridDim.x - 1 && !dry) {
+  if (blockIdx.x == gridDim.x - 1) {
     if (threadIdx.x == 0) {
       *total = off + bc;
       lb[0] = epoch;
@@ -1714,7 +1715,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     // the flags of blocks this launch does not have carry its epoch too, so a
     // later, larger launch never finds a flag older than the previous launch
     for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += kThreads) {
-      lb[1 + j] = epoch << 32;
+      lb[1 + j * fs] = epoch << 32;
       if (dbg & 8) inc[j] = epoch << 32;
     }
   }
@@ -1875,17 +1876,12 @@ constexpr bool kDefaultNT = true;
 // is known -- no second launch, no re-read of the BitSet.  Plans of 1..4
 // 4-byte int literal terms (no float compare: no NaN reach), wave ranges of
 // <= kSelRegs x 16 tiles (tables up to ~134 M rows), <= kLookbackBlocks blocks.
-//
-// WARM: every wave issues its first tile loads, then runs select_tail once
-// dry (fake words, LDS only) while they are in flight -- all 16 waves of a CU
-// reach the tail together after the scan, and the tail's code is then in the
-// instruction cache instead of being fetched cold by every CU at that moment.
-template <int K, bool DEL, int U, int TQ, int NW, int NR, int IR = 0, bool WARM = false>
+template <int K, bool DEL, int U, int TQ, int NW, int NR, int IR = 0>
 __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* __restrict__ lb, int64_t row_offset,
                                                          int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                         int64_t* __restrict__ stamps, int32_t dbg) {
+                                                         int64_t* __restrict__ stamps, int32_t dbg, int32_t fs) {
 #ifndef MBX_DIAG
-  dbg = 8;  // the chained look-back, write-through positions: the A/B forms are -DMBX_DIAG only
+  dbg &= 8;  // the look-back form (bit 3: chained, else every predecessor polled); write-through positions
 #endif
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
   __shared__ int64_t wcount[NW];
@@ -1922,24 +1918,9 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
   Acc acc;
   acc_init(acc);
   uint64_t wave_count = 0;
-  const int sub = wave % kWaves;
-  const int64_t tf = min(tb1, nrows / kTileRows);  // the segment's full tiles end here
-  TileRegs<K, 0> D0[U];
-  if constexpr (WARM) load_tiles<K, 0, U, kDefaultNT, true>(D0, tb0 + sub, kWaves, tf, colp, strp, lane);
-  // pass 0 (WARM only) is the dry tail; the asm keeps `pass` opaque so the
-  // loop is not peeled into a second copy of the tail
-  int32_t pass = WARM ? 0 : 1;
-  if constexpr (WARM) asm volatile("" : "+s"(pass));
-  for (;;) {
   uint64_t wr[NR];
   int64_t c = 0;
-  if (!pass) {
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      wr[r] = a0 + (int64_t)r * 64 + lane < a1 ? 0x0101010101010101ull : 0ull;
-      c += __popcll(wr[r]);
-    }
-  } else {
+  {
     // the segment's 4 waves read its tiles interleaved (wave w % 4 takes
     // tiles w % 4, + 4, + 8, ... as the fast scan does: at any moment the
     // waves of a segment stream adjacent tiles), the words go to LDS (the
@@ -1947,14 +1928,11 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
     // of them into registers -- the positions stay ascending by wave
     uint64_t* const segw =
         reinterpret_cast<uint64_t*>(&stage[0][0]) + (int64_t)(wave / kWaves) * L.tiles_per_block * kWordsPerTile;
+    const int sub = wave % kWaves;
+    const int64_t tf = min(tb1, nrows / kTileRows);  // the segment's full tiles end here
     for (int64_t base = tb0 + sub; base < tb1; base += (int64_t)kWaves * U) {
       TileRegs<K, 0> D[U];
-      if (WARM && base == tb0 + sub) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) D[u] = D0[u];
-      } else {
-        load_tiles<K, 0, U, kDefaultNT, true>(D, base, kWaves, tf, colp, strp, lane);
-      }
+      load_tiles<K, 0, U, kDefaultNT, true>(D, base, kWaves, tf, colp, strp, lane);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t t = base + (int64_t)u * kWaves;
@@ -1983,15 +1961,9 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
   }
   auto word_at = [&](int64_t) -> uint64_t { return 0ull; };  // never called: every range is cached
   const Gather4 G{};
-  select_tail<0, Gather4, decltype(word_at), NW, NR>(
-      wr, c, true, a0, a1, word_at, lane, wave, lb, epoch, row_offset, pass ? ids : nullptr, total, G,
-      pass ? stamps : nullptr, dbg, pass ? L.seg_counts : nullptr, nseg, wcount, wpre, stage,
-      pass ? L.out_words : nullptr, !pass);
-  if (pass) break;
-  __syncthreads();  // the dry pass's stage reads before the scan's words land there
-  pass = 1;
-  asm volatile("" : "+s"(pass));
-  }
+  select_tail<0, Gather4, decltype(word_at), NW, NR>(wr, c, true, a0, a1, word_at, lane, wave, lb, epoch, row_offset,
+                                                     ids, total, G, stamps, dbg, L.seg_counts, nseg, wcount, wpre,
+                                                     stage, L.out_words, fs);
 }
 
 // Late materialisation (Heapfile.findRID + getRecord per output column,
@@ -2477,14 +2449,17 @@ bool scan_select_fusable(int64_t nrows, int64_t tiles_per_block, int32_t fast_k,
 }
 
 hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offset, int64_t* ids, int64_t* total,
-                              hipStream_t s, int64_t* stamps, int32_t dbg, int32_t waves, int32_t warm) {
+                              hipStream_t s, int64_t* stamps, int32_t dbg, int32_t waves, int32_t flag_stride) {
   // waves per block: 4 (one BitSet segment per block) or 16 (four): a
   // quarter of the blocks publish and walk back
   const int nw = waves == 16 ? 16 : kWaves;
   const int64_t nseg = grid_blocks(L.nrows, L.tiles_per_block);
   const int64_t g = (nseg + nw / kWaves - 1) / (nw / kWaves);
-  // the chained look-back (32-bit inclusive prefixes: tables < 2^32 rows)
+  // the chained look-back (32-bit inclusive prefixes: tables < 2^32 rows),
+  // or (select_dbg bit 7) every predecessor's count polled, one flag per
+  // flag_stride int64 words (the chained walk needs them packed)
   dbg = (dbg & ~8) | (!(dbg & 8) ? 8 : 0);
+  const int32_t fs = (dbg & 8) || flag_stride != kFlagStride ? 1 : kFlagStride;
   const bool del = L.deleted != nullptr;
   const bool ir = L.int_range != 0;  // branch-free int terms (every fused plan qualifies; the knob can turn it off)
   // registers of 64 words per wave: only as many as a wave's quarter
@@ -2493,25 +2468,19 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
   // instruction cache, fewer VGPRs)
   const int64_t wave_words = (L.tiles_per_block + kWaves - 1) / kWaves * kWordsPerTile;
   const int nr = wave_words <= 64 ? 1 : wave_words <= 128 ? 2 : wave_words <= 256 ? 4 : kSelRegs;
-#define MBX_SCAN_SELECT_W(KK, UU, NW, NR, W)                                                                     \
-  if (del && ir)                                                                                                 \
-    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR, 1, W>), dim3((unsigned)g), dim3(64 * NW), \
-                       0, s, L, lb, row_offset, ids, total, stamps, dbg);                                        \
-  else if (del)                                                                                                  \
-    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR, 0, W>), dim3((unsigned)g), dim3(64 * NW), \
-                       0, s, L, lb, row_offset, ids, total, stamps, dbg);                                        \
-  else if (ir)                                                                                                   \
-    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR, 1, W>), dim3((unsigned)g),           \
-                       dim3(64 * NW), 0, s, L, lb, row_offset, ids, total, stamps, dbg);                         \
-  else                                                                                                           \
-    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR, 0, W>), dim3((unsigned)g),           \
-                       dim3(64 * NW), 0, s, L, lb, row_offset, ids, total, stamps, dbg)
-#define MBX_SCAN_SELECT_NW(KK, UU, NW, NR) \
-  if (warm) {                              \
-    MBX_SCAN_SELECT_W(KK, UU, NW, NR, true);  \
-  } else {                                 \
-    MBX_SCAN_SELECT_W(KK, UU, NW, NR, false); \
-  }
+#define MBX_SCAN_SELECT_NW(KK, UU, NW, NR)                                                                       \
+  if (del && ir)                                                                                               \
+    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR, 1>), dim3((unsigned)g), dim3(64 * NW), \
+                       0, s, L, lb, row_offset, ids, total, stamps, dbg, fs);                                  \
+  else if (del)                                                                                                \
+    hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \
+                       s, L, lb, row_offset, ids, total, stamps, dbg, fs);                                     \
+  else if (ir)                                                                                                 \
+    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR, 1>), dim3((unsigned)g),            \
+                       dim3(64 * NW), 0, s, L, lb, row_offset, ids, total, stamps, dbg, fs);                   \
+  else                                                                                                         \
+    hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \
+                       s, L, lb, row_offset, ids, total, stamps, dbg, fs)
 #define MBX_SCAN_SELECT(KK, UU)                  \
   if (nw != 16) {                                \
     MBX_SCAN_SELECT_NW(KK, UU, kWaves, kSelRegs); \
@@ -2535,7 +2504,6 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
   }
 #undef MBX_SCAN_SELECT
 #undef MBX_SCAN_SELECT_NW
-#undef MBX_SCAN_SELECT_W
   return hipGetLastError();
 }
 

@@ -119,14 +119,18 @@ def test_fused_c2_full_size_launch_after_launch(ctx):
     g.close()
 
 
-@pytest.mark.parametrize("warm", [0, 1])
+LOOKBACK = {"chained": (0, 1), "poll": (128, 1), "poll_spread": (128, 16)}
+
+
+@pytest.mark.parametrize("lookback", list(LOOKBACK))
 @pytest.mark.parametrize("tpb", [1, 4, 37, 200, 512, 513, 1000])
-def test_fused_segment_sizes_and_fallback(ctx, tune, tpb, warm):
+def test_fused_segment_sizes_and_fallback(ctx, tune, tpb, lookback):
     """segments of 1..1000 tiles: up to 128 tiles per wave run fused, larger
-    ones fall back to the two launches -- both exact, with and without the
-    dry tail pass (every register count NR: 1, 2, 4, 8 groups of 64 words)"""
+    ones fall back to the two launches -- both exact, with every look-back
+    form (every register count NR: 1, 2, 4, 8 groups of 64 words)"""
     tune("tiles_per_block", tpb)
-    tune("scan_select_warm", warm)
+    tune("select_dbg", LOOKBACK[lookback][0])
+    tune("select_flag_stride", LOOKBACK[lookback][1])
     n = 3_000_017
     cols = int_cols(n, hi=1000, seed=5)
     t = ctx.stage(cols)
@@ -137,16 +141,17 @@ def test_fused_segment_sizes_and_fallback(ctx, tune, tpb, warm):
     assert np.array_equal(ctx.select(bm), ids)
 
 
-@pytest.mark.parametrize("warm", [0, 1])
+@pytest.mark.parametrize("lookback", list(LOOKBACK))
 @pytest.mark.parametrize("waves", [4, 16])
 @pytest.mark.parametrize("n", [255, 70001, 3_000_017, 10_000_000])
-def test_fused_waves_per_block(ctx, tune, waves, n, warm):
+def test_fused_waves_per_block(ctx, tune, waves, n, lookback):
     """one BitSet segment per 4-wave block, or four per 16-wave block (a
-    quarter of the blocks in the look-back), with and without the dry tail
-    pass under the first loads (scan_select_warm): the same positions, words
-    and segment counts"""
+    quarter of the blocks in the look-back), with each look-back form (the
+    chained walk; every predecessor polled, flags packed or one per 128-byte
+    line): the same positions, words and segment counts"""
     tune("scan_select_waves", waves)
-    tune("scan_select_warm", warm)
+    tune("select_dbg", LOOKBACK[lookback][0])
+    tune("select_flag_stride", LOOKBACK[lookback][1])
     cols = int_cols(n, ncols=2, hi=1000, seed=n + waves)
     dele = helpers.random_deleted(n, 0.03, seed=n) if n == 70001 else None
     ot = oracle.Table(cols, dele)

@@ -172,14 +172,15 @@ def main():
         wpos = torch.nonzero(cols[0] < 104858).flatten()
         # both forms, interleaved: the BitSet scan + compaction (two launches)
         # and k_scan_select (one launch, knob scan_select_fused)
-        # and the one launch with its dry tail pass under the first loads
-        # (knob scan_select_warm)
+        # and the one launch with the polling look-back (select_dbg 128),
+        # flags packed or one per 128-byte line (select_flag_stride 16)
         forms = {}
-        variants = {0: (0, 0), 1: (1, 0), "warm": (1, 1)}
+        variants = {0: (0, 0, 1), 1: (1, 0, 1), "poll": (1, 128, 1), "poll_spread": (1, 128, 16)}
         for rep in range(3):
-            for key, (fused, warm) in variants.items():
+            for key, (fused, dbg, fs) in variants.items():
                 ctx.set_tuning("scan_select_fused", fused)
-                ctx.set_tuning("scan_select_warm", warm)
+                ctx.set_tuning("select_dbg", dbg)
+                ctx.set_tuning("select_flag_stride", fs)
                 ids.zero_()
                 torch.cuda.synchronize()
                 forms.setdefault(key, []).append(kernel_ms(step, args.steps, args.warmup))
@@ -193,10 +194,10 @@ def main():
             ntiles = -(-n // 256)
             tpb = max(4, -(-ntiles // 1024))
             nb = -(-(-(-ntiles // tpb)) // 4)  # 16-wave blocks of 4 BitSet segments
-            for key in (1, "warm"):
+            for key in (1, "poll", "poll_spread"):
                 ctx.set_tuning("scan_select_fused", 1)
-                ctx.set_tuning("scan_select_warm", variants[key][1])
-                ctx.set_tuning("select_dbg", 8)
+                ctx.set_tuning("select_flag_stride", variants[key][2])
+                ctx.set_tuning("select_dbg", 8 | variants[key][1])
                 step()
                 ctx.sync()
                 st = np.zeros(4 * nb, dtype=np.int64)
@@ -209,10 +210,9 @@ def main():
                                     "s3_s2_pct": pct(st[:, 3] - st[:, 2])}
                 ctx.set_tuning("select_dbg", 0)
         fused_default = int(os.environ.get("MBX_SCAN_SELECT_FUSED", "1") or 0)
-        warm_default = int(os.environ.get("MBX_SCAN_SELECT_WARM", "0") or 0)
+        ctx.set_tuning("reset")
         ctx.set_tuning("scan_select_fused", fused_default)
-        ctx.set_tuning("scan_select_warm", warm_default)
-        ms = sorted(forms["warm" if fused_default and warm_default else fused_default])[1]  # median of 3 rounds
+        ms = sorted(forms[fused_default])[1]  # the median of the three interleaved rounds
         # the same queries replayed from a HIP graph of 10 (mbx_graph_*: no host launches between them)
         ctx.sync()
         ctx.graph_begin()
@@ -227,7 +227,8 @@ def main():
         emit({"config": "C2", "rows": n, "gpus": 1, "selected": got, "ms_per_query": ms, "rows_per_s": n / ms * 1e3,
               "form": "one launch (k_scan_select)" if fused_default else "two launches (BitSet scan + k_select_ids)",
               "ms_per_query_two_launch": forms[0], "ms_per_query_one_launch": forms[1],
-              "ms_per_query_one_launch_warm": forms["warm"], "stamps_us": stamps,
+              "ms_per_query_one_launch_poll": forms["poll"], "ms_per_query_one_launch_poll_spread": forms["poll_spread"],
+              "stamps_us": stamps,
               "graph_replay_ms_per_query": graph_ms,
               "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
               "scan_gbs": (n * 4 + n / 8) / scan_ms / 1e6})
@@ -239,19 +240,21 @@ def main():
             bmt = ctx.bitmap_alloc(n)
             res = {}
             for rep in range(3):
-                for warm in (0, 1):
+                for key in (1, "poll_spread"):
                     ctx.set_tuning("scan_select_fused", 1)
-                    ctx.set_tuning("scan_select_warm", warm)
+                    ctx.set_tuning("select_dbg", variants[key][1])
+                    ctx.set_tuning("select_flag_stride", variants[key][2])
                     ids.zero_()
                     torch.cuda.synchronize()
                     f = lambda: M._chk(L.mbx_scan_select_async(ctx.h, plan.h, bmt.h, ids.data_ptr(), cnt.data_ptr()))
-                    res.setdefault(warm, []).append(kernel_ms(f, args.steps, args.warmup))
+                    res.setdefault(str(key), []).append(kernel_ms(f, args.steps, args.warmup))
                     got = int(cnt.item())
-                    assert got == want and bool((ids[:got] == wpos).all()), (tpb, warm)
-            emit({"config": "C2-tpb", "tiles_per_block": tpb, "ms_one_launch": res[0], "ms_one_launch_warm": res[1]})
+                    assert got == want and bool((ids[:got] == wpos).all()), (tpb, key)
+            emit({"config": "C2-tpb", "tiles_per_block": tpb, "ms_one_launch": res})
             del bmt
             ctx.set_tuning("tiles_per_block", 0)
-        ctx.set_tuning("scan_select_warm", warm_default)
+        ctx.set_tuning("reset")
+        ctx.set_tuning("scan_select_fused", fused_default)
         del cols, t, plan, bm, ids
         torch.cuda.empty_cache()
 
