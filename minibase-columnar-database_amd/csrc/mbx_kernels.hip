@@ -1615,39 +1615,46 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // on the same few lines); the chained form needs 1
   dbg &= kDiagDbg;  // bits 0-2: A/B poll forms, -DMBX_DIAG builds only
   int64_t* const inc = lb + 1 + kLookbackBlocks;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
-  // wave 0 loads the look-back's first window (the 64 predecessors) BEFORE
-  // this block stores its own flag: vmcnt counts loads and stores in issue
-  // order, so a wait for a poll issued after the flag store also waits for
-  // that store's write-through round trip (and for any BitSet word stores
-  // before it -- k_scan_select stores its words at the end, words_out)
-  int64_t in0 = 0, a0f = epoch << 32;
-  if ((dbg & 8) && wave == 0 && blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
   if (lane == 0) wcount[wave] = c;
   __syncthreads();
   int64_t bc = 0;
   for (int k = 0; k < NW; ++k) bc += wcount[k];
-  // the count is published by wave 1, not by the polling wave 0: each wave
-  // has its own vmcnt, and a wave's wait for a poll also waits for every
-  // store it issued before (the flag's write-through round trip)
-  if (threadIdx.x == 64) {
+  // The count is published by the LAST wave, which reads nothing back from
+  // global memory before the emission: vmcnt counts loads and stores in
+  // issue order, so any wave that waits for a load after the publishing
+  // store also waits for that store's write-through round trip (~1.5 us at
+  // C2).  Every value the look-back loads is therefore consumed inside
+  // branches the publishing wave does not take (the chained walk and its
+  // wave sum in wave 0; the polls in the other waves), and reaches the rest
+  // of the block through LDS.
+  constexpr int kPub = NW - 1;
+  constexpr int kPollers = 64 * (NW - 1);
+  constexpr int kPolls = (kLookbackBlocks + kPollers - 1) / kPollers;
+  if (threadIdx.x == 64 * kPub) {
     __hip_atomic_store(&lb[1 + (int64_t)blockIdx.x * fs], (epoch << 32) | bc, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     if (stamps) stamps[4 * blockIdx.x + 1] = wall_clock64();
   }
-  // look-back: the predecessors' counts, all polls of a thread in flight together
-  constexpr int kThreads = 64 * NW;
-  int64_t v[kLookbackBlocks / kThreads];
+  if (lane == 0) wpre[wave] = 0;
+  // look-back loads in flight before the staging: wave 0's first window of
+  // the chained walk, or every predecessor's count (one per polling thread)
+  int64_t in0 = 0, a0f = epoch << 32;
+  int64_t v[kPolls];
+  if (dbg & 8) {
+    if (wave == 0 && blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
+  } else if (wave != kPub) {
 #pragma unroll
-  for (int k = 0; k < kLookbackBlocks / kThreads; ++k) {
-    const int64_t j = (int64_t)k * kThreads + threadIdx.x;
-    if ((dbg & 8) || j >= (int64_t)blockIdx.x)
-      v[k] = epoch << 32;
-    else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
-      v[k] = __builtin_nontemporal_load(&lb[1 + j * fs]);
-    else
-      v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < kPolls; ++k) {
+      const int64_t j = (int64_t)k * kPollers + threadIdx.x;
+      if (j >= (int64_t)blockIdx.x)
+        v[k] = epoch << 32;
+      else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
+        v[k] = __builtin_nontemporal_load(&lb[1 + j * fs]);
+      else
+        v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   // meanwhile: stage the wave's leading steps together, load the first
   // kPrefetch x 64 rows' values
@@ -1678,35 +1685,41 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       }
     }
   }
-  int64_t pre = 0;
   if (dbg & 8) {
     // chained form: wave 0 walks back over its predecessors, 64 per round,
     // stops at the nearest one whose inclusive prefix is published and adds
-    // the counts after it; other waves contribute 0
-    if (wave == 0) pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
-  } else {
+    // the counts after it, and publishes this block's inclusive prefix at once
+    if (wave == 0) {
+      int64_t pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
 #pragma unroll
-  for (int k = 0; k < kLookbackBlocks / kThreads; ++k) {
-    const int64_t j = (int64_t)k * kThreads + threadIdx.x;
-    while (!(dbg & 2) && (v[k] >> 32) != epoch) {
-      if (dbg & 1)
-        __builtin_amdgcn_s_sleep(16);
-      else
-        __builtin_amdgcn_s_sleep(1);
-      v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
+      if (lane == 0) {
+        wpre[0] = pre;
+        __hip_atomic_store(&inc[blockIdx.x], (epoch << 32) | (pre + bc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
-    pre += v[k] & 0xffffffffll;
-  }
-  }
+  } else if (wave != kPub) {
+    int64_t pre = 0;
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
-  if (lane == 0) wpre[wave] = pre;
+    for (int k = 0; k < kPolls; ++k) {
+      const int64_t j = (int64_t)k * kPollers + threadIdx.x;
+      while (!(dbg & 2) && (v[k] >> 32) != epoch) {
+        if (dbg & 1)
+          __builtin_amdgcn_s_sleep(16);
+        else
+          __builtin_amdgcn_s_sleep(1);
+        v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      pre += v[k] & 0xffffffffll;
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
+    if (lane == 0) wpre[wave] = pre;
+  }
   __syncthreads();
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
   for (int k = 0; k < NW; ++k) off += wpre[k];
-  if ((dbg & 8) && threadIdx.x == 0)
-    __hip_atomic_store(&inc[blockIdx.x], (epoch << 32) | (off + bc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (blockIdx.x == gridDim.x - 1) {
     if (threadIdx.x == 0) {
       *total = off + bc;
@@ -1714,7 +1727,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     }
     // the flags of blocks this launch does not have carry its epoch too, so a
     // later, larger launch never finds a flag older than the previous launch
-    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += kThreads) {
+    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += 64 * NW) {
       lb[1 + j * fs] = epoch << 32;
       if (dbg & 8) inc[j] = epoch << 32;
     }
