@@ -1621,43 +1621,38 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   __syncthreads();
   int64_t bc = 0;
   for (int k = 0; k < NW; ++k) bc += wcount[k];
-  // The count is published by the LAST wave, which reads nothing back from
-  // global memory before the emission: vmcnt counts loads and stores in
-  // issue order, so any wave that waits for a load after the publishing
-  // store also waits for that store's write-through round trip (~1.5 us at
-  // C2).  Every value the look-back loads is therefore consumed inside
-  // branches the publishing wave does not take (the chained walk and its
-  // wave sum in wave 0; the polls in the other waves), and reaches the rest
-  // of the block through LDS.
+  // The count is published by the LAST wave, which then loads nothing until
+  // the emission: vmcnt counts loads and stores in issue order, so a wave
+  // that waits for anything after the publishing store also waits for that
+  // store's write-through round trip (~1.5 us at C2).  The compiler places
+  // waits wherever a register of a load that may be in flight on some path
+  // is touched, so no look-back load may be in flight on any path into code
+  // the publishing wave runs before the offset barrier: the staging comes
+  // first for every wave, the look-back loads are issued after it, in
+  // branches the publishing wave does not take, and consumed there; their
+  // result reaches the block through LDS.  The flag store itself is inline
+  // asm -- the write-through vector store the relaxed agent-scope atomic
+  // store compiles to -- with its address and data moved into VGPRs by an
+  // asm of their own and kept live to the end of the function, so no later
+  // write of those registers calls for a wait; the compiler does not count
+  // the store, and a wait it emits for its own operations can only wait
+  // longer (completion is in issue order), never less.
   constexpr int kPub = NW - 1;
   constexpr int kPollers = 64 * (NW - 1);
   constexpr int kPolls = (kLookbackBlocks + kPollers - 1) / kPollers;
-  if (threadIdx.x == 64 * kPub) {
-    __hip_atomic_store(&lb[1 + (int64_t)blockIdx.x * fs], (epoch << 32) | bc, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    if (stamps) stamps[4 * blockIdx.x + 1] = wall_clock64();
-  }
-  if (lane == 0) wpre[wave] = 0;
-  // look-back loads in flight before the staging: wave 0's first window of
-  // the chained walk, or every predecessor's count (one per polling thread)
-  int64_t in0 = 0, a0f = epoch << 32;
-  int64_t v[kPolls];
-  if (dbg & 8) {
-    if (wave == 0 && blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
-  } else if (wave != kPub) {
-#pragma unroll
-    for (int k = 0; k < kPolls; ++k) {
-      const int64_t j = (int64_t)k * kPollers + threadIdx.x;
-      if (j >= (int64_t)blockIdx.x)
-        v[k] = epoch << 32;
-      else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
-        v[k] = __builtin_nontemporal_load(&lb[1 + j * fs]);
-      else
-        v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int64_t* flag_at = nullptr;
+  int64_t flag = 0;
+  if (wave == kPub) {
+    flag_at = &lb[1 + (int64_t)blockIdx.x * fs];
+    flag = (epoch << 32) | bc;
+    asm volatile("" : "+v"(flag_at), "+v"(flag));
+    if (lane == 0) {
+      asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(flag_at), "v"(flag) : "memory");
+      wpre[kPub] = 0;
     }
   }
-  // meanwhile: stage the wave's leading steps together, load the first
-  // kPrefetch x 64 rows' values
+  // the wave's leading steps staged together, the first kPrefetch x 64
+  // rows' values loaded
   uint16_t* const st = stage[wave];
   uint32_t tot = 0;  // staged positions (offsets from bit 0 of word a0: < 8 x 4096)
   int nst = 0;       // steps staged
@@ -1685,11 +1680,16 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       }
     }
   }
-  if (dbg & 8) {
+  if (wave == kPub) {
+  } else if (dbg & 8) {
     // chained form: wave 0 walks back over its predecessors, 64 per round,
     // stops at the nearest one whose inclusive prefix is published and adds
-    // the counts after it, and publishes this block's inclusive prefix at once
+    // the counts after it, and publishes this block's inclusive prefix at
+    // once; the other waves contribute 0
+    if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
     if (wave == 0) {
+      int64_t in0 = 0, a0f = epoch << 32;
+      if (blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
       int64_t pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
 #pragma unroll
       for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
@@ -1697,8 +1697,24 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
         wpre[0] = pre;
         __hip_atomic_store(&inc[blockIdx.x], (epoch << 32) | (pre + bc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+    } else if (lane == 0) {
+      wpre[wave] = 0;
     }
-  } else if (wave != kPub) {
+  } else {
+    // polling form: every predecessor's count, one per thread of the other
+    // waves, all in flight together
+    if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
+    int64_t v[kPolls];
+#pragma unroll
+    for (int k = 0; k < kPolls; ++k) {
+      const int64_t j = (int64_t)k * kPollers + threadIdx.x;
+      if (j >= (int64_t)blockIdx.x)
+        v[k] = epoch << 32;
+      else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
+        v[k] = __builtin_nontemporal_load(&lb[1 + j * fs]);
+      else
+        v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     int64_t pre = 0;
 #pragma unroll
     for (int k = 0; k < kPolls; ++k) {
@@ -1789,6 +1805,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     __syncthreads();
     if (threadIdx.x == 0) stamps[4 * blockIdx.x + 3] = wall_clock64();
   }
+  asm volatile("" ::"v"(flag_at), "v"(flag));  // the flag store's registers, live to here
 }
 
 template <int G4, int NB, class GT = Gather4>
