@@ -1626,43 +1626,33 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // that waits for anything after the publishing store also waits for that
   // store's write-through round trip (~1.5 us at C2).  The compiler places
   // waits wherever a register of a load that may be in flight on some path
-  // is touched, so no look-back load may be in flight on any path into code
-  // the publishing wave runs before the offset barrier: the staging comes
-  // first for every wave, the look-back loads are issued after it, in
-  // branches the publishing wave does not take, and consumed there; their
-  // result reaches the block through LDS.  The flag store itself is inline
-  // asm -- the write-through vector store the relaxed agent-scope atomic
-  // store compiles to -- with its address and data moved into VGPRs by an
-  // asm of their own and kept live to the end of the function, so no later
-  // write of those registers calls for a wait; the compiler does not count
-  // the store, and a wait it emits for its own operations can only wait
-  // longer (completion is in issue order), never less.
+  // is touched, so the publishing wave runs no code shared with the
+  // look-back before the offset barrier: it stages its steps in a copy of
+  // its own (a constant LDS base: the copies cannot be merged), while the
+  // other waves have their look-back loads in flight during their staging
+  // and consume them in their own branch; the result reaches the block
+  // through LDS.  The flag store itself is inline asm -- the write-through
+  // vector store the relaxed agent-scope atomic store compiles to -- with
+  // its address and data moved into VGPRs by an asm of their own and kept
+  // live to the end of the function, so no later write of those registers
+  // calls for a wait; the compiler does not count the store, and a wait it
+  // emits for its own operations can only wait longer (completion is in
+  // issue order), never less.
   constexpr int kPub = NW - 1;
   constexpr int kPollers = 64 * (NW - 1);
   constexpr int kPolls = (kLookbackBlocks + kPollers - 1) / kPollers;
-  int64_t* flag_at = nullptr;
-  int64_t flag = 0;
-  if (wave == kPub) {
-    flag_at = &lb[1 + (int64_t)blockIdx.x * fs];
-    flag = (epoch << 32) | bc;
-    asm volatile("" : "+v"(flag_at), "+v"(flag));
-    if (lane == 0) {
-      asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(flag_at), "v"(flag) : "memory");
-      wpre[kPub] = 0;
-    }
-  }
-  // the wave's leading steps staged together, the first kPrefetch x 64
-  // rows' values loaded
-  uint16_t* const st = stage[wave];
   uint32_t tot = 0;  // staged positions (offsets from bit 0 of word a0: < 8 x 4096)
   int nst = 0;       // steps staged
   constexpr int kPrefetch = prefetch_rows<G4>();
   uint32_t pv[kPrefetch > 0 ? kPrefetch : 1][G4 > 0 ? G4 : 1];
-  if (cached) {
+  // the wave's leading steps staged together, the first kPrefetch x 64
+  // rows' values loaded
+  auto stage_leading = [&](uint16_t* const sw) {
+    if (!cached) return;
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       if (a0 + r * 64 >= a1) break;
-      const StepScan q = stage_step(wr[r], st, lane, tot, (uint32_t)r * 4096u);
+      const StepScan q = stage_step(wr[r], sw, lane, tot, (uint32_t)r * 4096u);
       if (tot + q.total > kStageIds) break;
       tot += q.total;
       nst = r + 1;
@@ -1672,24 +1662,40 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       for (int k = 0; k < kPrefetch; ++k) {
         const uint32_t i = (uint32_t)lane + 64u * k;
         if (i < tot) {
-          const int64_t p = a0 * 64 + st[i];
+          const int64_t p = a0 * 64 + sw[i];
 #pragma unroll
           for (int g = 0; g < G4; ++g)
             if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p * G.stride[g]];
         }
       }
     }
-  }
+  };
+  int64_t* flag_at = nullptr;
+  int64_t flag = 0;
   if (wave == kPub) {
+    flag_at = &lb[1 + (int64_t)blockIdx.x * fs];
+    flag = (epoch << 32) | bc;
+    asm volatile("" : "+v"(flag_at), "+v"(flag));
+    // vmcnt(0) before the flag: free (nothing of this wave is in flight here
+    // but a diagnostic stamp), and the compiler then counts nothing in flight
+    // on this path, so it places no wait after the flag
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+    if (lane == 0) {
+      asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(flag_at), "v"(flag) : "memory");
+      wpre[kPub] = 0;
+    }
+    stage_leading(stage[kPub]);
   } else if (dbg & 8) {
-    // chained form: wave 0 walks back over its predecessors, 64 per round,
-    // stops at the nearest one whose inclusive prefix is published and adds
-    // the counts after it, and publishes this block's inclusive prefix at
-    // once; the other waves contribute 0
+    // chained form: wave 0 walks back over its predecessors, 64 per round
+    // (the first window in flight during its staging), stops at the nearest
+    // one whose inclusive prefix is published and adds the counts after it,
+    // and publishes this block's inclusive prefix at once; the other waves
+    // contribute 0
     if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
+    int64_t in0 = 0, a0f = epoch << 32;
+    if (wave == 0 && blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
+    stage_leading(stage[wave]);
     if (wave == 0) {
-      int64_t in0 = 0, a0f = epoch << 32;
-      if (blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
       int64_t pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
 #pragma unroll
       for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
@@ -1702,7 +1708,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     }
   } else {
     // polling form: every predecessor's count, one per thread of the other
-    // waves, all in flight together
+    // waves, all in flight during their staging
     if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
     int64_t v[kPolls];
 #pragma unroll
@@ -1715,6 +1721,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       else
         v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    stage_leading(stage[wave]);
     int64_t pre = 0;
 #pragma unroll
     for (int k = 0; k < kPolls; ++k) {
@@ -1732,6 +1739,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
     if (lane == 0) wpre[wave] = pre;
   }
+  uint16_t* const st = stage[wave];
   __syncthreads();
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
@@ -2485,10 +2493,12 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
   const int nw = waves == 16 ? 16 : kWaves;
   const int64_t nseg = grid_blocks(L.nrows, L.tiles_per_block);
   const int64_t g = (nseg + nw / kWaves - 1) / (nw / kWaves);
-  // the chained look-back (32-bit inclusive prefixes: tables < 2^32 rows),
-  // or (select_dbg bit 7) every predecessor's count polled, one flag per
-  // flag_stride int64 words (the chained walk needs them packed)
-  dbg = (dbg & ~8) | (!(dbg & 8) ? 8 : 0);
+  // every predecessor's count polled (<= 256 blocks: one poll per thread of
+  // 15 waves), one flag per 128-byte line (flag_stride kFlagStride, the
+  // default: the polls of all blocks do not queue on a few lines) -- C2
+  // 11.8-12.1 us vs 13.4-13.6 for the chained walk and 12.0-12.2 with the
+  // flags packed (profiles/r04/f1); select_dbg bit 7: the chained walk
+  // (32-bit inclusive prefixes: tables < 2^32 rows)
   const int32_t fs = (dbg & 8) || flag_stride != kFlagStride ? 1 : kFlagStride;
   const bool del = L.deleted != nullptr;
   const bool ir = L.int_range != 0;  // branch-free int terms (every fused plan qualifies; the knob can turn it off)

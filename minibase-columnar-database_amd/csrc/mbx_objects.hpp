@@ -58,7 +58,7 @@ struct MbxTuning {
   int32_t cursor_prefetch = 1;    // MBX_CURSOR_PREFETCH: 0 = mbx_cursor_next copies each batch on demand
   int32_t scan_select_fused = 1;  // MBX_SCAN_SELECT_FUSED: 1 = BitSet + positions in one launch (k_scan_select)
   int32_t scan_select_waves = 16; // MBX_SCAN_SELECT_WAVES: waves per k_scan_select block (4 or 16)
-  int32_t select_flag_stride = 1; // MBX_SELECT_FLAG_STRIDE: 1, or 16 = the polling look-back's flags one per line
+  int32_t select_flag_stride = 16; // MBX_SELECT_FLAG_STRIDE: 16 = k_scan_select's polled flags one per line, or 1
   int32_t scan_words_wt = 1;      // MBX_SCAN_WORDS_WT: BitSet scan words stored write-through
   int32_t comm_same_stream = 1;   // MBX_COMM_SAME_STREAM: collectives on the context stream (0: the exchange stream)
   int32_t select_dbg = 0;         // MBX_SELECT_DBG: bit 3 per-block stamps, 128 every-predecessor poll

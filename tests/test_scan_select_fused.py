@@ -119,7 +119,7 @@ def test_fused_c2_full_size_launch_after_launch(ctx):
     g.close()
 
 
-LOOKBACK = {"chained": (0, 1), "poll": (128, 1), "poll_spread": (128, 16)}
+LOOKBACK = {"poll_spread": (0, 16), "poll": (0, 1), "chained": (128, 1)}
 
 
 @pytest.mark.parametrize("lookback", list(LOOKBACK))

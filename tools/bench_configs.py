@@ -172,10 +172,11 @@ def main():
         wpos = torch.nonzero(cols[0] < 104858).flatten()
         # both forms, interleaved: the BitSet scan + compaction (two launches)
         # and k_scan_select (one launch, knob scan_select_fused)
-        # and the one launch with the polling look-back (select_dbg 128),
-        # flags packed or one per 128-byte line (select_flag_stride 16)
+        # (its default look-back: every predecessor polled, one flag per
+        # 128-byte line), with the flags packed (select_flag_stride 1) and
+        # with the chained walk (select_dbg 128)
         forms = {}
-        variants = {0: (0, 0, 1), 1: (1, 0, 1), "poll": (1, 128, 1), "poll_spread": (1, 128, 16)}
+        variants = {0: (0, 0, 16), 1: (1, 0, 16), "poll_packed": (1, 0, 1), "chained": (1, 128, 1)}
         for rep in range(3):
             for key, (fused, dbg, fs) in variants.items():
                 ctx.set_tuning("scan_select_fused", fused)
@@ -194,7 +195,7 @@ def main():
             ntiles = -(-n // 256)
             tpb = max(4, -(-ntiles // 1024))
             nb = -(-(-(-ntiles // tpb)) // 4)  # 16-wave blocks of 4 BitSet segments
-            for key in (1, "poll", "poll_spread"):
+            for key in (1, "poll_packed", "chained"):
                 ctx.set_tuning("scan_select_fused", 1)
                 ctx.set_tuning("select_flag_stride", variants[key][2])
                 ctx.set_tuning("select_dbg", 8 | variants[key][1])
@@ -227,7 +228,8 @@ def main():
         emit({"config": "C2", "rows": n, "gpus": 1, "selected": got, "ms_per_query": ms, "rows_per_s": n / ms * 1e3,
               "form": "one launch (k_scan_select)" if fused_default else "two launches (BitSet scan + k_select_ids)",
               "ms_per_query_two_launch": forms[0], "ms_per_query_one_launch": forms[1],
-              "ms_per_query_one_launch_poll": forms["poll"], "ms_per_query_one_launch_poll_spread": forms["poll_spread"],
+              "ms_per_query_one_launch_flags_packed": forms["poll_packed"],
+              "ms_per_query_one_launch_chained": forms["chained"],
               "stamps_us": stamps,
               "graph_replay_ms_per_query": graph_ms,
               "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
@@ -240,7 +242,7 @@ def main():
             bmt = ctx.bitmap_alloc(n)
             res = {}
             for rep in range(3):
-                for key in (1, "poll_spread"):
+                for key in (1, "chained"):
                     ctx.set_tuning("scan_select_fused", 1)
                     ctx.set_tuning("select_dbg", variants[key][1])
                     ctx.set_tuning("select_flag_stride", variants[key][2])
