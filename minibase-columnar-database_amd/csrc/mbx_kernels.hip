@@ -1626,50 +1626,20 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // that waits for anything after the publishing store also waits for that
   // store's write-through round trip (~1.5 us at C2).  The compiler places
   // waits wherever a register of a load that may be in flight on some path
-  // is touched, so the publishing wave runs no code shared with the
-  // look-back before the offset barrier: it stages its steps in a copy of
-  // its own (a constant LDS base: the copies cannot be merged), while the
-  // other waves have their look-back loads in flight during their staging
-  // and consume them in their own branch; the result reaches the block
-  // through LDS.  The flag store itself is inline asm -- the write-through
-  // vector store the relaxed agent-scope atomic store compiles to -- with
-  // its address and data moved into VGPRs by an asm of their own and kept
-  // live to the end of the function, so no later write of those registers
-  // calls for a wait; the compiler does not count the store, and a wait it
-  // emits for its own operations can only wait longer (completion is in
-  // issue order), never less.
+  // is touched, so no look-back load may be in flight on any path into code
+  // the publishing wave runs before the offset barrier: the staging comes
+  // first for every wave, the look-back loads are issued after it, in
+  // branches the publishing wave does not take, and consumed there; their
+  // result reaches the block through LDS.  The flag store itself is inline
+  // asm -- the write-through vector store the relaxed agent-scope atomic
+  // store compiles to -- with its address and data moved into VGPRs by an
+  // asm of their own and kept live to the end of the function, so no later
+  // write of those registers calls for a wait; the compiler does not count
+  // the store, and a wait it emits for its own operations can only wait
+  // longer (completion is in issue order), never less.
   constexpr int kPub = NW - 1;
   constexpr int kPollers = 64 * (NW - 1);
   constexpr int kPolls = (kLookbackBlocks + kPollers - 1) / kPollers;
-  uint32_t tot = 0;  // staged positions (offsets from bit 0 of word a0: < 8 x 4096)
-  int nst = 0;       // steps staged
-  constexpr int kPrefetch = prefetch_rows<G4>();
-  uint32_t pv[kPrefetch > 0 ? kPrefetch : 1][G4 > 0 ? G4 : 1];
-  // the wave's leading steps staged together, the first kPrefetch x 64
-  // rows' values loaded
-  auto stage_leading = [&](uint16_t* const sw) {
-    if (!cached) return;
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      if (a0 + r * 64 >= a1) break;
-      const StepScan q = stage_step(wr[r], sw, lane, tot, (uint32_t)r * 4096u);
-      if (tot + q.total > kStageIds) break;
-      tot += q.total;
-      nst = r + 1;
-    }
-    if constexpr (G4 != kWide) {
-#pragma unroll
-      for (int k = 0; k < kPrefetch; ++k) {
-        const uint32_t i = (uint32_t)lane + 64u * k;
-        if (i < tot) {
-          const int64_t p = a0 * 64 + sw[i];
-#pragma unroll
-          for (int g = 0; g < G4; ++g)
-            if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p * G.stride[g]];
-        }
-      }
-    }
-  };
   int64_t* flag_at = nullptr;
   int64_t flag = 0;
   if (wave == kPub) {
@@ -1684,18 +1654,46 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(flag_at), "v"(flag) : "memory");
       wpre[kPub] = 0;
     }
-    stage_leading(stage[kPub]);
+  }
+  // the wave's leading steps staged together, the first kPrefetch x 64
+  // rows' values loaded
+  uint16_t* const st = stage[wave];
+  uint32_t tot = 0;  // staged positions (offsets from bit 0 of word a0: < 8 x 4096)
+  int nst = 0;       // steps staged
+  constexpr int kPrefetch = prefetch_rows<G4>();
+  uint32_t pv[kPrefetch > 0 ? kPrefetch : 1][G4 > 0 ? G4 : 1];
+  if (cached) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      if (a0 + r * 64 >= a1) break;
+      const StepScan q = stage_step(wr[r], st, lane, tot, (uint32_t)r * 4096u);
+      if (tot + q.total > kStageIds) break;
+      tot += q.total;
+      nst = r + 1;
+    }
+    if constexpr (G4 != kWide) {
+#pragma unroll
+      for (int k = 0; k < kPrefetch; ++k) {
+        const uint32_t i = (uint32_t)lane + 64u * k;
+        if (i < tot) {
+          const int64_t p = a0 * 64 + st[i];
+#pragma unroll
+          for (int g = 0; g < G4; ++g)
+            if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p * G.stride[g]];
+        }
+      }
+    }
+  }
+  if (wave == kPub) {
   } else if (dbg & 8) {
-    // chained form: wave 0 walks back over its predecessors, 64 per round
-    // (the first window in flight during its staging), stops at the nearest
-    // one whose inclusive prefix is published and adds the counts after it,
-    // and publishes this block's inclusive prefix at once; the other waves
-    // contribute 0
+    // chained form: wave 0 walks back over its predecessors, 64 per round,
+    // stops at the nearest one whose inclusive prefix is published and adds
+    // the counts after it, and publishes this block's inclusive prefix at
+    // once; the other waves contribute 0
     if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
-    int64_t in0 = 0, a0f = epoch << 32;
-    if (wave == 0 && blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
-    stage_leading(stage[wave]);
     if (wave == 0) {
+      int64_t in0 = 0, a0f = epoch << 32;
+      if (blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
       int64_t pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
 #pragma unroll
       for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
@@ -1708,7 +1706,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     }
   } else {
     // polling form: every predecessor's count, one per thread of the other
-    // waves, all in flight during their staging
+    // waves, all in flight together
     if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
     int64_t v[kPolls];
 #pragma unroll
@@ -1721,7 +1719,6 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       else
         v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    stage_leading(stage[wave]);
     int64_t pre = 0;
 #pragma unroll
     for (int k = 0; k < kPolls; ++k) {
@@ -1739,22 +1736,16 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
     if (lane == 0) wpre[wave] = pre;
   }
-  uint16_t* const st = stage[wave];
   __syncthreads();
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
   for (int k = 0; k < NW; ++k) off += wpre[k];
-  if (blockIdx.x == gridDim.x - 1) {
-    if (threadIdx.x == 0) {
-      *total = off + bc;
-      lb[0] = epoch;
-    }
-    // the flags of blocks this launch does not have carry its epoch too, so a
-    // later, larger launch never finds a flag older than the previous launch
-    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += 64 * NW) {
-      lb[1 + j * fs] = epoch << 32;
-      if (dbg & 8) inc[j] = epoch << 32;
-    }
+  // the last block: the total, and the epoch the next launch starts from
+  // (every block has read it: the last block's offset needs every other
+  // block's count)
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+    *total = off + bc;
+    lb[0] = epoch;
   }
   // a block whose rows would end past the outputs' capacity writes none of
   // them: the caller sees *total > cap and fails, with nothing out of bounds
@@ -1807,6 +1798,16 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       int64_t sc = 0;
       for (int k = 0; k < kWaves; ++k) sc += wcount[threadIdx.x * kWaves + k];
       segc[sg] = sc;
+    }
+  }
+  // the flags of blocks this launch does not have carry its epoch too, so a
+  // later, larger launch never finds a flag older than the previous launch:
+  // written by block 0 after its rows (it waits for no predecessor; the last
+  // block, which did this before, ends the kernel)
+  if (blockIdx.x == 0) {
+    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += 64 * NW) {
+      lb[1 + j * fs] = epoch << 32;
+      if (dbg & 8) inc[j] = epoch << 32;
     }
   }
   if (stamps) {
