@@ -427,6 +427,10 @@ int mbx_set_tuning(mbx_ctx *ctx, const char *knob, int64_t value);
  * end) of the last compaction launched with select_dbg bit 3: 4 * nblocks
  * int64 into host (diagnostic of DESIGN.md section 5) */
 int mbx_diag_select_stamps(mbx_ctx *ctx, int64_t *host, int64_t nblocks);
+/* the epoch the next one-launch selection (k_scan_select / k_cnf_select)
+ * counts from (the look-back words' lb[0], 0 .. 2^31 - 1): lets a test run
+ * launches across the epoch wrap (diagnostic of DESIGN.md section 3) */
+int mbx_diag_lookback_epoch(mbx_ctx *ctx, int64_t epoch);
 
 #ifdef __cplusplus
 }

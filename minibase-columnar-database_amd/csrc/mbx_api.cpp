@@ -1770,6 +1770,15 @@ extern "C" int mbx_diag_select_stamps(mbx_ctx* c, int64_t* host, int64_t nblocks
   return MBX_OK;
 }
 
+extern "C" int mbx_diag_lookback_epoch(mbx_ctx* c, int64_t epoch) {
+  NOTNULL(c);
+  if (epoch < 0 || epoch > 0x7fffffff) return fail(MBX_E_INVALID, "diag_lookback_epoch: %lld", (long long)epoch);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(c->lookback, &epoch, sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return MBX_OK;
+}
+
 static int64_t col_bytes(const mbx_table* t, int32_t j) {
   const TCol& tc = t->cols[(size_t)j];
   return (int64_t)tc.stride_w * 4;

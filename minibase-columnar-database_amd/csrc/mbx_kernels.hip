@@ -1516,13 +1516,13 @@ __global__ __launch_bounds__(kBlock) void k_select_ids(const uint64_t* __restric
 // look-back resolves: the look-back's round trips overlap those gathers, and
 // a sparse wave (C4: ~250 rows) needs one gather round trip, not one per
 // 64-word step.
-// lb[0] = the epoch of the previous launch; lb[1 + b] = epoch << 32 | count
-// of block b (the last block stamps the flags past the grid too).  Every
-// launch's epoch differs from the stale flags it finds (they carry the
-// previous launch's), so nothing is cleared between launches (graph replays included: the epoch
-// is read from lb[0], not baked into the launch); the last block, having
-// seen every other block's flag (so every block has read lb[0]), stores the
-// new epoch.
+// lb[0] = the epoch of the previous launch; lb[1 + b * fs] = epoch << 32 |
+// count of block b.  Every launch's epoch differs from the stale flags it
+// finds (they carry earlier launches' epochs; the words are set back to
+// epoch 0 around the wrap, select_tail), so nothing is cleared between
+// launches (graph replays included: the epoch is read from lb[0], not baked
+// into the launch); the last block, having seen every other block's flag (so
+// every block has read lb[0]), stores the new epoch.
 constexpr int kLookbackBlocks = 4 * kBlock;  // one poll load per thread per 256 predecessors
 // staged rows per lane whose values load before the look-back: 6 x 64 covers
 // a 1 % wave of ~245 rows with 9 sd to spare; 4 columns hold fewer (occupancy)
@@ -1800,14 +1800,20 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       segc[sg] = sc;
     }
   }
-  // the flags of blocks this launch does not have carry its epoch too, so a
-  // later, larger launch never finds a flag older than the previous launch:
-  // written by block 0 after its rows (it waits for no predecessor; the last
-  // block, which did this before, ends the kernel)
-  if (blockIdx.x == 0) {
-    for (int64_t j = (int64_t)gridDim.x + threadIdx.x; j < kLookbackBlocks; j += 64 * NW) {
-      lb[1 + j * fs] = epoch << 32;
-      if (dbg & 8) inc[j] = epoch << 32;
+  // Epochs run 1 .. 2^31 - 1 and wrap, every launch of either kernel on this
+  // look-back buffer taking the next one, so a word can only be mistaken for
+  // this launch's if it was written exactly one cycle earlier and never
+  // since.  The last two launches before the wrap (their last block, once
+  // its offset -- i.e. every other block's count -- is known) set every
+  // word they do not use back to epoch 0, which no launch has: by induction
+  // no word holds the epoch of a launch before that launch writes it.
+  if (blockIdx.x == gridDim.x - 1 && epoch >= 0x7ffffffe) {
+    for (int64_t w = 1 + threadIdx.x; w < kLookbackWords; w += 64 * NW) {
+      const int64_t x = w - 1;
+      const bool live = (dbg & 8) ? (x < (int64_t)gridDim.x ||
+                                     (x >= kLookbackBlocks && x - kLookbackBlocks < (int64_t)gridDim.x))
+                                  : (x % fs == 0 && x / fs < (int64_t)gridDim.x);
+      if (!live) lb[w] = 0;
     }
   }
   if (stamps) {

@@ -90,7 +90,7 @@ EXPORTS = [
     "mbx_bitmap_select", "mbx_materialize", "mbx_materialize_async", "mbx_cursor_open", "mbx_cursor_count",
     "mbx_cursor_next", "mbx_cursor_next_view", "mbx_cursor_restart", "mbx_cursor_close", "mbx_cursor_stats", "mbx_cnf_cursor_open", "mbx_cnf_cursor_launch",
     "mbx_probe_read", "mbx_set_tuning",
-    "mbx_diag_select_stamps", "mbx_dev_alloc", "mbx_dev_free", "mbx_dev_download", "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
+    "mbx_diag_select_stamps", "mbx_diag_lookback_epoch", "mbx_dev_alloc", "mbx_dev_free", "mbx_dev_download", "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
     "mbx_comm_info", "mbx_comm_wait", "mbx_comm_allreduce_count_async", "mbx_comm_scan_count_async",
     "mbx_comm_allreduce_agg_async",
     "mbx_comm_allgather_count_async", "mbx_comm_allreduce_count_all", "mbx_comm_allreduce_agg_all",
@@ -182,6 +182,7 @@ def lib():
         "mbx_probe_read": ([V, V, P(I32), I32, I64, I32, I64], ctypes.c_int),
         "mbx_set_tuning": ([V, ctypes.c_char_p, I64], ctypes.c_int),
         "mbx_diag_select_stamps": ([V, V, I64], ctypes.c_int),
+        "mbx_diag_lookback_epoch": ([V, I64], ctypes.c_int),
         "mbx_dev_alloc": ([V, I64, P(V)], ctypes.c_int),
         "mbx_dev_free": ([V, V], ctypes.c_int),
         "mbx_dev_download": ([V, V, V, I64], ctypes.c_int),

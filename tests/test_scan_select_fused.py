@@ -204,3 +204,30 @@ def test_fused_100m_rows_large_segments(ctx):
     bm, ids, k = run_async(ctx, plan, n)
     assert k == n_o and np.array_equal(ids, ids_o)
     assert np.array_equal(bm.download(), w_o)
+
+
+@pytest.mark.parametrize("lookback", list(LOOKBACK))
+def test_lookback_epoch_wrap(m, ctx, tune, lookback):
+    """Launches across the look-back epoch's wrap (2^31 - 1 -> 1), k_scan_select
+    (every look-back form) alternating with k_cnf_select at different grid
+    sizes: the words set back to epoch 0 by the last two launches before the
+    wrap leave no stale flag that a later launch could take for its own."""
+    tune("select_dbg", LOOKBACK[lookback][0])
+    tune("select_flag_stride", LOOKBACK[lookback][1])
+    runs = []
+    for n in (3_000_017, 100_003, 1_000_003):
+        cols = int_cols(n, hi=10, seed=n)
+        t = ctx.stage(cols)
+        bms = ctx.index_build(t, 2, [("int", v) for v in range(10)])
+        runs.append((n, cols, t, bms))
+    m.mbx._chk(m.lib().mbx_diag_lookback_epoch(ctx.h, 0x7FFFFFFF - 5))
+    for _ in range(4):  # 12 launches of each kernel: through the wrap and well past it
+        for n, cols, t, bms in runs:
+            c0 = np.asarray(cols[0][2])
+            plan = ctx.compile(t, [[(oracle.LT, ("sym", 1), ("int", 4))]])
+            bm, ids, k = run_async(ctx, plan, n)
+            assert np.array_equal(ids, np.nonzero(c0 < 4)[0]), n
+            cur = ctx.cnf_cursor(t, [[bms[3], bms[5]]], [0])
+            want = np.nonzero(np.isin(np.asarray(cols[2][2]), [3, 5]))[0]
+            got, (v0,) = cur.next(max(1, n))
+            assert np.array_equal(got, want) and np.array_equal(v0, c0[want]), n
