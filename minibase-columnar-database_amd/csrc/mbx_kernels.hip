@@ -1619,8 +1619,17 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
   if (lane == 0) wcount[wave] = c;
   __syncthreads();
-  int64_t bc = 0;
-  for (int k = 0; k < NW; ++k) bc += wcount[k];
+  // the block's count and this wave's offset within it, read now (every
+  // count unrolled, the loads in flight together) rather than after the
+  // offset barrier, where a loop over the lower waves' counts was a chain
+  // of dependent LDS round trips on every wave's critical path
+  int64_t bc = 0, wpos = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int64_t x = wcount[k];
+    bc += x;
+    wpos += k < wave ? x : 0;
+  }
   // The count is published by the LAST wave, which then loads nothing until
   // the emission: vmcnt counts loads and stores in issue order, so a wave
   // that waits for anything after the publishing store also waits for that
@@ -1739,6 +1748,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   __syncthreads();
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
   int64_t off = 0;
+#pragma unroll
   for (int k = 0; k < NW; ++k) off += wpre[k];
   // the last block: the total, and the epoch the next launch starts from
   // (every block has read it: the last block's offset needs every other
@@ -1750,7 +1760,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // a block whose rows would end past the outputs' capacity writes none of
   // them: the caller sees *total > cap and fails, with nothing out of bounds
   const bool fits = off + bc <= G.cap;
-  for (int k = 0; k < wave; ++k) off += wcount[k];
+  off += wpos;
   const bool wt = (G4 == 0) != ((dbg & 32) != 0);
   if (!fits) {
   } else if (cached) {
