@@ -39,7 +39,7 @@ constexpr int kMaxProj = 16;
 #ifdef MBX_DIAG
 constexpr int32_t kDiagDbg = ~0;
 #else
-constexpr int32_t kDiagDbg = ~(1 | 2 | 4);
+constexpr int32_t kDiagDbg = ~(1 | 2 | 4 | 64);
 #endif
 
 enum ColKind : int32_t { kInt = 0, kReal = 1, kStr = 2 };

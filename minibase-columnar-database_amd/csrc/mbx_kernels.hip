@@ -620,7 +620,21 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
                                            int lane, const GT& G, uint32_t first = 0, bool wt = false) {
   if (r.total == 0) return;
   const int64_t lbase = base * 64;  // table-local row of bit 0 of word `base`
-  if (r.total <= kStageIds) {
+  if (r.total <= kStageIds && G4 == 0) {
+    // positions only: 4 staged positions per lane read together, then
+    // their 4 stores (one LDS round trip per 256 positions, not per 64)
+    for (uint32_t i0 = first + lane; i0 < r.total; i0 += 256) {
+      uint32_t q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = i0 + 64u * u < r.total ? st[i0 + 64u * u] : 0u;
+      if (ids) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (i0 + 64u * u < r.total) put(&ids[off + i0 + 64u * u], row_offset + lbase + q[u], wt);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next step
+  } else if (r.total <= kStageIds) {
     // staged positions from `first` on (the caller wrote those below it)
     for (uint32_t i0 = first + lane; i0 < r.total; i0 += 128) {
       const uint32_t i1 = i0 + 64;
@@ -1759,7 +1773,9 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   }
   // a block whose rows would end past the outputs' capacity writes none of
   // them: the caller sees *total > cap and fails, with nothing out of bounds
-  const bool fits = off + bc <= G.cap;
+  // (dbg bit 6, -DMBX_DIAG builds: no positions written -- the emission's
+  // cost, for the C2 anatomy)
+  const bool fits = off + bc <= G.cap && !(dbg & 64);
   off += wpos;
   const bool wt = (G4 == 0) != ((dbg & 32) != 0);
   if (!fits) {
