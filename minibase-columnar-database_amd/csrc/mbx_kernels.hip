@@ -1678,6 +1678,10 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       wpre[kPub] = 0;
     }
   }
+  if (dbg & 128) {  // diagnostic: the count only (wrong output by design)
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) lb[0] = epoch;
+    return;
+  }
   // the wave's leading steps staged together, the first kPrefetch x 64
   // rows' values loaded
   uint16_t* const st = stage[wave];
@@ -1685,7 +1689,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   int nst = 0;       // steps staged
   constexpr int kPrefetch = prefetch_rows<G4>();
   uint32_t pv[kPrefetch > 0 ? kPrefetch : 1][G4 > 0 ? G4 : 1];
-  if (cached) {
+  if (cached && !(dbg & 16)) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       if (a0 + r * 64 >= a1) break;
@@ -1775,7 +1779,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // them: the caller sees *total > cap and fails, with nothing out of bounds
   // (dbg bit 6, -DMBX_DIAG builds: no positions written -- the emission's
   // cost, for the C2 anatomy)
-  const bool fits = off + bc <= G.cap && !(dbg & 64);
+  const bool fits = off + bc <= G.cap && !(dbg & (64 | 16));
   off += wpos;
   const bool wt = (G4 == 0) != ((dbg & 32) != 0);
   if (!fits) {
@@ -1811,7 +1815,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
                         wt);
   }
   // the BitSet (k_scan_select): its words and one segment count per 4 waves
-  if (words_out) {
+  if (words_out && !(dbg & 256)) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       const int64_t wd = a0 + r * 64 + lane;

@@ -64,10 +64,13 @@ def main():
         return a.elapsed_time(b) / args.steps * 1e3
 
     # select_dbg values (k_scan_select gets select_dbg >> 4): 0 the default;
-    # 32 skips the look-back's wait; 1024 skips the positions; 512 plain
-    # (not write-through) positions; 128 the chained walk
+    # 32 skips the look-back's wait; 1024 skips the positions; 256 skips the
+    # staging (and so the positions); 4096 skips the BitSet words; 2048 ends
+    # every block once its count is published; 512 plain (not
+    # write-through) positions; 128 the chained walk
     variants = {"default": 0, "no_lookback_wait": 32, "no_positions": 1024, "neither": 32 | 1024,
-                "plain_stores": 512, "chained": 128}
+                "no_staging": 256, "no_words": 4096, "no_staging_no_words": 256 | 4096,
+                "count_only": 2048, "plain_stores": 512, "chained": 128}
     res = {}
     for rep in range(3):
         for k, v in variants.items():
