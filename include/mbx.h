@@ -420,7 +420,7 @@ int mbx_probe_read(mbx_ctx *ctx, const mbx_table *t, const int32_t *cols, int32_
  * counterpart.  mbx_init reads their MBX_* environment defaults once; no
  * launch reads the environment.  knob: "tiles_per_block", "force_generic",
  * "scan_hoist", "scan_ri", "sink_lds", "ticket_groups", "fin_mode",
- * "join_plain", "distinct_lds_probes", "gather_fused", "select_blocks", "select_dbg", "cursor_prefetch", "scan_select_fused", "scan_select_waves", "select_flag_stride", "select_flag_copies"; "reset"
+ * "join_plain", "distinct_lds_probes", "gather_fused", "select_blocks", "select_dbg", "cursor_prefetch", "scan_select_fused", "scan_select_waves", "select_flag_stride"; "reset"
  * restores the defaults. */
 int mbx_set_tuning(mbx_ctx *ctx, const char *knob, int64_t value);
 /* per-block wall_clock64() stamps (start, loads in, after the block barrier,

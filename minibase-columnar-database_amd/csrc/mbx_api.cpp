@@ -99,7 +99,6 @@ static void tuning_from_env(MbxTuning& t) {
   t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 1);
   t.scan_select_waves = (int32_t)env_knob("MBX_SCAN_SELECT_WAVES", 16);
   t.select_flag_stride = (int32_t)env_knob("MBX_SELECT_FLAG_STRIDE", kFlagStride);
-  t.select_flag_copies = (int32_t)env_knob("MBX_SELECT_FLAG_COPIES", 1);
   t.scan_words_wt = (int32_t)env_knob("MBX_SCAN_WORDS_WT", 1);
   t.comm_same_stream = (int32_t)env_knob("MBX_COMM_SAME_STREAM", 1);
   t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
@@ -317,8 +316,6 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "scan_select_fused")) t.scan_select_fused = v;
   else if (!strcmp(knob, "scan_select_waves")) t.scan_select_waves = v == 4 ? 4 : 16;
   else if (!strcmp(knob, "select_flag_stride")) t.select_flag_stride = v == 1 ? 1 : kFlagStride;
-  else if (!strcmp(knob, "select_flag_copies"))
-    t.select_flag_copies = v < 1 ? 1 : (v > kMaxFlagCopies ? kMaxFlagCopies : (int32_t)v);
   else if (!strcmp(knob, "scan_words_wt")) t.scan_words_wt = v != 0;
   else if (!strcmp(knob, "comm_same_stream")) t.comm_same_stream = v != 0;
   else return fail(MBX_E_INVALID, "mbx_set_tuning: unknown knob `%s`", knob);
@@ -1097,8 +1094,7 @@ static int enqueue_scan(mbx_ctx* c, const mbx_plan* p, const PlanVariant& v, int
       stamps = c->stamps;
     }
     HIPCHK(launch_scan_select(L, c->lookback, p->t->row_offset, fused->ids, fused->total, c->stream, stamps,
-                              c->tune.select_dbg >> 4, c->tune.scan_select_waves,
-                              c->tune.select_flag_stride | (c->tune.select_flag_copies << 8)));
+                              c->tune.select_dbg >> 4, c->tune.scan_select_waves, c->tune.select_flag_stride));
     return MBX_OK;
   }
   HIPCHK(launch_scan(L, c->stream));

@@ -342,8 +342,7 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
 // epoch, per-block counts, per-block inclusive prefixes; the polling form's
 // counts may sit one per 128-byte line (kFlagStride words apart)
 constexpr int32_t kFlagStride = 16;
-constexpr int32_t kMaxFlagCopies = 8;  // copies of every polled flag (select_flag_copies)
-constexpr int64_t kLookbackWords = 1 + (int64_t)kFlagStride * 1024 * kMaxFlagCopies;
+constexpr int64_t kLookbackWords = 1 + kFlagStride * 1024;
 // BitSet + positions + COUNT of a plan in one launch (k_scan_select): plans of
 // 1..4 int literal terms on 4-byte columns, tables whose segments fit the
 // one-launch form (scan_select_fusable); L as for a kModeBitmap scan (its
@@ -351,7 +350,7 @@ constexpr int64_t kLookbackWords = 1 + (int64_t)kFlagStride * 1024 * kMaxFlagCop
 bool scan_select_fusable(int64_t nrows, int64_t tiles_per_block, int32_t fast_k, int32_t fast_ks, int32_t nterms,
                          int32_t has_real, int32_t waves);
 hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offset, int64_t* ids, int64_t* total,
-                              hipStream_t s, int64_t* stamps, int32_t dbg, int32_t waves, int32_t flag_layout);
+                              hipStream_t s, int64_t* stamps, int32_t dbg, int32_t waves, int32_t flag_stride);
 hipError_t launch_bitmap_cnf(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                              int64_t words_per_block, uint64_t* out, int64_t* segc, hipStream_t s);
 hipError_t launch_bitmap_combine(int32_t op, const uint64_t* a, const uint64_t* b, int64_t nwords,

@@ -1623,16 +1623,10 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
                                             int64_t* __restrict__ total, const GT& G, int64_t* __restrict__ stamps,
                                             int32_t dbg, int64_t* __restrict__ segc, int64_t nseg, int64_t* wcount,
                                             int64_t* wpre, uint16_t (*stage)[32 * 64],
-                                            uint64_t* __restrict__ words_out = nullptr, int32_t layout = 1) {
-  // layout (the polling form; the chained walk needs 1): bits 0-7 fs = int64
-  // words between two blocks' count flags (1, or 16 = one 128-byte line per
-  // flag), bits 8-15 the number of copies of every flag (1..kMaxFlagCopies):
-  // block b polls copy b % copies, so a flag's line is read by 1 / copies of
-  // the blocks
-  const int32_t fs = layout & 0xff;
-  const int32_t ncopy = (layout >> 8) > 0 ? (layout >> 8) : 1;
-  const int64_t copy_words = (int64_t)kLookbackBlocks * fs;
-  const int64_t rb = 1 + (int64_t)(blockIdx.x % ncopy) * copy_words;  // this block's copy
+                                            uint64_t* __restrict__ words_out = nullptr, int32_t fs = 1) {
+  // fs: int64 words between two blocks' count flags (1, or 16 = one 128-byte
+  // line per flag for the polling form: the polls of every block do not queue
+  // on the same few lines); the chained form needs 1
   dbg &= kDiagDbg;  // bits 0-2: A/B poll forms, -DMBX_DIAG builds only
   int64_t* const inc = lb + 1 + kLookbackBlocks;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
 #pragma unroll
@@ -1672,15 +1666,17 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   int64_t* flag_at = nullptr;
   int64_t flag = 0;
   if (wave == kPub) {
-    flag_at = &lb[1 + (int64_t)(lane < ncopy ? lane : 0) * copy_words + (int64_t)blockIdx.x * fs];
+    flag_at = &lb[1 + (int64_t)blockIdx.x * fs];
     flag = (epoch << 32) | bc;
     asm volatile("" : "+v"(flag_at), "+v"(flag));
     // vmcnt(0) before the flag: free (nothing of this wave is in flight here
     // but a diagnostic stamp), and the compiler then counts nothing in flight
     // on this path, so it places no wait after the flag
     __builtin_amdgcn_s_waitcnt(0x0f70);
-    if (lane < ncopy) asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(flag_at), "v"(flag) : "memory");
-    if (lane == 0) wpre[kPub] = 0;
+    if (lane == 0) {
+      asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(flag_at), "v"(flag) : "memory");
+      wpre[kPub] = 0;
+    }
   }
   if (dbg & 128) {  // diagnostic: the count only (wrong output by design)
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) lb[0] = epoch;
@@ -1746,9 +1742,9 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       if (j >= (int64_t)blockIdx.x)
         v[k] = epoch << 32;
       else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
-        v[k] = __builtin_nontemporal_load(&lb[rb + j * fs]);
+        v[k] = __builtin_nontemporal_load(&lb[1 + j * fs]);
       else
-        v[k] = __hip_atomic_load(&lb[rb + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     int64_t pre = 0;
 #pragma unroll
@@ -1759,7 +1755,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
           __builtin_amdgcn_s_sleep(16);
         else
           __builtin_amdgcn_s_sleep(1);
-        v[k] = __hip_atomic_load(&lb[rb + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[k] = __hip_atomic_load(&lb[1 + j * fs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       pre += v[k] & 0xffffffffll;
     }
@@ -1846,8 +1842,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       const int64_t x = w - 1;
       const bool live = (dbg & 8) ? (x < (int64_t)gridDim.x ||
                                      (x >= kLookbackBlocks && x - kLookbackBlocks < (int64_t)gridDim.x))
-                                  : (x / copy_words < ncopy && (x % copy_words) % fs == 0 &&
-                                     (x % copy_words) / fs < (int64_t)gridDim.x);
+                                  : (x % fs == 0 && x / fs < (int64_t)gridDim.x);
       if (!live) lb[w] = 0;
     }
   }
@@ -1959,7 +1954,7 @@ constexpr bool kDefaultNT = true;
 template <int K, bool DEL, int U, int TQ, int NW, int NR, int IR = 0>
 __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* __restrict__ lb, int64_t row_offset,
                                                          int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                         int64_t* __restrict__ stamps, int32_t dbg, int32_t layout) {
+                                                         int64_t* __restrict__ stamps, int32_t dbg, int32_t fs) {
 #ifndef MBX_DIAG
   dbg &= 8;  // the look-back form (bit 3: chained, else every predecessor polled); write-through positions
 #endif
@@ -2043,7 +2038,7 @@ __global__ __launch_bounds__(64 * NW) void k_scan_select(ScanLaunch L, int64_t* 
   const Gather4 G{};
   select_tail<0, Gather4, decltype(word_at), NW, NR>(wr, c, true, a0, a1, word_at, lane, wave, lb, epoch, row_offset,
                                                      ids, total, G, stamps, dbg, L.seg_counts, nseg, wcount, wpre,
-                                                     stage, L.out_words, layout);
+                                                     stage, L.out_words, fs);
 }
 
 // Late materialisation (Heapfile.findRID + getRecord per output column,
@@ -2529,7 +2524,7 @@ bool scan_select_fusable(int64_t nrows, int64_t tiles_per_block, int32_t fast_k,
 }
 
 hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offset, int64_t* ids, int64_t* total,
-                              hipStream_t s, int64_t* stamps, int32_t dbg, int32_t waves, int32_t flag_layout) {
+                              hipStream_t s, int64_t* stamps, int32_t dbg, int32_t waves, int32_t flag_stride) {
   // waves per block: 4 (one BitSet segment per block) or 16 (four): a
   // quarter of the blocks publish and walk back
   const int nw = waves == 16 ? 16 : kWaves;
@@ -2541,10 +2536,7 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
   // 11.8-12.1 us vs 13.4-13.6 for the chained walk and 12.0-12.2 with the
   // flags packed (profiles/r04/f1); select_dbg bit 7: the chained walk
   // (32-bit inclusive prefixes: tables < 2^32 rows)
-  const int32_t fs = (dbg & 8) || (flag_layout & 0xff) != kFlagStride ? 1 : kFlagStride;
-  const int32_t want_copies = flag_layout >> 8;
-  const int32_t copies = (dbg & 8) || want_copies < 1 ? 1 : (want_copies > kMaxFlagCopies ? kMaxFlagCopies : want_copies);
-  const int32_t layout = fs | (copies << 8);
+  const int32_t fs = (dbg & 8) || flag_stride != kFlagStride ? 1 : kFlagStride;
   const bool del = L.deleted != nullptr;
   const bool ir = L.int_range != 0;  // branch-free int terms (every fused plan qualifies; the knob can turn it off)
   // registers of 64 words per wave: only as many as a wave's quarter
@@ -2556,16 +2548,16 @@ hipError_t launch_scan_select(const ScanLaunch& L, int64_t* lb, int64_t row_offs
 #define MBX_SCAN_SELECT_NW(KK, UU, NW, NR)                                                                       \
   if (del && ir)                                                                                               \
     hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR, 1>), dim3((unsigned)g), dim3(64 * NW), \
-                       0, s, L, lb, row_offset, ids, total, stamps, dbg, layout);                                  \
+                       0, s, L, lb, row_offset, ids, total, stamps, dbg, fs);                                  \
   else if (del)                                                                                                \
     hipLaunchKernelGGL((k_scan_select<KK, true, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \
-                       s, L, lb, row_offset, ids, total, stamps, dbg, layout);                                     \
+                       s, L, lb, row_offset, ids, total, stamps, dbg, fs);                                     \
   else if (ir)                                                                                                 \
     hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR, 1>), dim3((unsigned)g),            \
-                       dim3(64 * NW), 0, s, L, lb, row_offset, ids, total, stamps, dbg, layout);                   \
+                       dim3(64 * NW), 0, s, L, lb, row_offset, ids, total, stamps, dbg, fs);                   \
   else                                                                                                         \
     hipLaunchKernelGGL((k_scan_select<KK, false, UU, kHoistTerms, NW, NR>), dim3((unsigned)g), dim3(64 * NW), 0, \
-                       s, L, lb, row_offset, ids, total, stamps, dbg, layout)
+                       s, L, lb, row_offset, ids, total, stamps, dbg, fs)
 #define MBX_SCAN_SELECT(KK, UU)                  \
   if (nw != 16) {                                \
     MBX_SCAN_SELECT_NW(KK, UU, kWaves, kSelRegs); \

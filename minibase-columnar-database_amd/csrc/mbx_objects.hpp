@@ -59,7 +59,6 @@ struct MbxTuning {
   int32_t scan_select_fused = 1;  // MBX_SCAN_SELECT_FUSED: 1 = BitSet + positions in one launch (k_scan_select)
   int32_t scan_select_waves = 16; // MBX_SCAN_SELECT_WAVES: waves per k_scan_select block (4 or 16)
   int32_t select_flag_stride = 16; // MBX_SELECT_FLAG_STRIDE: 16 = k_scan_select's polled flags one per line, or 1
-  int32_t select_flag_copies = 1;  // MBX_SELECT_FLAG_COPIES: copies of every polled flag (1..kMaxFlagCopies)
   int32_t scan_words_wt = 1;      // MBX_SCAN_WORDS_WT: BitSet scan words stored write-through
   int32_t comm_same_stream = 1;   // MBX_COMM_SAME_STREAM: collectives on the context stream (0: the exchange stream)
   int32_t select_dbg = 0;         // MBX_SELECT_DBG: bit 3 per-block stamps, 128 every-predecessor poll

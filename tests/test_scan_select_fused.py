@@ -119,8 +119,7 @@ def test_fused_c2_full_size_launch_after_launch(ctx):
     g.close()
 
 
-LOOKBACK = {"poll_spread": (0, 16, 1), "poll": (0, 1, 1), "chained": (128, 1, 1), "poll_spread_4copies": (0, 16, 4),
-            "poll_8copies": (0, 1, 8)}
+LOOKBACK = {"poll_spread": (0, 16), "poll": (0, 1), "chained": (128, 1)}
 
 
 @pytest.mark.parametrize("lookback", list(LOOKBACK))
@@ -132,7 +131,6 @@ def test_fused_segment_sizes_and_fallback(ctx, tune, tpb, lookback):
     tune("tiles_per_block", tpb)
     tune("select_dbg", LOOKBACK[lookback][0])
     tune("select_flag_stride", LOOKBACK[lookback][1])
-    tune("select_flag_copies", LOOKBACK[lookback][2])
     n = 3_000_017
     cols = int_cols(n, hi=1000, seed=5)
     t = ctx.stage(cols)
@@ -154,7 +152,6 @@ def test_fused_waves_per_block(ctx, tune, waves, n, lookback):
     tune("scan_select_waves", waves)
     tune("select_dbg", LOOKBACK[lookback][0])
     tune("select_flag_stride", LOOKBACK[lookback][1])
-    tune("select_flag_copies", LOOKBACK[lookback][2])
     cols = int_cols(n, ncols=2, hi=1000, seed=n + waves)
     dele = helpers.random_deleted(n, 0.03, seed=n) if n == 70001 else None
     ot = oracle.Table(cols, dele)
@@ -217,7 +214,6 @@ def test_lookback_epoch_wrap(m, ctx, tune, lookback):
     wrap leave no stale flag that a later launch could take for its own."""
     tune("select_dbg", LOOKBACK[lookback][0])
     tune("select_flag_stride", LOOKBACK[lookback][1])
-    tune("select_flag_copies", LOOKBACK[lookback][2])
     runs = []
     for n in (3_000_017, 100_003, 1_000_003):
         cols = int_cols(n, hi=10, seed=n)

@@ -176,14 +176,12 @@ def main():
         # 128-byte line), with the flags packed (select_flag_stride 1) and
         # with the chained walk (select_dbg 128)
         forms = {}
-        variants = {0: (0, 0, 16, 1), 1: (1, 0, 16, 1), "poll_packed": (1, 0, 1, 1), "chained": (1, 128, 1, 1),
-                    "copies4": (1, 0, 16, 4), "copies8": (1, 0, 16, 8), "packed_copies8": (1, 0, 1, 8)}
+        variants = {0: (0, 0, 16), 1: (1, 0, 16), "poll_packed": (1, 0, 1), "chained": (1, 128, 1)}
         for rep in range(3):
-            for key, (fused, dbg, fs, cp) in variants.items():
+            for key, (fused, dbg, fs) in variants.items():
                 ctx.set_tuning("scan_select_fused", fused)
                 ctx.set_tuning("select_dbg", dbg)
                 ctx.set_tuning("select_flag_stride", fs)
-                ctx.set_tuning("select_flag_copies", cp)
                 ids.zero_()
                 torch.cuda.synchronize()
                 forms.setdefault(key, []).append(kernel_ms(step, args.steps, args.warmup))
@@ -200,7 +198,6 @@ def main():
             for key in (1, "poll_packed", "chained"):
                 ctx.set_tuning("scan_select_fused", 1)
                 ctx.set_tuning("select_flag_stride", variants[key][2])
-                ctx.set_tuning("select_flag_copies", variants[key][3])
                 ctx.set_tuning("select_dbg", 8 | variants[key][1])
                 step()
                 ctx.sync()
@@ -233,7 +230,6 @@ def main():
               "ms_per_query_two_launch": forms[0], "ms_per_query_one_launch": forms[1],
               "ms_per_query_one_launch_flags_packed": forms["poll_packed"],
               "ms_per_query_one_launch_chained": forms["chained"],
-              "ms_per_query_one_launch_copies": {k: forms[k] for k in ("copies4", "copies8", "packed_copies8")},
               "stamps_us": stamps,
               "graph_replay_ms_per_query": graph_ms,
               "algorithmic_gbs": byts / ms / 1e6, "scan_bitmap_ms": scan_ms,
@@ -250,7 +246,6 @@ def main():
                     ctx.set_tuning("scan_select_fused", 1)
                     ctx.set_tuning("select_dbg", variants[key][1])
                     ctx.set_tuning("select_flag_stride", variants[key][2])
-                    ctx.set_tuning("select_flag_copies", variants[key][3])
                     ids.zero_()
                     torch.cuda.synchronize()
                     f = lambda: M._chk(L.mbx_scan_select_async(ctx.h, plan.h, bmt.h, ids.data_ptr(), cnt.data_ptr()))
