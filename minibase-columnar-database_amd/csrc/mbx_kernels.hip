@@ -1733,17 +1733,8 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     }
   } else {
     // polling form: every predecessor's count, one per thread of the other
-    // waves, all in flight together -- after the wave's BitSet words, whose
-    // write-through round trip then overlaps the polls' instead of following
-    // the offset barrier (the publishing wave stores its words at the end)
+    // waves, all in flight together
     if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
-    if (words_out && !(dbg & 256)) {
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int64_t wd = a0 + r * 64 + lane;
-        if (wd < a1) put(&words_out[wd], wr[r], (G4 == 0) != ((dbg & 32) != 0));
-      }
-    }
     int64_t v[kPolls];
 #pragma unroll
     for (int k = 0; k < kPolls; ++k) {
@@ -1823,9 +1814,8 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       emit_step<G4, GT>(base, base + lane < a1 ? word_at(base + lane) : 0ull, off, row_offset, ids, st, lane, G,
                         wt);
   }
-  // the BitSet (k_scan_select): its words (the polling waves stored theirs
-  // before the look-back) and one segment count per 4 waves
-  if (words_out && !(dbg & 256) && (wave == kPub || (dbg & 8))) {
+  // the BitSet (k_scan_select): its words and one segment count per 4 waves
+  if (words_out && !(dbg & 256)) {
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       const int64_t wd = a0 + r * 64 + lane;
