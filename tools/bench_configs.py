@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--configs", default="C2,C4,C5")
     ap.add_argument("--c2-stamps", action="store_true", help="C2: per-block stamps of each one-launch form")
     ap.add_argument("--c2-tpb", default="", help="C2: comma list of tiles_per_block to sweep (one launch)")
+    ap.add_argument("--c2-stamps-out", default="", help="C2: per-block stamps of each form to PREFIX.<form>.csv")
     ap.add_argument("--c4-rows", type=int, default=100_000_000, help="global rows")
     ap.add_argument("--c4-positions", action="store_true",
                     help="C4 query also writes the selected positions (default: the projected rows only)")
@@ -206,6 +207,11 @@ def main():
                 st = st.reshape(nb, 4).astype(np.float64) / 100.0  # 100 MHz wall clock -> us
                 st -= st[:, 0].min()
                 pct = lambda x: [round(float(v), 2) for v in np.percentile(x, [0, 10, 50, 90, 100])]
+                if args.c2_stamps_out:
+                    with open(f"{args.c2_stamps_out}.{key}.csv", "w") as fh:
+                        fh.write("block,start_us,staged_us,offset_known_us,end_us\n")
+                        for b in range(nb):
+                            fh.write(f"{b},{st[b, 0]:.2f},{st[b, 1]:.2f},{st[b, 2]:.2f},{st[b, 3]:.2f}\n")
                 stamps[str(key)] = {"blocks": nb, "s1_pct": pct(st[:, 1]), "s2_pct": pct(st[:, 2]),
                                     "s3_pct": pct(st[:, 3]), "s2_s1_pct": pct(st[:, 2] - st[:, 1]),
                                     "s3_s2_pct": pct(st[:, 3] - st[:, 2])}
