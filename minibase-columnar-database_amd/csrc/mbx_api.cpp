@@ -93,7 +93,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.join_plain = (int32_t)env_knob("MBX_JOIN_PLAIN", 0);
   t.distinct_lds_probes = (int32_t)env_knob("MBX_DISTINCT_LDS_PROBES", -1);
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
-  if (((t.select_dbg & 3) | ((t.select_dbg >> 4) & 471)) & ~kDiagDbg) t.select_dbg = 0;  // A/B forms: -DMBX_DIAG
+  if (((t.select_dbg & 3) | ((t.select_dbg >> 4) & 983)) & ~kDiagDbg) t.select_dbg = 0;  // A/B forms: -DMBX_DIAG
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
   t.cursor_prefetch = (int32_t)env_knob("MBX_CURSOR_PREFETCH", 1);
   t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 1);
@@ -306,7 +306,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "select_dbg")) {
     // k_select_ids takes bits 0-1, the one-launch selections bits 4-6: A/B
     // forms a production build compiles out (kDiagDbg)
-    if (((v & 3) | ((v >> 4) & 471)) & ~kDiagDbg)
+    if (((v & 3) | ((v >> 4) & 983)) & ~kDiagDbg)
       return fail(MBX_E_UNSUPPORTED, "mbx_set_tuning: select_dbg %d needs a -DMBX_DIAG build", v);
     t.select_dbg = v;
   }

@@ -33,14 +33,15 @@ constexpr int kMaxProj = 16;
 // select_dbg kernel bits that exist only for A/B measurements: skip the
 // prefix loads / the look-back wait (wrong output by design), skip the
 // emission (64), the staging (16), the BitSet words (256), everything after
-// the count (128), the back-off and plain-load poll forms.  A production build
+// the count (128), nontemporal positions stores (512), the back-off and
+// plain-load poll forms.  A production build
 // compiles them out (the kernels mask dbg with kDiagDbg); -DMBX_DIAG keeps
 // them.  Stamps, the write-through flip and the every-predecessor look-back
 // (tables of >= 2^32 rows take it) stay in every build.
 #ifdef MBX_DIAG
 constexpr int32_t kDiagDbg = ~0;
 #else
-constexpr int32_t kDiagDbg = ~(1 | 2 | 4 | 16 | 64 | 128 | 256);
+constexpr int32_t kDiagDbg = ~(1 | 2 | 4 | 16 | 64 | 128 | 256 | 512);
 #endif
 
 enum ColKind : int32_t { kInt = 0, kReal = 1, kStr = 2 };

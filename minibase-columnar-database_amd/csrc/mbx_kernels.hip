@@ -617,7 +617,8 @@ __device__ __forceinline__ void wide_row(const GatherW& G, int64_t p, int64_t o)
 template <int G4, class GT = Gather4>
 __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const StepScan& r, int64_t& off,
                                            int64_t row_offset, int64_t* __restrict__ ids, const uint16_t* st,
-                                           int lane, const GT& G, uint32_t first = 0, bool wt = false) {
+                                           int lane, const GT& G, uint32_t first = 0, bool wt = false,
+                                           bool nt = false) {
   if (r.total == 0) return;
   const int64_t lbase = base * 64;  // table-local row of bit 0 of word `base`
   if (r.total <= kStageIds && G4 == 0) {
@@ -630,7 +631,12 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
       if (ids) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (i0 + 64u * u < r.total) put(&ids[off + i0 + 64u * u], row_offset + lbase + q[u], wt);
+          if (i0 + 64u * u < r.total) {
+            if (nt)  // diagnostic (-DMBX_DIAG, dbg bit 9): nontemporal positions stores
+              __builtin_nontemporal_store(row_offset + lbase + q[u], &ids[off + i0 + 64u * u]);
+            else
+              put(&ids[off + i0 + 64u * u], row_offset + lbase + q[u], wt);
+          }
       }
     }
     __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next step
@@ -1801,7 +1807,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       }
     }
     const StepScan all{0u, tot};
-    store_step<G4, GT>(a0, 0ull, all, off, row_offset, ids, st, lane, G, 64u * kPrefetch, wt);
+    store_step<G4, GT>(a0, 0ull, all, off, row_offset, ids, st, lane, G, 64u * kPrefetch, wt, (dbg & 512) != 0);
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       const int64_t base = a0 + r * 64;

@@ -67,10 +67,10 @@ def main():
     # 32 skips the look-back's wait; 1024 skips the positions; 256 skips the
     # staging (and so the positions); 4096 skips the BitSet words; 2048 ends
     # every block once its count is published; 512 plain (not
-    # write-through) positions; 128 the chained walk
+    # write-through) positions; 8192 nontemporal positions; 128 the chained walk
     variants = {"default": 0, "no_lookback_wait": 32, "no_positions": 1024, "neither": 32 | 1024,
                 "no_staging": 256, "no_words": 4096, "no_staging_no_words": 256 | 4096,
-                "count_only": 2048, "plain_stores": 512, "chained": 128}
+                "count_only": 2048, "plain_stores": 512, "nt_stores": 8192, "chained": 128}
     res = {}
     for rep in range(3):
         for k, v in variants.items():
@@ -78,7 +78,7 @@ def main():
             ids.zero_()
             torch.cuda.synchronize()
             res.setdefault(k, []).append(round(kernel_ms(), 2))
-            if v in (0, 512, 128):
+            if v in (0, 512, 8192, 128):
                 got = int(cnt.item())
                 assert got == wpos.numel() and bool((ids[:got] == wpos).all()), k
     ctx.set_tuning("select_dbg", 0)
