@@ -1,41 +1,56 @@
 #!/usr/bin/env python3
 """bench.py -- BASELINE.json headline: scanned rows/s + HBM GB/s on the C3
 workload (100M-row 4 x int32 Columnarfile, 2-predicate conjunction + COUNT),
-at 1 / 2 / 4 / 8 GPUs.
+at 1 / 2 / 4 / 8 GPUs, plus one record per other BASELINE config (C2, C4, C5).
 
 One "step" = one ColumnarFileScan COUNT pass over the resident table:
-`query ... {(c0 < 2^19)} ^ {(c1 >= 2^19)} FILESCAN` -> Total Results Count,
-executed as ONE kernel launch per GPU (k_scan_fast<2, COUNT>; its last block
-folds the per-block counts), plus -- on N > 1 GPUs -- the path's one exchange
+`query ... {(c0 < 2^19)} ^ {(c1 >= 2^19)} FILESCAN` -> Total Results Count
+(R/input/Query.java:137-152), executed as ONE kernel launch per GPU
+(k_scan_fast<2, COUNT>), plus -- on N > 1 GPUs -- the path's one exchange
 step: an in-place RCCL all-reduce of the COUNTs over xGMI, issued by libmbx
-(mbx_comm_allreduce_count_async) right after the scan on the same stream
-(libmbx's default: inside a captured graph a collective forked to a second
-stream is not overlapped on this ROCm and costs more, profiles/r03/parts).
-Every step (= query) has its own collective
-(--exchange-bucket 1, the default: SURVEY 8(e)'s per-query
-N_total / (max_k t_kernel,k + t_reduce)); --exchange-bucket B > 1 lets the
-COUNTs of B consecutive steps share one all-reduce (a diagnostic: a tiny
-all-reduce costs its latency, not its bytes).
+(mbx_comm_allreduce_count_async) right after the scan on the same stream.
+Every step (= query) has its own collective (--exchange-bucket 1, the
+default: SURVEY 8(e)'s per-query N_total / (max_k t_kernel,k + t_reduce)).
 Inputs are resident in HBM before the timed region.
 
 Scaling.  The path partitions by row
-range with no data-path collective and one exchange per query (the COUNT
-reduce north_star names), so the default reports weak scaling:
+range with no data-path collective and one exchange per query, so the
+headline reports weak scaling:
   --scaling weak (default): per-GPU work fixed at the C3 table -- rank r owns
       rows [r * 100M, (r + 1) * 100M) of an N x 100M-row logical table (its own
-      seeds 42 + 1000 r + col; N = 1 is exactly the C3 table); every step's
-      global COUNT is checked against the sum of the ranks' torch counts.
-  --scaling strong: ONE 100M-row table split into N 64-aligned row-range
-      shards (mbx_shard_bounds), generated full size with the same seeds on
-      every rank and sliced, the global COUNT checked against a torch
-      reduction of the whole table (12.5M rows per GPU at N = 8: launch- and
-      exchange-latency bound).
+      seeds 42 + 1000 r + col; N = 1 is exactly the C3 table).  At N > 1 the
+      same run also times the STRONG form and reports it as the `strong`
+      sub-record: the metric's ONE 100M-row table in N 64-aligned shards
+      (mbx_shard_bounds), with its phases (scan max over ranks, exchange).
+  --scaling strong: the headline itself is the strong form.
 The timed steps replay HIP graphs (mbx_graph_*) of --graph-steps captured
 steps (scans + their exchange), so small shards do not wait on the host.
-value = global rows scanned by all ranks / max-over-ranks wall time.  stdout
-carries only the JSON line.
+Before any timing, ONE exchanged step runs eagerly and is verified (global
+COUNT, every count-frame arrival): a broken collective or frame decode exits
+non-zero with a one-line reason before any timed work (`pre_check`).
+value = global rows scanned by all ranks / max-over-ranks wall time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
+Kernel time (`roofline.kernel_ms`, every config's `kernel_ms`): one captured
+HIP graph of --kernel-graph launches of the query's kernels alone, replayed,
+HIP events on the library stream around the replays / launches -- so
+kernel_ms <= ms_per_step (no per-launch event pair).
+
+Config records (`configs`, --configs, default C2,C4,C5):
+  C2  10M rows x 4 int32, c0 < 104858 -> BitSet + positions + COUNT, one
+      launch (k_scan_select); a 1-GPU config: rank 0 only
+  C4  100M rows (global, row-range sharded over the N GPUs), AND of the
+      BitMapFiles bm(c2=3), bm(c3=7) -> positions + projected c0, c1 in ONE
+      launch (k_cnf_select, (c0, c1) column group); at N > 1 + the RCCL
+      all-gather of the per-rank counts (the concatenation offsets)
+      (R/index/ColumnarIndexScan.java:130-181,287-308)
+  C5  125M rows PER GPU (1B at N = 8) i32 / f32 / char(16),
+      (c0 < 2^19) ^ (c1 >= 0.25) ^ (c2 >= "M") -> COUNT, SUM / MIN / MAX(c1);
+      at N > 1 + the RCCL all-gather of the 48-byte records + the device
+      rank-ordered fold (k_fold_agg)
+Each is checked against torch reductions of the same device data before
+and after its timing.  stdout carries only the JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak] [--configs C2,C4,C5|none]
 
 Launch: with WORLD_SIZE unset and --gpus N > 1, this process is only a
 launcher: before anything touches a GPU it starts N rank processes of this
@@ -45,6 +60,10 @@ first failing rank's status (the others are then stopped by PID).  Under an
 external torch.distributed.run, WORLD_SIZE must equal --gpus.
 --dry-launch: the ranks print their rank env as JSON and exit before
 importing torch (the launcher's CPU test, tests/test_bench_launch.py).
+Rehearsal knobs (never set by the driver): MBX_BENCH_SAME_DEVICE=1 (N ranks on
+one GPU, gloo exchange), MBX_BENCH_FORCE_EXCHANGE=1 (the exchange at N = 1),
+MBX_BENCH_CORRUPT=frame|count (rank 0 damages its pre-check frame: the
+pre-check must fire).
 """
 import argparse
 import json
@@ -58,6 +77,13 @@ sys.path.insert(0, ROOT)
 METRIC = "scanned rows/sec + HBM GB/s, 100M-row 4×int32 conjunctive filter, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 THRESH = 1 << 19
+C2_LIT = 104858  # c0 < 104,858 (~10 %)
+PRECHECK_EXIT = 3
+
+# the keys every config record carries (tests/test_bench_launch.py)
+CONFIG_KEYS = ("workload", "rows", "rows_per_gpu", "gpus", "selected", "ms_per_query", "rows_per_s", "kernel",
+               "kernel_ms", "kernel_ms_max_over_ranks", "algorithmic_bytes_per_launch", "achieved_gbs", "frac",
+               "exchange", "pre_check", "timing")
 
 
 def cpu_baseline(rows, min_seconds):
@@ -155,32 +181,6 @@ def launch_ranks(n, argv, dry):
     return status
 
 
-def read_probe(ctx, table, ext, torch, reps=30):
-    """Best read bandwidth of k_read_probe (mbx_probe_read: the C3 kernel's
-    tiles and non-temporal dwordx4 loads over c0, c1 with no predicate) over a
-    few block mappings, timed with HIP events on the library stream."""
-    n = table.nrows
-    nbytes = 2 * 4 * (n // 256 * 256)
-    variants = [("segments, scan default", dict()), ("segments, tpb=256", dict(tiles_per_block=256)),
-                ("segments, tpb=96", dict(tiles_per_block=96)),
-                ("grid-stride 1024 blocks", dict(interleave=True, grid=1024)),
-                ("grid-stride 2048 blocks", dict(interleave=True, grid=2048))]
-    res = {}
-    for name, kw in variants:
-        for _ in range(3):
-            ctx.probe_read(table, [0, 1], **kw)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(ext)
-        for _ in range(reps):
-            ctx.probe_read(table, [0, 1], **kw)
-        b.record(ext)
-        ctx.sync()
-        ms = a.elapsed_time(b) / reps
-        res[name] = nbytes / (ms * 1e-3) / 1e9
-    best = max(res, key=res.get)
-    return {"best_gbs": res[best], "best": best, "gbs": res}
-
-
 def quiet_stdout():
     """The one JSON line is the only thing on stdout: fd 1 is pointed at
     stderr for the libraries (RCCL prints a version banner when it creates
@@ -192,36 +192,67 @@ def quiet_stdout():
     return fd
 
 
-def make_columns(torch, n_global, s, e, seed_base):
-    """Columns c0..c3 of rows [s, e) of one logical table: each column is
-    generated whole on this GPU from its own seed (torch Philox), so every
-    shard count N slices the same table, then the shard is copied out."""
-    cols = []
-    for j in range(4):
-        g = torch.Generator(device="cuda")
-        g.manual_seed(seed_base + j)
-        full = torch.randint(0, 1 << 20, (n_global,), dtype=torch.int32, device="cuda", generator=g)
-        cols.append(full[s:e].clone())
-        del full
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
-    return cols
+# ---------------------------------------------------------------- checks
+# pure functions over host copies (numpy), unit-tested on the CPU
+
+FRAME_SLOTS, FRAME_SLOT_WORDS = 32, 16
 
 
-def full_count(torch, n_global, seed_base):
-    """The global C3 COUNT of the whole table (torch reduction, chunk-free)."""
-    out = []
-    for j in range(2):
-        g = torch.Generator(device="cuda")
-        g.manual_seed(seed_base + j)
-        out.append(torch.randint(0, 1 << 20, (n_global,), dtype=torch.int32, device="cuda", generator=g))
-    c = int(((out[0] < THRESH) & (out[1] >= THRESH)).sum().item())
-    del out
-    torch.cuda.empty_cache()
-    return c
+def frame_fields(frames):
+    """(count, nan_blocks, arrivals) per step of (k, 512) int64 count frames:
+    slot i = word 16 i (its own 128-byte line), count in bits 24.., NaN blocks
+    in bits 12..23, arrivals in bits 0..11 (mbx_count_frame_decode)."""
+    import numpy as np
+    f = np.asarray(frames, dtype=np.int64).reshape(-1, FRAME_SLOTS, FRAME_SLOT_WORDS)[:, :, 0]
+    return (f >> 24).sum(1), ((f >> 12) & 0xFFF).sum(1), (f & 0xFFF).sum(1)
 
 
-def main():
+def check_counts(kind, got, want, frames=None, nblocks=None):
+    """None, or the one-line reason the exchanged step(s) are wrong: every
+    step's global COUNT must equal `want`; with count frames every block of
+    every rank must have arrived exactly once (`nblocks` summed over ranks)
+    and no block may report NaN."""
+    import numpy as np
+    if frames is not None:
+        c, nan, arr = frame_fields(frames)
+        if not (arr == nblocks).all():
+            return f"{kind}: frame arrivals {arr[:4].tolist()} != {nblocks} blocks over all ranks"
+        if nan.any():
+            return f"{kind}: {int(nan.sum())} NaN blocks in an integer plan"
+        got = c
+    got = np.asarray(got).reshape(-1)
+    if not (got == want).all():
+        return f"{kind}: global COUNT {got[:4].tolist()} != {want}"
+    return None
+
+
+def check_aggregate(kind, got, want, rel=1e-6):
+    """None, or why dict(count, sum, min, max) `got` differs from `want`:
+    COUNT / MIN / MAX exact, SUM within `rel` (north_star: 1e-6 relative)."""
+    for k in ("count", "min", "max"):
+        if got[k] != want[k]:
+            return f"{kind}: {k} {got[k]!r} != {want[k]!r}"
+    if abs(got["sum"] - want["sum"]) > rel * abs(want["sum"]):
+        return f"{kind}: sum {got['sum']!r} vs {want['sum']!r} beyond {rel} relative"
+    return None
+
+
+def config_record(workload, rows, rows_per_gpu, gpus, selected, ms_per_query, kernel, kernel_ms, kernel_ms_max,
+                  algo_bytes, exchange, pre_check, timing, **extra):
+    """One `configs` entry: global rows/s of the query with its exchange, the
+    dominant kernel's time from graph replay and its fraction of 8 TB/s over
+    SURVEY 8(d)'s algorithmic bytes of rank 0's launch."""
+    gbs = algo_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    rec = {"workload": workload, "rows": rows, "rows_per_gpu": rows_per_gpu, "gpus": gpus, "selected": selected,
+           "ms_per_query": ms_per_query, "rows_per_s": rows / (ms_per_query * 1e-3) if ms_per_query > 0 else 0.0,
+           "kernel": kernel, "kernel_ms": kernel_ms, "kernel_ms_max_over_ranks": kernel_ms_max,
+           "algorithmic_bytes_per_launch": algo_bytes, "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
+           "exchange": exchange, "pre_check": pre_check, "timing": timing}
+    rec.update(extra)
+    return rec
+
+
+def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -230,17 +261,555 @@ def main():
                     help="global rows (strong scaling) or rows per GPU (weak)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
     ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured HIP graph (0: eager launches)")
+    ap.add_argument("--kernel-graph", type=int, default=20, help="launches per graph timed for kernel_ms")
     ap.add_argument("--exchange-bucket", type=int, default=1,
                     help="steps whose COUNTs share one all-reduce (1, the default: one collective per query)")
     ap.add_argument("--count", choices=["auto", "frame", "finalize"], default="auto",
                     help="frame: each scan adds its COUNT into a 32-slot count frame (no in-launch finalize; the "
                          "exchange all-reduces whole frames); finalize: the scan's last block writes the COUNT; "
                          "auto: frame with an exchange, finalize without")
+    ap.add_argument("--configs", default="C2,C4,C5", help="config records to add (comma list, or none)")
+    ap.add_argument("--c4-rows", type=int, default=100_000_000, help="C4 global rows (sharded)")
+    ap.add_argument("--c5-rows", type=int, default=125_000_000, help="C5 rows per GPU")
+    ap.add_argument("--no-strong", action="store_true", help="no strong sub-record at N > 1")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-launch", action="store_true",
                     help="ranks print their rank env as JSON and exit before importing torch (launcher test)")
-    args = ap.parse_args()
+    return ap
+
+
+# ---------------------------------------------------------------- GPU side
+
+class Harness:
+    """One rank's clocks, barriers and collective verdicts."""
+
+    def __init__(self, torch, dist, m, ctx, world, rank, comm, same_device, exchange):
+        self.torch, self.dist, self.m, self.ctx = torch, dist, m, ctx
+        self.world, self.rank, self.comm = world, rank, comm
+        self.same_device, self.exchange = same_device, exchange
+        self.ext = torch.cuda.ExternalStream(ctx.stream)
+        torch.cuda.set_stream(self.ext)
+
+    def barrier(self):
+        self.ctx.sync()
+        self.torch.cuda.synchronize()
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def rmax(self, x):
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t[0])
+
+    def rsum(self, x):
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.int64)
+        self.dist.all_reduce(t)
+        return int(t[0])
+
+    def agree(self, reason):
+        """Every rank learns whether any rank's check failed; then each
+        failing rank prints its one-line reason and all exit non-zero."""
+        bad = int(reason is not None)
+        if self.world > 1:
+            t = self.torch.tensor([bad], dtype=self.torch.int32)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            anybad = int(t[0])
+        else:
+            anybad = bad
+        if anybad:
+            print(f"bench: pre-check failed on rank {self.rank}: {reason}" if reason else
+                  f"bench: rank {self.rank} stops: another rank's pre-check failed", file=sys.stderr, flush=True)
+            sys.stderr.flush()
+            os._exit(PRECHECK_EXIT)
+
+    def graphs(self, enqueue, k0, k1, per):
+        """HIP graphs of `per` steps each covering steps k0..k1-1 (None when
+        the runtime refuses a capture: the steps then run eagerly)."""
+        out = []
+        try:
+            k = k0
+            while k < k1:
+                g = min(per, k1 - k)
+                self.ctx.graph_begin()
+                try:
+                    enqueue(k, k + g)
+                finally:
+                    out.append(self.ctx.graph_end())
+                k += g
+            return out
+        except self.m.MbxError as err:
+            print(f"rank {self.rank}: HIP graph capture failed ({err}); eager steps", file=sys.stderr)
+            for gr in out:
+                gr.close()
+            self.ctx.sync()
+            return None
+
+    def kernel_ms(self, enqueue_one, k, reps=3):
+        """Average duration of one launch of the query's kernels: one graph of
+        k launches (enqueue_one(i), i < k), one untimed replay, then `reps`
+        replays between HIP events on the library stream; (own, max over
+        ranks).  Eager launches if the capture is refused."""
+        torch = self.torch
+        gr = self.graphs(lambda a, b: [enqueue_one(i) for i in range(a, b)], 0, k, k)
+        run = (lambda: gr[0].launch()) if gr else (lambda: [enqueue_one(i) for i in range(k)])
+        run()
+        self.ctx.sync()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(self.ext)
+        for _ in range(reps):
+            run()
+        b.record(self.ext)
+        self.ctx.sync()
+        ms = a.elapsed_time(b) / (reps * k)
+        for g in gr or []:
+            g.close()
+        return ms, self.rmax(ms)
+
+    def timed(self, enqueue, drain, steps, warmup, graph_steps, reset=None):
+        """warmup steps (eager), graphs of graph_steps captured and replayed
+        once untimed, reset(), then EXACTLY `steps` steps between barrier +
+        synchronize on both sides; (max-over-ranks ms per step, host enqueue
+        us per step, graph steps used)."""
+        enqueue(0, warmup)
+        drain()
+        gr = None
+        if graph_steps and (self.comm is not None or not self.exchange):  # gloo exchanges run eagerly
+            gr = self.graphs(enqueue, warmup, warmup + steps, graph_steps)
+            if gr:
+                for g in gr:
+                    g.launch()
+                drain()
+        if reset:
+            reset()
+        self.barrier()
+        t0 = time.perf_counter()
+        if gr:
+            for g in gr:
+                g.launch()
+        else:
+            enqueue(warmup, warmup + steps)
+        t_enq = time.perf_counter() - t0
+        drain()
+        self.torch.cuda.synchronize()
+        if self.world > 1:
+            self.dist.barrier()
+        wall = time.perf_counter() - t0
+        for g in gr or []:
+            g.close()
+        return self.rmax(wall * 1e3 / steps), t_enq * 1e6 / steps, (graph_steps if gr else 0)
+
+
+def gen_column(torch, n_global, s, e, seed, hi):
+    """Rows [s, e) of one int32 column uniform in [0, hi), generated whole
+    from its seed (torch Philox on the device), so every shard count slices
+    the same table."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    full = torch.randint(0, hi, (n_global,), dtype=torch.int32, device="cuda", generator=g)
+    if s == 0 and e == n_global:
+        return full
+    out = full[s:e].clone()
+    del full
+    return out
+
+
+def make_columns(torch, n_global, s, e, seed_base, his=(1 << 20,) * 4):
+    cols = [gen_column(torch, n_global, s, e, seed_base + j, hi) for j, hi in enumerate(his)]
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return cols
+
+
+def full_count(torch, n_global, seed_base):
+    """The global C3 COUNT of the whole table (torch reduction)."""
+    a = gen_column(torch, n_global, 0, n_global, seed_base, 1 << 20)
+    b = gen_column(torch, n_global, 0, n_global, seed_base + 1, 1 << 20)
+    c = int(((a < THRESH) & (b >= THRESH)).sum().item())
+    del a, b
+    torch.cuda.empty_cache()
+    return c
+
+
+def read_probe(H, table, reps=30):
+    """Best read bandwidth of k_read_probe (mbx_probe_read: the C3 kernel's
+    tiles and non-temporal dwordx4 loads over c0, c1 with no predicate) over a
+    few block mappings, timed with HIP events on the library stream."""
+    torch, ctx = H.torch, H.ctx
+    n = table.nrows
+    nbytes = 2 * 4 * (n // 256 * 256)
+    variants = [("segments, scan default", dict()), ("segments, tpb=256", dict(tiles_per_block=256)),
+                ("segments, tpb=96", dict(tiles_per_block=96)),
+                ("grid-stride 1024 blocks", dict(interleave=True, grid=1024)),
+                ("grid-stride 2048 blocks", dict(interleave=True, grid=2048))]
+    res = {}
+    for name, kw in variants:
+        for _ in range(3):
+            ctx.probe_read(table, [0, 1], **kw)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(H.ext)
+        for _ in range(reps):
+            ctx.probe_read(table, [0, 1], **kw)
+        b.record(H.ext)
+        ctx.sync()
+        ms = a.elapsed_time(b) / reps
+        res[name] = nbytes / (ms * 1e-3) / 1e9
+    best = max(res, key=res.get)
+    return {"best_gbs": res[best], "best": best, "gbs": res}
+
+
+def run_c3(H, args, cols, n, s, glob, label):
+    """The C3 query over one rank's shard (`cols`, rows [s, s + n)), whose
+    global COUNT over all ranks is `glob`: pre-check of one exchanged step,
+    `args.steps` timed steps (graph replay), kernel time, every step's count
+    checked.  Returns the measurements (the table stays open for the probe)."""
+    torch, ctx, m, world, rank = H.torch, H.ctx, H.m, H.world, H.rank
+    table = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [col.data_ptr() for col in cols], n, None, row_offset=s)
+    cnf = [[(m.mbx.LT, ("sym", 1), ("int", THRESH))], [(m.mbx.GE, ("sym", 2), ("int", THRESH))]]
+    plan = ctx.compile(table, cnf)
+
+    # the kernel's count vs a torch reduction of the same device columns
+    got = ctx.scan_count(plan)
+    want = int(((cols[0] < THRESH) & (cols[1] >= THRESH)).sum().item())
+    H.agree(None if got == want else f"{label}: scan count {got} != torch {want}")
+
+    # count frames (mbx_scan_count_frame_async): with an exchange, each step's
+    # scan adds its packed per-block counts into its own zeroed 4 KB frame with
+    # no-return atomics and the all-reduce sums whole frames -- the launch ends
+    # without the finalize's dependent atomic round trips.  A slot's 12-bit
+    # arrival field sums every rank's arrivals: it must stay < 4096
+    # (mbx_count_frame_fits), else the in-launch finalize is used.
+    frames = args.count == "frame" or (args.count == "auto" and H.exchange)
+    nb_own = ctx.scan_blocks(plan)
+    nb_all = H.rsum(nb_own)
+    if frames and not m.mbx.count_frame_fits(int(H.rmax(nb_own)), world):
+        if args.count == "frame":
+            raise SystemExit(f"bench: {world} ranks x {nb_own} blocks overflow a count frame")
+        frames = False
+        print(f"rank {rank}: {world} ranks x {nb_own} blocks overflow a count frame; in-launch finalize",
+              file=sys.stderr)
+    FW = m.mbx.COUNT_FRAME_WORDS if frames else 1
+    steps, warmup = args.steps, args.warmup
+    counts = torch.zeros((steps + warmup, FW), dtype=torch.int64, device="cuda")
+    base = counts.data_ptr()
+    B = max(1, args.exchange_bucket)
+    gloo_works = []
+
+    def scan(k, buf=base):
+        if frames:
+            ctx.scan_count_frame_async(plan, buf + 8 * FW * k)
+        else:
+            ctx.scan_count_async(plan, buf + 8 * k)
+
+    def enqueue(k0, k1):
+        """steps k0..k1-1: one scan each; the exchange all-reduces the COUNTs
+        of every B consecutive steps in one collective"""
+        for j in range(k0, k1, B):
+            je = min(j + B, k1)
+            for k in range(j, je):
+                scan(k)
+            if H.comm is not None:
+                H.comm.allreduce_count_async(base + 8 * FW * j, FW * (je - j))
+            elif H.exchange:  # same-device rehearsal: gloo over host copies
+                gloo_works.extend(range(j, je))
+
+    def drain():
+        ctx.sync()
+        if gloo_works:
+            h = counts[gloo_works].cpu()
+            H.dist.all_reduce(h)
+            counts[gloo_works] = h.cuda()
+            gloo_works.clear()
+        torch.cuda.synchronize()
+
+    def verify(k0, k1, kind):
+        c = counts[k0:k1].cpu().numpy()
+        if frames:
+            return check_counts(kind, None, glob if H.exchange else want, frames=c,
+                                nblocks=nb_all if H.exchange else nb_own)
+        return check_counts(kind, c[:, 0], glob if H.exchange else want)
+
+    # pre-check: ONE exchanged step, eagerly, verified on every rank before
+    # anything is timed
+    torch.cuda.synchronize()
+    enqueue(0, 1)
+    drain()
+    corrupt = os.environ.get("MBX_BENCH_CORRUPT", "")
+    if corrupt and rank == 0:  # rehearsal: a damaged frame / count must stop the run here
+        counts[0, 0] += (1 << 24) if (corrupt == "count" or not frames) else 1
+        torch.cuda.synchronize()
+    H.agree(verify(0, 1, f"{label} pre-check"))
+    counts.zero_()
+    torch.cuda.synchronize()
+
+    ms_step, enq_us, G = H.timed(enqueue, drain, steps, warmup, args.graph_steps,
+                                 reset=lambda: (counts.zero_(), torch.cuda.synchronize()))
+    reason = verify(warmup, warmup + steps, f"{label} timed steps")
+    H.agree(reason)
+
+    # kernel duration: a graph of --kernel-graph scans alone (own scratch slots)
+    KG = max(1, args.kernel_graph)
+    scratch = torch.zeros((KG, FW), dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    kern_ms, kern_max = H.kernel_ms(lambda i: scan(i, scratch.data_ptr()), KG)
+    print(f"rank {rank}: {label} rows [{s}, {s + n}), host enqueue {enq_us:.1f} us/step, "
+          f"wall {ms_step * 1e3:.1f} us/step, scan kernel {kern_ms * 1e3:.1f} us (graph of {KG})", file=sys.stderr)
+    return dict(table=table, plan=plan, frames=frames, ms_step=ms_step, enq_us=enq_us, G=G, B=B,
+                kern_ms=kern_ms, kern_max=kern_max, want=want)
+
+
+def timing_label(G, steps):
+    return f"HIP graphs of {G} queries replayed, {steps} timed" if G else f"{steps} eager queries (gloo exchange)"
+
+
+def exchange_name(H, what):
+    if H.comm is not None:
+        return what
+    if H.exchange:
+        return "gloo (same-device rehearsal)"
+    return "none"
+
+
+def config_c2(H, args):
+    """C2 (1 GPU, rank 0): 10M x 4 int32, c0 < 104858 -> BitSet + ascending
+    positions + COUNT in one launch (mbx_scan_select_async, k_scan_select);
+    ColumnarFileScan's get_next_tid stream (R/iterator/ColumnarFileScan.java:174-188)."""
+    torch, ctx, m = H.torch, H.ctx, H.m
+    n = 10_000_000
+    cols = make_columns(torch, n, 0, n, 42)
+    t = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [c.data_ptr() for c in cols], n)
+    plan = ctx.compile(t, [[(m.mbx.LT, ("sym", 1), ("int", C2_LIT))]])
+    bm = ctx.bitmap_alloc(n)
+    ids = torch.zeros(n, dtype=torch.int64, device="cuda")
+    steps, warmup = args.steps, args.warmup
+    cnt = torch.zeros(steps + warmup, dtype=torch.int64, device="cuda")
+    sel = cols[0] < C2_LIT
+    want = int(sel.sum().item())
+    wpos = torch.nonzero(sel).flatten()
+
+    def query(k):
+        ctx.scan_select_async(plan, bm, ids.data_ptr(), cnt.data_ptr() + 8 * k)
+
+    def verify(k0, k1, kind):
+        c = cnt[k0:k1].cpu().numpy()
+        r = check_counts(kind, c, want)
+        if r is None and not bool((ids[:want] == wpos).all()):
+            r = f"{kind}: positions differ from torch.nonzero"
+        return r
+
+    torch.cuda.synchronize()
+    query(0)
+    ctx.sync()
+    H.agree(verify(0, 1, "C2 pre-check"))
+    ms, _, G = H.timed(lambda a, b: [query(k) for k in range(a, b)], ctx.sync, steps, warmup, args.graph_steps,
+                       reset=lambda: (cnt.zero_(), ids.zero_(), torch.cuda.synchronize()))
+    H.agree(verify(warmup, warmup + steps, "C2 timed steps"))
+    kms, kmax = H.kernel_ms(lambda i: query(0), max(1, args.kernel_graph))
+    byts = n * 4 + n // 8 + want * 8
+    rec = config_record("C2: 10M-row 4xint32, c0 < 104858 -> BitSet + positions + COUNT (one launch)",
+                        n, n, 1, want, ms, "mbx::k_scan_select", kms, kmax, byts, "none", "ok",
+                        timing_label(G, steps))
+    del cols, t, plan, bm, ids, sel, wpos
+    torch.cuda.empty_cache()
+    return rec
+
+
+def config_c4(H, args):
+    """C4: 100M global rows sharded by row range; ColumnarIndexScan over the
+    BitMapFiles bm(c2=3) AND bm(c3=7) -> positions + projected c0, c1 in one
+    launch (mbx_cnf_materialize_async, (c0, c1) column group), at N > 1 the
+    RCCL all-gather of the per-rank counts (the concatenation offsets)."""
+    torch, ctx, m, world, rank = H.torch, H.ctx, H.m, H.world, H.rank
+    N = args.c4_rows
+    s, e = m.mbx.shard_bounds(N, world, rank)
+    n = e - s
+    c0, c1, c2, c3 = make_columns(torch, N, s, e, 42, his=(1 << 20, 1 << 20, 10, 10))
+    t = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [x.data_ptr() for x in (c0, c1, c2, c3)], n, row_offset=s)
+    bm2 = ctx.index_build(t, 2, [("int", v) for v in range(10)])
+    bm3 = ctx.index_build(t, 3, [("int", v) for v in range(10)])
+    a, b = bm2[3], bm3[7]
+    ctx.group(t, [0, 1])
+    sel = (c2 == 3) & (c3 == 7)
+    want = int(sel.sum().item())
+    cap = max(1, n // 50)
+    ids = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    o0 = torch.zeros(cap, dtype=torch.int32, device="cuda")
+    o1 = torch.zeros(cap, dtype=torch.int32, device="cuda")
+    steps, warmup = args.steps, args.warmup
+    cnts = torch.zeros(steps + warmup, dtype=torch.int64, device="cuda")
+    alls = torch.zeros(steps + warmup, world, dtype=torch.int64, device="cuda")
+    conj = [[a], [b]]
+    glob = H.rsum(want)
+    gloo = []
+
+    def launch(k):
+        ctx.cnf_materialize_async(t, conj, [0, 1], ids.data_ptr(), [o0.data_ptr(), o1.data_ptr()],
+                                  cnts.data_ptr() + 8 * k)
+
+    def enqueue(k0, k1):
+        for k in range(k0, k1):
+            launch(k)
+            if H.comm is not None:
+                H.comm.allgather_count_async(cnts.data_ptr() + 8 * k, alls[k].data_ptr())
+            elif world > 1:
+                gloo.append(k)
+
+    def drain():
+        ctx.sync()
+        if gloo:
+            parts = [torch.empty(len(gloo), dtype=torch.int64) for _ in range(world)]
+            H.dist.all_gather(parts, cnts[gloo].cpu())
+            alls[gloo] = torch.stack(parts, 1).cuda()
+            gloo.clear()
+        torch.cuda.synchronize()
+
+    def verify(k0, k1, kind):
+        r = check_counts(kind + " (own)", cnts[k0:k1].cpu().numpy(), want)
+        al = alls[k0:k1] if (H.comm is not None or world > 1) else cnts[k0:k1].unsqueeze(1)  # no exchange at N = 1
+        if r is None:
+            r = check_counts(kind + " (all-gathered)", al.sum(1).cpu().numpy(), glob)
+        if r is None and not bool((al[:, rank] == want).all()):
+            r = f"{kind}: all-gathered slot {rank} != own count {want}"
+        if r is None and want > cap:
+            r = f"{kind}: {want} rows exceed the output capacity {cap}"
+        if r is None and not (bool((o0[:want] == c0[sel]).all()) and bool((o1[:want] == c1[sel]).all())
+                              and bool((ids[:want] == torch.nonzero(sel).flatten() + s).all())):
+            r = f"{kind}: positions / projected rows differ from torch"
+        return r
+
+    torch.cuda.synchronize()
+    enqueue(0, 1)
+    drain()
+    H.agree(verify(0, 1, "C4 pre-check"))
+
+    def reset():
+        cnts.zero_(), alls.zero_(), o0.zero_(), o1.zero_(), ids.zero_()
+        torch.cuda.synchronize()
+
+    ms, _, G = H.timed(enqueue, drain, steps, warmup, args.graph_steps, reset=reset)
+    H.agree(verify(warmup, warmup + steps, "C4 timed steps"))
+    kms, kmax = H.kernel_ms(lambda i: launch(0), max(1, args.kernel_graph))
+    byts = 2 * ((n + 63) // 64) * 8 + want * (8 + 8)
+    rec = config_record(
+        "C4: 100M-row BitMapFile AND bm(c2=3) ^ bm(c3=7) -> positions + c0, c1 (one launch, column group), "
+        "row-range sharded", N, n, world, glob, ms, "mbx::k_cnf_select", kms, kmax, byts,
+        exchange_name(H, "RCCL all-gather of the per-rank counts (libmbx mbx_comm, after each query)"), "ok",
+        timing_label(G, steps),
+        algorithmic_bytes_global=2 * N // 8 + glob * 16)
+    del c0, c1, c2, c3, t, bm2, bm3, a, b, ids, o0, o1, sel, conj
+    torch.cuda.empty_cache()
+    return rec
+
+
+def c5_dictionary(torch):
+    """50 ASCII names of <= 16 characters, zero padded."""
+    names = [f"{chr(65 + (i * 7) % 26)}{'abcdefghijklmnop'[:(i % 15) + 1]}"[:16] for i in range(50)]
+    dic = torch.zeros(50, 16, dtype=torch.uint8)
+    for i, nm in enumerate(names):
+        dic[i, :len(nm)] = torch.tensor(list(nm.encode()), dtype=torch.uint8)
+    return dic.cuda()
+
+
+def config_c5(H, args):
+    """C5: 125M rows per GPU (1B over 8) of i32 / f32 / char(16),
+    (c0 < 2^19) ^ (c1 >= 0.25) ^ (c2 >= "M") -> COUNT, SUM / MIN / MAX(c1) in
+    one scan; at N > 1 the RCCL all-gather of the 48-byte records + the
+    device rank-ordered fold (mbx_comm_allreduce_agg_async)."""
+    torch, ctx, m, world, rank = H.torch, H.ctx, H.m, H.world, H.rank
+    D = m.dist
+    n = args.c5_rows
+    N, s = n * world, n * rank
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5 + 1000 * rank)
+    c0 = torch.randint(0, 1 << 20, (n,), dtype=torch.int32, device="cuda", generator=g)
+    c1 = torch.rand((n,), dtype=torch.float32, device="cuda", generator=g)
+    dic = c5_dictionary(torch)
+    c2 = torch.empty((n, 16), dtype=torch.uint8, device="cuda")
+    chunk = 1 << 23  # one advanced-index launch per chunk (tests/helpers.device_dictionary_column)
+    for a in range(0, n, chunk):
+        idx = torch.randint(0, 50, (min(chunk, n - a),), dtype=torch.int64, device="cuda", generator=g)
+        c2[a:a + chunk].copy_(dic[idx])
+    t = ctx.wrap([(m.mbx.INTEGER, 4), (m.mbx.REAL, 4), (m.mbx.STRING, 16)],
+                 [c0.data_ptr(), c1.data_ptr(), c2.data_ptr()], n, row_offset=s)
+    cnf = [[(m.mbx.LT, ("sym", 1), ("int", 1 << 19))], [(m.mbx.GE, ("sym", 2), ("real", 0.25))],
+           [(m.mbx.GE, ("sym", 3), ("str", "M"))]]
+    plan = ctx.compile(t, cnf)
+    sel = (c0 < (1 << 19)) & (c1 >= 0.25) & (c2[:, 0] >= ord("M"))
+    want = dict(count=int(sel.sum().item()), sum=float(torch.where(sel, c1.double(), 0.0).sum().item()),
+                min=float(torch.where(sel, c1, float("inf")).min().item()),
+                max=float(torch.where(sel, c1, float("-inf")).max().item()))
+    del sel
+    gwant = D.combine_aggregate(want) if world > 1 else want
+    W = D.AGG_WORDS
+    steps, warmup = args.steps, args.warmup
+    recs = torch.zeros(steps + warmup, W, dtype=torch.int64, device="cuda")
+    gathered = torch.zeros(world, W, dtype=torch.int64, device="cuda")
+    gloo = []
+
+    def scan(k):
+        ctx.scan_aggregate_async(plan, 1, recs[k].data_ptr())
+
+    def enqueue(k0, k1):
+        for k in range(k0, k1):
+            scan(k)
+            if H.comm is not None:  # all-gather + rank-ordered fold into recs[k], on the device
+                H.comm.allreduce_agg_async(recs[k].data_ptr())
+            elif world > 1:
+                gloo.append(k)
+
+    def drain():
+        ctx.sync()
+        for k in gloo:  # rehearsal: gloo all-gather of the records, then the same device fold
+            parts = [torch.empty(W, dtype=torch.int64) for _ in range(world)]
+            H.dist.all_gather(parts, recs[k].cpu())
+            gathered.copy_(torch.stack(parts))
+            torch.cuda.synchronize()
+            ctx.agg_fold_async(gathered.data_ptr(), world, recs[k].data_ptr())
+            ctx.sync()
+        gloo.clear()
+        torch.cuda.synchronize()
+
+    def verify(k0, k1, kind):
+        h = recs[k0:k1].cpu().numpy()
+        for k in range(h.shape[0]):
+            r = check_aggregate(kind, D.fold_aggregates(h[k]), gwant)
+            if r:
+                return r
+        return None
+
+    # own record first (no exchange), then one exchanged step
+    torch.cuda.synchronize()
+    scan(0)
+    ctx.sync()
+    H.agree(check_aggregate("C5 pre-check (own shard)", D.fold_aggregates(recs[0].cpu().numpy()), want))
+    recs.zero_()
+    torch.cuda.synchronize()
+    enqueue(0, 1)
+    drain()
+    H.agree(verify(0, 1, "C5 pre-check"))
+    ms, _, G = H.timed(enqueue, drain, steps, warmup, args.graph_steps,
+                       reset=lambda: (recs.zero_(), torch.cuda.synchronize()))
+    H.agree(verify(warmup, warmup + steps, "C5 timed steps"))
+    kms, kmax = H.kernel_ms(lambda i: scan(0), max(1, args.kernel_graph))
+    glob = D.fold_aggregates(recs[-1].cpu().numpy())
+    rec = config_record(
+        "C5: mixed int32 / float32 / char(16), (c0 < 2^19) ^ (c1 >= 0.25) ^ (c2 >= \"M\") -> COUNT, SUM / MIN / "
+        "MAX(c1), 125M rows per GPU", N, n, world, glob["count"], ms, "mbx::k_scan_fast<aggregate>", kms, kmax,
+        n * 24, exchange_name(H, "RCCL all-gather of the 48-byte records + device rank-ordered fold (libmbx)"), "ok",
+        timing_label(G, steps),
+        sum=glob["sum"], min=glob["min"], max=glob["max"])
+    del c0, c1, c2, t, plan, recs
+    torch.cuda.empty_cache()
+    return rec
+
+
+def main():
+    args = make_parser().parse_args()
     if args.gpus < 1:
         print(f"bench: --gpus {args.gpus}", file=sys.stderr)
         sys.exit(2)
@@ -260,6 +829,11 @@ def main():
         print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world, "gpus": args.gpus,
                           "torch_imported": "torch" in sys.modules, "env": env}), flush=True)
         return
+    configs = [c.strip().upper() for c in args.configs.split(",") if c.strip() and c.strip().lower() != "none"]
+    bad = [c for c in configs if c not in ("C2", "C4", "C5")]
+    if bad:
+        print(f"bench: unknown config(s) {bad}", file=sys.stderr)
+        sys.exit(2)
     out_fd = quiet_stdout()
 
     import torch
@@ -267,260 +841,103 @@ def main():
 
     import mbx_pkg
 
-    # rehearsal knob (never set by the driver): MBX_BENCH_SAME_DEVICE=1 runs N
-    # ranks on one GPU (RCCL refuses two ranks on one device, so the exchange
-    # then goes over gloo on the host)
     same_device = os.environ.get("MBX_BENCH_SAME_DEVICE") == "1"
     device = 0 if same_device else local_rank
     torch.cuda.set_device(device)
-    # MBX_BENCH_FORCE_EXCHANGE=1 keeps the per-step exchange at N=1 (a one-rank
-    # RCCL clique): the N>1 step on one GPU
     exchange = world > 1 or os.environ.get("MBX_BENCH_FORCE_EXCHANGE") == "1"
     if world > 1:
-        # host-side bootstrap, barriers and the max-over-ranks clock only: the
-        # data-path exchange is libmbx's own RCCL communicator
+        # host-side bootstrap, barriers, verdicts and the max-over-ranks clock
+        # only: the data-path exchange is libmbx's own RCCL communicator
         dist.init_process_group("gloo")
     m = mbx_pkg.load()
     ctx = m.Context(device)
 
-    n_global = args.rows if args.scaling == "strong" else args.rows * world
-    if args.scaling == "strong":
-        s, e = m.mbx.shard_bounds(args.rows, world, rank)
-        seed_base = 42
-    else:
-        s, e = rank * args.rows, (rank + 1) * args.rows
-        seed_base = 42 + 1000 * rank
-    n = e - s
-
-    # synthetic C3 shard, generated in HBM: 4 x int32 uniform [0, 2^20)
-    if args.scaling == "strong":
-        cols = make_columns(torch, args.rows, s, e, seed_base)
-    else:
-        cols = make_columns(torch, n, 0, n, seed_base)
-    table = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [col.data_ptr() for col in cols], n, None, row_offset=s)
-    cnf = [[(m.mbx.LT, ("sym", 1), ("int", THRESH))], [(m.mbx.GE, ("sym", 2), ("int", THRESH))]]
-    plan = ctx.compile(table, cnf)
-
     comm = None
-    torch_pg = None  # fallback exchange: torch.distributed's own RCCL group
     if exchange and not same_device:
         uid = m.mbx.comm_unique_id() if rank == 0 else None
         if world > 1:
             box = [uid]
             dist.broadcast_object_list(box, src=0)
             uid = box[0]
-        ok = 1
         try:
             comm = ctx.comm_init_rank(world, rank, uid)
+            reason = None
         except m.MbxError as err:
-            if world == 1:
-                raise
-            ok = 0
-            print(f"rank {rank}: libmbx RCCL communicator failed ({err})", file=sys.stderr)
-        if world > 1:
-            # every rank takes the same exchange: libmbx's communicator if it
-            # came up everywhere, else torch.distributed's RCCL group (eager)
-            flag = torch.tensor([ok], dtype=torch.int32)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if int(flag[0]) == 0:
-                if comm is not None:
-                    comm.close()
-                    comm = None
-                torch_pg = dist.new_group(backend="nccl")
-                print(f"rank {rank}: exchange falls back to torch.distributed (nccl = RCCL)", file=sys.stderr)
+            reason = f"libmbx RCCL communicator failed ({err})"
+    H = Harness(torch, dist, m, ctx, world, rank, comm, same_device, exchange)
+    if exchange and not same_device:
+        H.agree(reason)
 
-    # correctness gate before timing: the kernel's count vs a torch reduction
-    # of the same device columns; with the exchange, the global count vs the
-    # whole table (strong) (the oracle cross-check lives in tests/)
-    got = ctx.scan_count(plan)
-    want = int(((cols[0] < THRESH) & (cols[1] >= THRESH)).sum().item())
-    assert got == want, f"rank {rank}: scan count {got} != reference {want}"
-
-    steps, warmup = args.steps, args.warmup
-    # count frames (mbx_scan_count_frame_async): with an exchange, each step's
-    # scan adds its packed per-block counts into its own zeroed 4 KB frame with
-    # no-return atomics and the all-reduce sums whole frames -- the launch ends
-    # without the finalize's dependent atomic round trips
-    frames = args.count == "frame" or (args.count == "auto" and exchange)
-    if frames:
-        # a frame slot's 12-bit arrival field sums every rank's arrivals: it
-        # must stay < 4096 (mbx_count_frame_fits); otherwise the in-launch
-        # finalize (one int64 per rank, summed exactly) is used
-        nb = ctx.scan_blocks(plan)
-        if world > 1:
-            tb = torch.tensor([nb], dtype=torch.int64)
-            dist.all_reduce(tb, op=dist.ReduceOp.MAX)
-            nb = int(tb[0])
-        if not m.mbx.count_frame_fits(nb, world):
-            if args.count == "frame":
-                raise SystemExit(f"bench: {world} ranks x {nb} blocks overflow a count frame")
-            frames = False
-            print(f"rank {rank}: {world} ranks x {nb} blocks overflow a count frame; in-launch finalize",
-                  file=sys.stderr)
-    FW = m.mbx.COUNT_FRAME_WORDS if frames else 1
-    counts = torch.zeros((steps + warmup, FW), dtype=torch.int64, device="cuda")
-    ext = torch.cuda.ExternalStream(ctx.stream)
-    torch.cuda.set_stream(ext)
-    base = counts.data_ptr()
-    gloo_works = []
-
-    B = max(1, args.exchange_bucket)
-    # diagnostic (MBX_BENCH_XS_KERNEL=1): one more real kernel per step where
-    # the collective runs (an aggregate all-gather + device fold of a dummy
-    # record), standing in on one GPU for an N-rank collective's kernel
-    xs_kernel = comm is not None and os.environ.get("MBX_BENCH_XS_KERNEL") == "1"
-    dummy = torch.zeros(8, dtype=torch.int64, device="cuda") if xs_kernel else None
-
-    def run_steps(k0, k1):
-        """steps k0..k1-1: one scan each; the exchange all-reduces the COUNTs
-        of every B consecutive steps in one collective (bucketed: each step's
-        count is still combined over all ranks, B per collective)"""
-        for j in range(k0, k1, B):
-            je = min(j + B, k1)
-            for k in range(j, je):
-                if frames:
-                    ctx.scan_count_frame_async(plan, base + 8 * FW * k)
-                else:
-                    ctx.scan_count_async(plan, base + 8 * k)
-            if comm is not None:
-                comm.allreduce_count_async(base + 8 * FW * j, FW * (je - j))
-                if xs_kernel:
-                    comm.allreduce_agg_async(dummy.data_ptr())
-            elif torch_pg is not None:
-                dist.all_reduce(counts[j:je], group=torch_pg)
-            elif exchange:  # same-device rehearsal: gloo over host copies
-                gloo_works.extend(range(j, je))
-
-    def drain():
-        ctx.sync()
-        if gloo_works:
-            h = counts[gloo_works].cpu()
-            dist.all_reduce(h)
-            counts[gloo_works] = h.cuda()
-            gloo_works.clear()
-
-    run_steps(0, warmup)
-    drain()
-
-    # HIP graphs of G steps each (the timed region replays them); captured
-    # after the warm-up, which sized every scratch buffer
-    G = args.graph_steps if (args.graph_steps > 0 and not gloo_works and not (exchange and comm is None)) else 0
-    if torch_pg is not None:
-        G = 0
-    graphs = []
-    if G:
-        try:
-            k0 = warmup
-            while k0 < warmup + steps:
-                g = min(G, warmup + steps - k0)
-                ctx.graph_begin()
-                try:
-                    run_steps(k0, k0 + g)
-                finally:
-                    graphs.append(ctx.graph_end())
-                k0 += g
-            for gr in graphs:  # one untimed replay
-                gr.launch()
-            drain()
-        except m.MbxError as err:
-            # a capture the runtime refuses (e.g. a collective it cannot
-            # capture) is not fatal: the steps run eagerly instead
-            print(f"rank {rank}: HIP graph capture failed ({err}); timing eager steps", file=sys.stderr)
-            for gr in graphs:
-                gr.close()
-            graphs, G = [], 0
-            ctx.sync()
-    counts.zero_()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-
-    # timed region: exactly `steps` steps, barrier + synchronize on both sides
-    t0 = time.perf_counter()
-    if G:
-        for gr in graphs:
-            gr.launch()
+    # ---- headline: C3 ------------------------------------------------------
+    if args.scaling == "strong":
+        n_global = args.rows
+        s, e = m.mbx.shard_bounds(args.rows, world, rank)
+        cols = make_columns(torch, args.rows, s, e, 42)
+        glob = full_count(torch, n_global, 42) if exchange else None
     else:
-        run_steps(warmup, warmup + steps)
-    t_enq = time.perf_counter() - t0  # host enqueue time of the steps (diagnostic, stderr)
-    drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    if frames:
-        # decode every step's frame (mbx_count_frame_decode's sums, on the
-        # device): count = sum of the slots' high bits; every block of every
-        # rank must have arrived exactly once
-        slots = counts[warmup:].view(steps, 32, 16)[:, :, 0]
-        c = (slots >> 24).sum(1).cpu()
-        arrivals = (slots & 0xFFF).sum(1).cpu()
-        nblocks = ctx.scan_blocks(plan)
-        if world > 1:  # shards may differ by a block: the frames hold every rank's
-            tb = torch.tensor([nblocks], dtype=torch.int64)
-            dist.all_reduce(tb)
-            nblocks = int(tb[0])
-        assert bool((arrivals == nblocks).all()), f"rank {rank}: frame arrivals {arrivals[:4].tolist()} != {nblocks}"
-        assert int(((slots >> 12) & 0xFFF).sum()) == 0, "NaN blocks in an integer plan"
-        h0 = counts[warmup].cpu().numpy()
-        assert m.mbx.count_frame_decode(h0)[0] == int(c[0])
-    else:
-        c = counts[warmup:, 0].cpu()
+        n_global = args.rows * world
+        s, e = rank * args.rows, (rank + 1) * args.rows
+        cols = make_columns(torch, args.rows, 0, args.rows, 42 + 1000 * rank)
+        glob = None
+    n = e - s
+    if glob is None and exchange:  # weak: the sum of every rank's own torch count
+        glob = H.rsum(int(((cols[0] < THRESH) & (cols[1] >= THRESH)).sum().item()))
+    r3 = run_c3(H, args, cols, n, s, glob, "C3")
+    probe = read_probe(H, r3["table"]) if rank == 0 else None
+    r3["table"].close()
+    r3["plan"].close()
+    del cols
+    torch.cuda.empty_cache()
 
-    # kernel duration: the scans alone again, each bracketed by HIP events
-    # recorded on the stream the kernel runs on (the library's stream)
-    ev_s = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    ev_e = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    for k in range(steps):
-        ev_s[k].record(ext)
-        if frames:
-            ctx.scan_count_frame_async(plan, base + 8 * FW * (warmup + k))
-        else:
-            ctx.scan_count_async(plan, base + 8 * (warmup + k))
-        ev_e[k].record(ext)
-    ctx.sync()
-    kern_ms = sum(a.elapsed_time(b) for a, b in zip(ev_s, ev_e)) / steps
-    print(f"rank {rank}: rows [{s}, {e}), host enqueue {t_enq * 1e6 / steps:.1f} us/step, "
-          f"wall {wall * 1e6 / steps:.1f} us/step, scan kernel {kern_ms * 1e3:.1f} us", file=sys.stderr)
-    probe = read_probe(ctx, table, ext, torch) if rank == 0 else None
+    # ---- strong sub-record at N > 1: the metric's ONE 100M-row table ----------
+    strong = None
+    if world > 1 and args.scaling == "weak" and not args.no_strong:
+        ss, se = m.mbx.shard_bounds(args.rows, world, rank)
+        scols = make_columns(torch, args.rows, ss, se, 42)
+        sglob = full_count(torch, args.rows, 42)
+        rs = run_c3(H, args, scols, se - ss, ss, sglob, "C3 strong")
+        rs["table"].close()
+        rs["plan"].close()
+        del scols
+        torch.cuda.empty_cache()
+        strong = {"rows": args.rows, "rows_per_gpu_rank0": se - ss if rank == 0 else None,
+                  "value": args.rows / (rs["ms_step"] * 1e-3), "unit": "rows/s", "ms_per_step": rs["ms_step"],
+                  "phases_us": {"step_wall": rs["ms_step"] * 1e3, "scan_kernel_max_over_ranks": rs["kern_max"] * 1e3,
+                                "exchange_and_overlap": max(0.0, (rs["ms_step"] - rs["kern_max"]) * 1e3)},
+                  "count": "frame" if rs["frames"] else "finalize", "graph_steps": rs["G"], "pre_check": "ok"}
+        if rank == 0:
+            strong["rows_per_gpu_rank0"] = se - ss
 
-    if exchange:
-        if args.scaling == "strong":
-            glob = full_count(torch, n_global, seed_base)
-        else:  # the sum of every rank's own torch count
-            tw = torch.tensor([want], dtype=torch.int64)
-            if world > 1:
-                dist.all_reduce(tw)
-            glob = int(tw[0])
-        assert bool((c == glob).all()), f"rank {rank}: per-step global counts {c[:4].tolist()} != {glob}"
-    else:
-        assert bool((c == got).all()), "per-step counts differ"
-
-    t_max, kern_max = wall, kern_ms
-    if world > 1:
-        tt = torch.tensor([wall, kern_ms], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max, kern_max = float(tt[0]), float(tt[1])
+    # ---- the other BASELINE configs ------------------------------------------
+    crecs = {}
+    for name in configs:
+        if name == "C2":
+            if rank == 0:
+                crecs["C2"] = config_c2(Harness1(H), args)
+            H.barrier()
+        elif name == "C4":
+            crecs["C4"] = config_c4(H, args)
+        elif name == "C5":
+            crecs["C5"] = config_c5(H, args)
 
     if rank == 0:
-        total_rows = n_global * steps
-        ms_per_step = t_max * 1e3 / steps
+        steps = args.steps
+        ms_per_step = r3["ms_step"]
+        kern_ms, kern_max, frames = r3["kern_ms"], r3["kern_max"], r3["frames"]
         algo_bytes = 2 * 4 * n  # c0 + c1 read once per launch (rank 0's shard)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+        B = r3["B"]
         xchg = ((f"RCCL all-reduce of the COUNTs of every {B} steps (libmbx mbx_comm, after the scans)" if B > 1
                  else "RCCL all-reduce of every step's COUNT (one collective per query; libmbx mbx_comm, right "
                       "after the step's scan on the same stream)")
-                if comm is not None else None) or (
-            "torch.distributed RCCL all-reduce per step (fallback: libmbx's communicator failed)" if torch_pg is not None
-            else None) or ("gloo all-reduce (same-device rehearsal)" if exchange else "none")
+                if comm is not None else None) or ("gloo all-reduce (same-device rehearsal)" if exchange else "none")
         out = {
             "metric": METRIC,
-            "value": total_rows / t_max,
+            "value": n_global * steps / (ms_per_step * 1e-3 * steps),
             "unit": "rows/s",
             "n_gpus": world,
             "steps": steps,
-            "warmup": warmup,
+            "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": args.scaling,
@@ -537,18 +954,20 @@ def main():
                 "rows_per_gpu": n,
                 "parallelism": f"row-range shards x{world}",
                 "exchange": xchg,
-                "graph_steps": G,
+                "graph_steps": r3["G"],
                 "exchange_bucket_steps": B if exchange else None,
                 "count": "frame (32 packed slots per query, summed by the all-reduce; mbx_scan_count_frame_async)"
                          if frames else "in-launch finalize (mbx_scan_count_async)",
             },
+            "pre_check": "ok: one exchanged step verified on every rank before timing" if exchange else
+                         "ok: one step verified before timing",
             "phases_us": {
                 "step_wall": ms_per_step * 1e3,
                 "scan_kernel_max_over_ranks": kern_max * 1e3,
-                "host_enqueue_rank0": t_enq * 1e6 / steps,
+                "host_enqueue_rank0": r3["enq_us"],
                 "exchange_and_overlap": max(0.0, ms_per_step * 1e3 - kern_max * 1e3),
             },
-            "hbm_gbs": 2 * 4 * n_global / (t_max / steps) / 1e9,
+            "hbm_gbs": 2 * 4 * n_global / (ms_per_step * 1e-3) / 1e9,
             "roofline": {
                 "bound": "hbm",
                 "kernel": "mbx::k_scan_fast<2, COUNT, no-deleted>",
@@ -560,6 +979,8 @@ def main():
                 "traffic_unit": "HBM bytes per launch of rank 0's shard scan (rocprofv3 PMC, "
                                 "profiles/c3_scan_pmc.json, same rows and COUNT form)",
                 "kernel_ms": kern_ms,
+                "kernel_timing": f"one HIP graph of {max(1, args.kernel_graph)} scans replayed 3 times, HIP events "
+                                 "on the library stream / launches",
                 "algorithmic_bytes_per_launch": algo_bytes,
                 # secondary denominator: the best read rate of the
                 # scan's own load pattern with the predicate removed
@@ -567,20 +988,28 @@ def main():
                 "frac_of_measured_read_peak": achieved / probe["best_gbs"],
                 "read_probe": probe,
             },
+            "strong": strong,
+            "configs": crecs,
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline:
-            # rank 0, after the timed region, over rank 0's shard (the other
+            # rank 0, after the timed regions, over rank 0's shard (the other
             # ranks wait at the closing barrier)
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
         os.write(out_fd, (json.dumps(out) + "\n").encode())
 
-    for gr in graphs:
-        gr.close()
     ctx.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+class Harness1(Harness):
+    """Rank 0 alone (a 1-GPU config inside an N-rank run): no collectives."""
+
+    def __init__(self, H):  # noqa: super().__init__ not called: shares H's state
+        self.__dict__.update(H.__dict__)
+        self.world, self.comm, self.exchange = 1, None, False
 
 
 if __name__ == "__main__":

@@ -382,6 +382,13 @@ int mbx_comm_scan_count_async(mbx_comm *comm, const mbx_plan *plan, int64_t *dev
                               int64_t *dev_count);
 /* dev_all[r] = rank r's *dev_count (device memory, nranks entries) */
 int mbx_comm_allgather_count_async(mbx_comm *comm, const int64_t *dev_count, int64_t *dev_all);
+/* The aggregate combine's fold alone: *dev_out = the rank-ordered fold of
+ * dev_recs[0..n) (device memory; dev_out may alias dev_recs[0]) on the context
+ * stream -- exactly what mbx_comm_allreduce_agg_async runs after its
+ * all-gather (dist.fold_aggregates restated on the device: COUNT and int SUM
+ * exact, the double SUM added in record order, MIN / MAX over the records,
+ * whose empty shards carry the identities). */
+int mbx_agg_fold_async(mbx_ctx *ctx, const mbx_agg *dev_recs, int32_t n, mbx_agg *dev_out);
 /* one process, n communicators of one mbx_comm_init_all clique (rank order) */
 int mbx_comm_allreduce_count_all(mbx_comm *const *comms, int32_t n, int64_t *const *dev_counts, int64_t count);
 int mbx_comm_allreduce_agg_all(mbx_comm *const *comms, int32_t n, mbx_agg *const *dev_recs);

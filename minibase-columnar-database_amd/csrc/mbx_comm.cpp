@@ -293,6 +293,19 @@ extern "C" int mbx_comm_allreduce_agg_async(mbx_comm* m, mbx_agg* dev_rec) {
   return MBX_OK;
 }
 
+// the fold alone, over a caller's record array (a one-process caller that
+// gathered the records itself; the 8-rank combine exercised on one GPU)
+extern "C" int mbx_agg_fold_async(mbx_ctx* c, const mbx_agg* dev_recs, int32_t n, mbx_agg* dev_out) {
+  NOTNULL(c);
+  NOTNULL(dev_recs);
+  NOTNULL(dev_out);
+  if (n <= 0) return fail(MBX_E_INVALID, "agg_fold: %d records", n);
+  HIPCHK(hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_fold_agg, dim3(1), dim3(64), 0, c->stream, (const AggOut*)dev_recs, n, (AggOut*)dev_out);
+  HIPCHK(hipGetLastError());
+  return MBX_OK;
+}
+
 extern "C" int mbx_comm_allgather_count_async(mbx_comm* m, const int64_t* dev_count, int64_t* dev_all) {
   NOTNULL(m);
   NOTNULL(dev_count);

@@ -92,7 +92,7 @@ EXPORTS = [
     "mbx_probe_read", "mbx_set_tuning",
     "mbx_diag_select_stamps", "mbx_diag_lookback_epoch", "mbx_dev_alloc", "mbx_dev_free", "mbx_dev_download", "mbx_shard_bounds", "mbx_comm_unique_id", "mbx_comm_init_rank", "mbx_comm_init_all", "mbx_comm_free",
     "mbx_comm_info", "mbx_comm_wait", "mbx_comm_allreduce_count_async", "mbx_comm_scan_count_async",
-    "mbx_comm_allreduce_agg_async",
+    "mbx_comm_allreduce_agg_async", "mbx_agg_fold_async",
     "mbx_comm_allgather_count_async", "mbx_comm_allreduce_count_all", "mbx_comm_allreduce_agg_all",
     "mbx_comm_allgather_count_all",
     "mbx_graph_begin", "mbx_graph_end", "mbx_graph_launch", "mbx_graph_free",
@@ -196,6 +196,7 @@ def lib():
         "mbx_comm_allreduce_count_async": ([V, V, I64], ctypes.c_int),
         "mbx_comm_scan_count_async": ([V, V, V, I64, V], ctypes.c_int),
         "mbx_comm_allreduce_agg_async": ([V, V], ctypes.c_int),
+        "mbx_agg_fold_async": ([V, V, I32, V], ctypes.c_int),
         "mbx_comm_allgather_count_async": ([V, V, V], ctypes.c_int),
         "mbx_comm_allreduce_count_all": ([P(V), I32, P(V), I64], ctypes.c_int),
         "mbx_comm_allreduce_agg_all": ([P(V), I32, P(V)], ctypes.c_int),
@@ -652,6 +653,11 @@ class Context:
         buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
         _chk(lib().mbx_comm_init_rank(self.h, nranks, rank, buf, ctypes.byref(h)))
         return Comm(self, h, nranks, rank)
+
+    def agg_fold_async(self, dev_recs, n, dev_out):
+        """mbx_agg_fold_async: *dev_out = the rank-ordered fold of n 48-byte
+        records at dev_recs (the aggregate exchange's fold, without RCCL)."""
+        _chk(lib().mbx_agg_fold_async(self.h, dev_recs, n, dev_out))
 
     def graph_begin(self):
         _chk(lib().mbx_graph_begin(self.h))

@@ -77,3 +77,71 @@ def test_count_frame_fits():
     assert not m.count_frame_fits(32 * 255, 17)      # 4335 arrivals: would carry into the NaN bits
     assert m.count_frame_fits(32 * 127, 32) and not m.count_frame_fits(32 * 128, 32)
     assert not m.count_frame_fits(10, 0)
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", BENCH)
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+def test_default_run_adds_every_config_record():
+    """The driver's plain `bench.py --gpus N` measures C2, C4 and C5 beside
+    the C3 headline, and every record carries CONFIG_KEYS
+    with kernel time from graph replay."""
+    b = _bench_module()
+    a = b.make_parser().parse_args([])
+    assert a.configs == "C2,C4,C5" and a.scaling == "weak" and not a.no_strong
+    assert a.c4_rows == 100_000_000 and a.c5_rows == 125_000_000 and a.kernel_graph >= 10
+    rec = b.config_record("C4", 100_000_000, 50_000_000, 2, 1_000_000, 0.040, "k", 0.030, 0.031, 33_000_000,
+                          "RCCL", "ok", "graph replay")
+    assert set(b.CONFIG_KEYS) <= set(rec)
+    assert abs(rec["achieved_gbs"] - 1100.0) < 1e-6 and abs(rec["frac"] - 1100.0 / 8000.0) < 1e-12
+    assert abs(rec["rows_per_s"] - 100_000_000 / 40e-6) < 1
+
+
+def _frame(count, arrivals, nan=0, slots=32):
+    import numpy as np
+    f = np.zeros(512, dtype=np.int64)
+    for i in range(slots):  # spread over the slots like blockIdx % 32
+        c = count // slots + (1 if i < count % slots else 0)
+        a = arrivals // slots + (1 if i < arrivals % slots else 0)
+        f[16 * i] = (c << 24) | ((nan if i == 0 else 0) << 12) | a
+    return f
+
+
+def test_precheck_fires_on_a_wrong_frame_or_count():
+    """bench.py's pre-check (one exchanged step, verified before timing):
+    exact frames pass; a missing / duplicated block arrival, a NaN block or
+    a wrong global COUNT each give a one-line reason."""
+    import numpy as np
+    b = _bench_module()
+    nb = 2 * 1000  # two ranks x 1000 blocks
+    good = np.stack([_frame(12_345_678, nb), _frame(12_345_678, nb)])
+    assert b.check_counts("C3", None, 12_345_678, frames=good, nblocks=nb) is None
+    c, nan, arr = b.frame_fields(good)
+    assert c.tolist() == [12_345_678] * 2 and arr.tolist() == [nb] * 2 and nan.tolist() == [0, 0]
+    late = good.copy()
+    late[1, 16 * 5] -= 1                                      # one block of step 1 never arrived
+    assert "arrivals" in b.check_counts("C3", None, 12_345_678, frames=late, nblocks=nb)
+    dup = good.copy()
+    dup[0, 0] += 1                                            # MBX_BENCH_CORRUPT=frame
+    assert "arrivals" in b.check_counts("C3", None, 12_345_678, frames=dup, nblocks=nb)
+    wrong = good.copy()
+    wrong[0, 0] += 1 << 24                                    # MBX_BENCH_CORRUPT=count
+    assert "COUNT" in b.check_counts("C3", None, 12_345_678, frames=wrong, nblocks=nb)
+    nanf = np.stack([_frame(5, nb, nan=1)])
+    assert "NaN" in b.check_counts("C3", None, 5, frames=nanf, nblocks=nb)
+    assert b.check_counts("C3", [7, 7, 7], 7) is None
+    assert "COUNT" in b.check_counts("C3", [7, 8, 7], 7)
+
+
+def test_aggregate_check_tolerances():
+    b = _bench_module()
+    want = dict(count=10, sum=1.0e6, min=0.25, max=0.99)
+    assert b.check_aggregate("C5", dict(want, sum=1.0e6 * (1 + 5e-7)), want) is None
+    assert "sum" in b.check_aggregate("C5", dict(want, sum=1.0e6 * (1 + 2e-6)), want)
+    assert "count" in b.check_aggregate("C5", dict(want, count=11), want)
+    assert "min" in b.check_aggregate("C5", dict(want, min=0.2500001), want)

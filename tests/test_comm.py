@@ -215,3 +215,54 @@ def test_comm_scan_count_parts_and_exchange(m, torch_cuda, deleted):
         ctx.sync()
     finally:
         ctx.close()
+
+
+def _records(m, kind, n, seed):
+    """n rank records of one aggregate kind, rank 1 and rank n-2 empty shards
+    (count 0 and the identities the scan writes for them); float partial sums
+    spread over 1e-3..1e16 so that only the rank-order fold reproduces them."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    recs = np.zeros(n, dtype=m.dist.AGG_RECORD)
+    for r in range(n):
+        empty = n > 2 and r in (1, n - 2)
+        if kind == "int":
+            lo, hi = sorted(int(x) for x in rng.integers(-2 ** 31, 2 ** 31 - 1, 2))
+            agg = dict(count=0, sum=0, min=2 ** 31 - 1, max=-2 ** 31) if empty else dict(
+                count=int(rng.integers(1, 1 << 40)), sum=int(rng.integers(-(1 << 60), 1 << 60)), min=lo, max=hi)
+        else:
+            lo, hi = sorted(float(np.float32(x)) for x in rng.normal(0, 1e6, 2))
+            agg = dict(count=0, sum=0.0, min=float("inf"), max=float("-inf")) if empty else dict(
+                count=int(rng.integers(1, 1 << 40)), sum=float(rng.choice([1e16, -1e16, 1.0, 3.3e-3, 7.77e8])
+                                                          * rng.random()), min=lo, max=hi)
+        recs[r] = m.dist.pack_aggregate(agg, kind == "int")[0]
+    return recs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["int", "float"])
+@pytest.mark.parametrize("n", [1, 2, 8])
+def test_device_fold_of_n_rank_records_is_exact(m, torch_cuda, kind, n):
+    """mbx_agg_fold_async -- the fold the aggregate exchange runs after its
+    RCCL all-gather -- over n gathered records (n = 8: the driver's 8-GPU
+    C5 combine, run here without RCCL), with empty shards: equal to
+    dist.fold_aggregates bit for bit, also folded in place."""
+    torch = torch_cuda
+    ctx = m.Context(0)
+    try:
+        recs = _records(m, kind, n, seed=10 * n + (kind == "int"))
+        want = m.dist.fold_aggregates(recs)
+        dev = torch.from_numpy(recs.view(np.int64).copy()).cuda()
+        out = torch.zeros(m.dist.AGG_WORDS, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        ctx.agg_fold_async(dev.data_ptr(), n, out.data_ptr())
+        ctx.agg_fold_async(dev.data_ptr(), n, dev.data_ptr())  # in place over record 0
+        ctx.sync()
+        for got_words in (out.cpu().numpy(), dev.cpu().numpy()[:m.dist.AGG_WORDS]):
+            got = m.dist.fold_aggregates(got_words)
+            assert got == want
+            if kind == "float":
+                assert np.float64(got["sum"]).tobytes() == np.float64(want["sum"]).tobytes()
+        with pytest.raises(m.MbxError):
+            ctx.agg_fold_async(dev.data_ptr(), 0, out.data_ptr())
+    finally:
+        ctx.close()
