@@ -115,7 +115,8 @@ public final class GpuTables {
     for (int c = 0; c < nc; c++) {
       t[c] = types[c].attrType;
       w[c] = t[c] == AttrType.attrString ? sizes[c] : 4;
-      ByteBuffer b = ByteBuffer.allocateDirect(Math.max(1, nrows * w[c])).order(ByteOrder.nativeOrder());
+      ByteBuffer b = ByteBuffer.allocateDirect(Math.max(1, columnBytes(name, c, nrows, w[c])))
+          .order(ByteOrder.nativeOrder());
       BitSet have = new BitSet(nrows);
       Scan s = hfs[c].openScan();
       RID rid = new RID();
@@ -126,9 +127,11 @@ public final class GpuTables {
           byte[] rec = tu.getTupleByteArray();
           if (t[c] == AttrType.attrString) {
             int len = ((rec[0] & 0xff) << 8) | (rec[1] & 0xff);
-            for (int k = 0; k < w[c]; k++) b.put(p * w[c] + k, k < len ? rec[2 + k] : 0);
+            // p * w[c] + k < nrows * w[c] <= Integer.MAX_VALUE (columnBytes)
+            final int at = (int) ((long) p * w[c]);
+            for (int k = 0; k < w[c]; k++) b.put(at + k, k < len ? rec[2 + k] : 0);
           } else {
-            b.putInt(p * 4, Convert.getIntValue(0, rec));
+            b.putInt((int) ((long) p * 4), Convert.getIntValue(0, rec));
           }
           have.set(p);
         }
@@ -144,6 +147,23 @@ public final class GpuTables {
     holes.andNot(present);
     deleted.or(holes);
     return Native.tableStage(GpuContext.ctx(), t, w, nrows, cols, deleted.toLongArray(), 0);
+  }
+
+  /**
+   * The bytes of one decoded column, computed in long: a direct ByteBuffer
+   * holds at most Integer.MAX_VALUE bytes (e.g. a char(16) column past
+   * 134,217,727 rows does not fit), so a larger column is refused with
+   * FileScanException instead of an int product that wraps (to a negative
+   * allocation or to offsets inside another row).  The DB-file path
+   * (Native.dbStage) has no such limit.
+   */
+  static int columnBytes(String name, int col, long nrows, int width) throws iterator.FileScanException {
+    final long bytes = nrows * (long) width;
+    if (bytes > Integer.MAX_VALUE)
+      throw new iterator.FileScanException(null, "GpuTables: column " + col + " of " + name + " needs " + bytes
+          + " bytes; a decoded column (a dirty frame is pinned) holds at most " + Integer.MAX_VALUE
+          + " -- unpin it so the DB file can be staged");
+    return (int) bytes;
   }
 
   /**

@@ -79,3 +79,21 @@ def test_fixture_is_current(table):
     for rec in fresh.values():
         rec["source"] = "R/" + rec["source"]
     assert json.loads(json.dumps(fresh)) == table
+
+
+def test_decoded_staging_sizes_are_long():
+    """GpuTables.stageDecoded (the fallback when a dirty frame is pinned)
+    sizes and indexes its direct ByteBuffers through long products: no int
+    `nrows * width` / `p * width` remains, and a column over
+    Integer.MAX_VALUE bytes is refused by columnBytes with
+    FileScanException (the JNI side's own check is
+    test_jni_harness.test_table_stage_refuses_a_column_past_2_gib)."""
+    src = javarefs.strip(open(os.path.join(JAVA, "columnar", "GpuTables.java")).read())
+    body = src[src.index("static long stageDecoded"):src.index("static int columnBytes")]
+    assert "columnBytes(name, c, nrows, w[c])" in body
+    import re
+    ints = re.findall(r"(?<!\(long\) )\b(?:nrows|p)\s*\*\s*(?:w\[c\]|4)\b", body)
+    assert not ints, ints
+    cb = src[src.index("static int columnBytes"):]
+    cb = cb[:cb.index("\n  }\n")]
+    assert "nrows * (long) width" in cb and "Integer.MAX_VALUE" in cb and "FileScanException" in cb

@@ -111,6 +111,20 @@ def test_argument_checks_map_to_the_reference_exceptions(jvm):
     assert e.value.cls == "chainexception/ChainException"
 
 
+def test_table_stage_refuses_a_column_past_2_gib(jvm):
+    """a char(16) column of 2^27 rows needs 2^31 bytes -- one past what a Java
+    direct ByteBuffer holds: the glue sizes it in jlong (no wrap to a small
+    or negative size) and refuses the short buffer with FileScanException,
+    before any device call"""
+    i = lambda v: (V, jvm.array("I", v))
+    buf = np.zeros(1 << 20, dtype=np.uint8)
+    for nrows in [(1 << 27), (1 << 27) + 1, (1 << 31) // 16 * 3]:
+        with pytest.raises(JavaException) as e:
+            jvm.call("tableStage", I64, J(0), i([oracle.STRING]), (V, jvm.array("S", [16])), J(nrows),
+                     (V, jvm.object_array([jvm.direct_buffer(buf)])), (V, None), J(0))
+        assert e.value.cls == "iterator/FileScanException" and "direct ByteBuffer" in e.value.msg
+
+
 def test_harness_flags_jni_misuse(jvm):
     """the checker itself: a borrowed array left unreleased and a call made
     with an exception pending are reported"""
