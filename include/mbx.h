@@ -176,7 +176,11 @@ int mbx_table_info(const mbx_table *t, int64_t *nrows, int64_t *row_offset, int3
  * <= 4 four-byte columns) gathers them from the group, so one row's values
  * share a line: fewer HBM lines for a sparse selection.  Results are
  * identical; scans keep reading the columns.  Costs ncols x 4 bytes x nrows
- * of HBM. */
+ * of HBM.  A group is a snapshot taken at this call: for a table over caller
+ * memory (mbx_table_wrap) whose columns the caller rewrites, drop the groups
+ * (ncols = 0, cols may be NULL) and group again after the rewrite -- until
+ * then gathers of grouped columns return the snapshot's values (and a HIP
+ * graph captured before a drop must not be replayed after it). */
 int mbx_table_group(mbx_ctx *ctx, mbx_table *t, const int32_t *cols, int32_t ncols);
 
 /* ---- predicates: PredEval.Eval over one tuple (R/iterator/PredEval.java:25-183),
@@ -295,6 +299,9 @@ int mbx_materialize_async(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *se
 int mbx_cursor_open(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *sel, const int32_t *proj,
                     int32_t nproj, mbx_cursor **out);
 int mbx_cursor_count(const mbx_cursor *c, int64_t *count);
+/* At most max_rows rows per call, fewer when max_rows rows of the projection
+ * (8 + its host widths per row) would exceed 64 MiB of batch buffer: *n <
+ * max_rows is not the end of the stream, *n == 0 is. */
 int mbx_cursor_next(mbx_cursor *c, int64_t max_rows, int64_t *host_ids, void *const *host_out,
                     int64_t *n);
 /* The same batch without a copy: *ids and cols[j] (an array of nproj

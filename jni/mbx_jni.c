@@ -718,8 +718,9 @@ static jobject column_array(JNIEnv *env, jint type, jshort size, const void *buf
       (*env)->SetObjectArrayElement(env, sa, (jsize)r, js);
       (*env)->DeleteLocalRef(env, js);
     }
+    const int have_tmp = tmp != NULL; /* read before free: a freed pointer's value is indeterminate */
     free(tmp);
-    col = sa && tmp && !(*env)->ExceptionCheck(env) ? sa : NULL;
+    col = sa && have_tmp && !(*env)->ExceptionCheck(env) ? sa : NULL;
     if (sa && sa != col) (*env)->DeleteLocalRef(env, sa);
     if (!col && !(*env)->ExceptionCheck(env)) throw_chain(env, kChain, "cursor rows: host allocation");
   }

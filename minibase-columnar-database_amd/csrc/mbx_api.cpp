@@ -96,6 +96,7 @@ static void tuning_from_env(MbxTuning& t) {
   if (((t.select_dbg & 3) | ((t.select_dbg >> 4) & 983)) & ~kDiagDbg) t.select_dbg = 0;  // A/B forms: -DMBX_DIAG
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
   t.cursor_prefetch = (int32_t)env_knob("MBX_CURSOR_PREFETCH", 1);
+  t.cnf_rounds = env_knob("MBX_CNF_ROUNDS", 1) == 2 ? 2 : 1;
   t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 1);
   t.scan_select_waves = (int32_t)env_knob("MBX_SCAN_SELECT_WAVES", 16);
   t.select_flag_stride = (int32_t)env_knob("MBX_SELECT_FLAG_STRIDE", kFlagStride);
@@ -313,6 +314,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "gather_fused")) t.gather_fused = v;
   else if (!strcmp(knob, "select_blocks")) t.select_blocks = v < 1 ? 1024 : (int32_t)v;
   else if (!strcmp(knob, "cursor_prefetch")) t.cursor_prefetch = v;
+  else if (!strcmp(knob, "cnf_rounds")) t.cnf_rounds = v == 2 ? 2 : 1;
   else if (!strcmp(knob, "scan_select_fused")) t.scan_select_fused = v;
   else if (!strcmp(knob, "scan_select_waves")) t.scan_select_waves = v == 4 ? 4 : 16;
   else if (!strcmp(knob, "select_flag_stride")) t.select_flag_stride = v == 1 ? 1 : kFlagStride;
@@ -432,9 +434,17 @@ extern "C" int mbx_table_free(mbx_table* t) {
 extern "C" int mbx_table_group(mbx_ctx* c, mbx_table* t, const int32_t* cols, int32_t ncols) {
   NOTNULL(c);
   NOTNULL(t);
+  if (c->capturing) return fail(MBX_E_INVALID, "table_group: inside a graph capture (it allocates)");
+  if (ncols == 0) {  // drop every group (a wrapped table's columns were rewritten: drop, then group again)
+    int rc = set_device(c);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));  // no launch in flight still reads a group
+    for (TGroup& g : t->groups) hipFree(g.dev);
+    t->groups.clear();
+    return MBX_OK;
+  }
   NOTNULL(cols);
   if (ncols < 2 || ncols > 4) return fail(MBX_E_INVALID, "table_group: %d columns (2..4)", ncols);
-  if (c->capturing) return fail(MBX_E_INVALID, "table_group: inside a graph capture (it allocates)");
   const uint32_t* src[4];
   for (int32_t k = 0; k < ncols; k++) {
     if (cols[k] < 0 || cols[k] >= (int32_t)t->cols.size())
@@ -1754,7 +1764,7 @@ extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const m
   }
   HIPCHK(launch_cnf_materialize(C, deleted ? deleted->words : nullptr, nwords, t->nrows, c->lookback,
                                 t->row_offset, dev_ids, pc, dev_out, nproj, dev_count, c->stream, stamps,
-                                c->tune.select_dbg >> 4));
+                                c->tune.select_dbg >> 4, INT64_MAX, c->tune.cnf_rounds));
   return MBX_OK;
 }
 
@@ -1884,6 +1894,10 @@ static int64_t align16(int64_t v) { return (v + 15) & ~int64_t(15); }
 
 // host / staging layout of an n-row batch: n positions, then each projected
 // column's n rows, every part 16-byte aligned; returns the batch's bytes
+// the largest cursor batch buffer (256 Ki rows of 16 x char(256)
+// would pin ~1 GiB per buffer)
+constexpr int64_t kCursorBatchBytes = int64_t(64) << 20;
+
 static int64_t batch_layout(const mbx_cursor* k, int64_t n, int64_t* off) {
   int64_t o = align16(n * (int64_t)sizeof(int64_t));
   for (size_t j = 0; j < k->outs.size(); j++) {
@@ -1943,6 +1957,14 @@ static int cursor_next_view(mbx_cursor* k, int64_t max_rows, const int64_t** ids
   NOTNULL(n);
   *n = 0;
   if (max_rows <= 0) return fail(MBX_E_INVALID, "cursor_next: max_rows %lld", (long long)max_rows);
+  {
+    // a batch's buffers (2 pinned + 1 device) are sized by bytes, not rows:
+    // at most kCursorBatchBytes each, however wide the projected row
+    int64_t row_bytes = (int64_t)sizeof(int64_t);
+    for (size_t j = 0; j < k->outs.size(); j++) row_bytes += host_width(k, j);
+    const int64_t cap = kCursorBatchBytes / row_bytes;
+    if (max_rows > cap) max_rows = cap > 0 ? cap : 1;
+  }
   if (int rc0 = cursor_resolve(k)) return rc0;
   const int64_t take = k->count - k->next < max_rows ? k->count - k->next : max_rows;
   if (take <= 0) return MBX_OK;  // end of stream: get_next() returns null
@@ -2097,7 +2119,7 @@ extern "C" int mbx_cnf_cursor_launch(mbx_ctx* c, const mbx_table* t, const mbx_b
   }
   e = launch_cnf_materialize(C, deleted ? deleted->words : nullptr, (t->nrows + 63) >> 6, t->nrows, c->lookback,
                              t->row_offset, k->ids, pc, k->outs.data(), nproj, k->dcount, c->stream, nullptr,
-                             c->tune.select_dbg >> 4, bound);
+                             c->tune.select_dbg >> 4, bound, c->tune.cnf_rounds);
   if (e != hipSuccess) {
     mbx_cursor_close(k);
     return fail(MBX_E_DEVICE, "cnf_cursor: %s", hipGetErrorString(e));

@@ -1,3 +1,4 @@
+#include <cstdio>
 // mbx_kernels.hip -- CDNA4 (gfx950) kernels of the columnar scan path.
 //
 //   k_scan_fast      PredEval over 4-byte columns (ColumnarFileScan.get_next,
@@ -1587,10 +1588,10 @@ __device__ __forceinline__ int64_t lookback_window(int64_t* __restrict__ lb, int
 
 // in0 / a0: the first window's flags (below blockIdx.x), loaded by the caller
 __device__ __forceinline__ int64_t chained_lookback(int64_t* __restrict__ lb, int64_t* __restrict__ inc,
-                                                    int64_t epoch, int lane, int64_t in0, int64_t a0) {
+                                                    int64_t epoch, int lane, int64_t in0, int64_t a0, int64_t bid) {
   constexpr int64_t kLow = 0xffffffffll;
   int64_t pre = 0;
-  int64_t e = blockIdx.x;
+  int64_t e = bid;
   bool first = true;
   while (e > 0) {
     const int64_t j = e - 64 + lane;
@@ -1622,19 +1623,35 @@ __device__ __forceinline__ int64_t chained_lookback(int64_t* __restrict__ lb, in
   return pre;
 }
 
-template <int G4, class GT, class WordAt, int NW = kWaves, int NR = kSelRegs>
+// the chained look-back's inclusive prefixes: lb[1 + kIncBase + segment]
+// (count flags below, one per segment, <= kIncBase segments)
+constexpr int64_t kIncBase = 8192;
+static_assert(1 + 2 * kIncBase <= kLookbackWords, "look-back buffer");
+struct NoAfter {
+  __device__ void operator()() const {}
+};
+
+// bid / nblk: the segment this call completes and the launch's segment count
+// (default: blockIdx.x / gridDim.x, one segment per block); after(): run by
+// every wave once its leading steps are staged and their values' loads are
+// issued, before the look-back (k_cnf_select's next round issues its operand
+// loads there)
+template <int G4, class GT, class WordAt, int NW = kWaves, int NR = kSelRegs, class After = NoAfter>
 __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c, bool cached, int64_t a0,
                                             int64_t a1, WordAt word_at, int lane, int wave, int64_t* __restrict__ lb,
                                             int64_t epoch, int64_t row_offset, int64_t* __restrict__ ids,
                                             int64_t* __restrict__ total, const GT& G, int64_t* __restrict__ stamps,
                                             int32_t dbg, int64_t* __restrict__ segc, int64_t nseg, int64_t* wcount,
                                             int64_t* wpre, uint16_t (*stage)[32 * 64],
-                                            uint64_t* __restrict__ words_out = nullptr, int32_t fs = 1) {
+                                            uint64_t* __restrict__ words_out = nullptr, int32_t fs = 1,
+                                            int64_t bid = -1, int64_t nblk = -1, After after = After{}) {
   // fs: int64 words between two blocks' count flags (1, or 16 = one 128-byte
   // line per flag for the polling form: the polls of every block do not queue
   // on the same few lines); the chained form needs 1
   dbg &= kDiagDbg;  // bits 0-2: A/B poll forms, -DMBX_DIAG builds only
-  int64_t* const inc = lb + 1 + kLookbackBlocks;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
+  int64_t* const inc = lb + 1 + kIncBase;  // chained form (dbg bit 3): epoch << 32 | inclusive prefix
+  const int64_t B = bid < 0 ? (int64_t)blockIdx.x : bid;
+  const int64_t NB = nblk < 0 ? (int64_t)gridDim.x : nblk;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
   if (lane == 0) wcount[wave] = c;
@@ -1672,7 +1689,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   int64_t* flag_at = nullptr;
   int64_t flag = 0;
   if (wave == kPub) {
-    flag_at = &lb[1 + (int64_t)blockIdx.x * fs];
+    flag_at = &lb[1 + B * fs];
     flag = (epoch << 32) | bc;
     asm volatile("" : "+v"(flag_at), "+v"(flag));
     // vmcnt(0) before the flag: free (nothing of this wave is in flight here
@@ -1685,7 +1702,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     }
   }
   if (dbg & 128) {  // diagnostic: the count only (wrong output by design)
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) lb[0] = epoch;
+    if (B == NB - 1 && threadIdx.x == 0) lb[0] = epoch;
     return;
   }
   // the wave's leading steps staged together, the first kPrefetch x 64
@@ -1717,22 +1734,23 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
       }
     }
   }
+  after();
   if (wave == kPub) {
   } else if (dbg & 8) {
     // chained form: wave 0 walks back over its predecessors, 64 per round,
     // stops at the nearest one whose inclusive prefix is published and adds
     // the counts after it, and publishes this block's inclusive prefix at
     // once; the other waves contribute 0
-    if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
+    if (stamps && threadIdx.x == 64) stamps[4 * B + 1] = wall_clock64();
     if (wave == 0) {
       int64_t in0 = 0, a0f = epoch << 32;
-      if (blockIdx.x > 0) a0f = lookback_window(lb, inc, blockIdx.x, epoch, lane, in0);
-      int64_t pre = chained_lookback(lb, inc, epoch, lane, in0, a0f);
+      if (B > 0) a0f = lookback_window(lb, inc, B, epoch, lane, in0);
+      int64_t pre = chained_lookback(lb, inc, epoch, lane, in0, a0f, B);
 #pragma unroll
       for (int m = 32; m >= 1; m >>= 1) pre += __shfl_xor(pre, m);
       if (lane == 0) {
         wpre[0] = pre;
-        __hip_atomic_store(&inc[blockIdx.x], (epoch << 32) | (pre + bc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&inc[B], (epoch << 32) | (pre + bc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else if (lane == 0) {
       wpre[wave] = 0;
@@ -1740,12 +1758,12 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   } else {
     // polling form: every predecessor's count, one per thread of the other
     // waves, all in flight together
-    if (stamps && threadIdx.x == 64) stamps[4 * blockIdx.x + 1] = wall_clock64();
+    if (stamps && threadIdx.x == 64) stamps[4 * B + 1] = wall_clock64();
     int64_t v[kPolls];
 #pragma unroll
     for (int k = 0; k < kPolls; ++k) {
       const int64_t j = (int64_t)k * kPollers + threadIdx.x;
-      if (j >= (int64_t)blockIdx.x)
+      if (j >= B)
         v[k] = epoch << 32;
       else if (dbg & 4)  // first round through L2 (a stale line only reads as "not yet"), then coherent polls
         v[k] = __builtin_nontemporal_load(&lb[1 + j * fs]);
@@ -1770,14 +1788,14 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
     if (lane == 0) wpre[wave] = pre;
   }
   __syncthreads();
-  if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x + 2] = wall_clock64();
+  if (stamps && threadIdx.x == 0) stamps[4 * B + 2] = wall_clock64();
   int64_t off = 0;
 #pragma unroll
   for (int k = 0; k < NW; ++k) off += wpre[k];
   // the last block: the total, and the epoch the next launch starts from
   // (every block has read it: the last block's offset needs every other
   // block's count)
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+  if (B == NB - 1 && threadIdx.x == 0) {
     *total = off + bc;
     lb[0] = epoch;
   }
@@ -1843,23 +1861,27 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // its offset -- i.e. every other block's count -- is known) set every
   // word they do not use back to epoch 0, which no launch has: by induction
   // no word holds the epoch of a launch before that launch writes it.
-  if (blockIdx.x == gridDim.x - 1 && epoch >= 0x7ffffffe) {
+  if (B == NB - 1 && epoch >= 0x7ffffffe) {
     for (int64_t w = 1 + threadIdx.x; w < kLookbackWords; w += 64 * NW) {
       const int64_t x = w - 1;
-      const bool live = (dbg & 8) ? (x < (int64_t)gridDim.x ||
-                                     (x >= kLookbackBlocks && x - kLookbackBlocks < (int64_t)gridDim.x))
-                                  : (x % fs == 0 && x / fs < (int64_t)gridDim.x);
+      const bool live = (dbg & 8) ? (x < NB || (x >= kIncBase && x - kIncBase < NB)) : (x % fs == 0 && x / fs < NB);
       if (!live) lb[w] = 0;
     }
   }
   if (stamps) {
     __syncthreads();
-    if (threadIdx.x == 0) stamps[4 * blockIdx.x + 3] = wall_clock64();
+    if (threadIdx.x == 0) stamps[4 * B + 3] = wall_clock64();
   }
   asm volatile("" ::"v"(flag_at), "v"(flag));  // the flag store's registers, live to here
 }
 
-template <int G4, int NB, class GT = Gather4>
+// R rounds (1 or 2): the launch covers gridDim.x x R segments of
+// words_per_block words, block b completing segment b, then b + gridDim.x;
+// the next round's operand words are loaded while this round's gathers are
+// in flight (the after() hook of select_tail), so from the second round on
+// the bitmap reads overlap the gathers instead of preceding them.  NR: the
+// registers holding a wave's words per round (64 words each).
+template <int G4, int NB, class GT = Gather4, int R = 1, int NR = kSelRegs>
 __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
                                                        int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
                                                        int64_t* __restrict__ lb, int64_t row_offset,
@@ -1883,58 +1905,82 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   // epochs 1 .. 2^31 - 1: epoch << 32 stays a positive int64
   const uint32_t prev = (uint32_t)lb[0];
   const int64_t epoch = prev >= 0x7fffffffu ? 1 : (int64_t)prev + 1;
-  const int64_t s0 = (int64_t)blockIdx.x * words_per_block;
-  const int64_t s1 = min(s0 + words_per_block, nwords);
-  const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
-  const int64_t a0 = min(s0 + wave * per, s1);
-  const int64_t a1 = min(a0 + per, s1);
-  const bool cached = a1 - a0 <= 64 * kSelRegs;
+  const int64_t nseg = (int64_t)gridDim.x * R;
+  auto range = [&](int64_t seg, int64_t& a0, int64_t& a1) {
+    const int64_t s0 = min(seg * words_per_block, nwords);
+    const int64_t s1 = min(s0 + words_per_block, nwords);
+    const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
+    a0 = min(s0 + wave * per, s1);
+    a1 = min(a0 + per, s1);
+  };
   auto word_at = [&](int64_t w) -> uint64_t {
     uint64_t r = cnf_word(C, w);
     if (del) r &= ~del[w];
     if (w == nwords - 1) r &= tail_mask;
     return r;
   };
-  uint64_t wr[kSelRegs];
-  int64_t c = 0;
-  if (NB > 0 && cached) {
-    // every operand word of the wave's range in flight at once (NB x 8
-    // register pairs: sized to the operand count)
-    uint64_t q[kSelRegs][NB > 0 ? NB : 1];
+  // every operand word of a wave's range in flight at once (NB x NR
+  // register pairs: sized to the operand count)
+  uint64_t q[NR][NB > 0 ? NB : 1];
+  auto load_ops = [&](int64_t a0, int64_t a1) {
 #pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
+    for (int r = 0; r < NR; ++r) {
       const int64_t w = a0 + r * 64 + lane;
 #pragma unroll
       for (int k = 0; k < NB; ++k) q[r][k] = w < a1 ? C.bms[k][w] : 0ull;
     }
+  };
+  int64_t a0, a1;
+  range(blockIdx.x, a0, a1);
+  if (NB > 0 && a1 - a0 <= 64 * NR) load_ops(a0, a1);
 #pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
-      const int64_t w = a0 + r * 64 + lane;
-      uint64_t x = ~0ull;
-      for (int cj = 0; cj < C.nconj; ++cj) {
-        uint64_t o = 0;
+  for (int round = 0; round < R; ++round) {
+    const int64_t seg = (int64_t)round * gridDim.x + blockIdx.x;
+    if (round > 0) range(seg, a0, a1);
+    const bool cached = a1 - a0 <= 64 * NR;
+    uint64_t wr[NR];
+    int64_t c = 0;
+    if (NB > 0 && cached) {
 #pragma unroll
-        for (int k = 0; k < NB; ++k)
-          if (k >= C.conj_off[cj] && k < C.conj_off[cj + 1]) o |= q[r][k];
-        x &= o;
+      for (int r = 0; r < NR; ++r) {
+        const int64_t w = a0 + r * 64 + lane;
+        uint64_t x = ~0ull;
+        for (int cj = 0; cj < C.nconj; ++cj) {
+          uint64_t o = 0;
+#pragma unroll
+          for (int k = 0; k < NB; ++k)
+            if (k >= C.conj_off[cj] && k < C.conj_off[cj + 1]) o |= q[r][k];
+          x &= o;
+        }
+        if (del && w < a1) x &= ~del[w];
+        if (w == nwords - 1) x &= tail_mask;
+        wr[r] = w < a1 ? x : 0ull;
+        c += __popcll(wr[r]);
       }
-      if (del && w < a1) x &= ~del[w];
-      if (w == nwords - 1) x &= tail_mask;
-      wr[r] = w < a1 ? x : 0ull;
-      c += __popcll(wr[r]);
-    }
-  } else if (cached) {
+    } else if (cached) {
 #pragma unroll
-    for (int r = 0; r < kSelRegs; ++r) {
-      const int64_t w = a0 + r * 64 + lane;
-      wr[r] = w < a1 ? word_at(w) : 0ull;
-      c += __popcll(wr[r]);
+      for (int r = 0; r < NR; ++r) {
+        const int64_t w = a0 + r * 64 + lane;
+        wr[r] = w < a1 ? word_at(w) : 0ull;
+        c += __popcll(wr[r]);
+      }
+    } else {
+      for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(word_at(w));
     }
-  } else {
-    for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(word_at(w));
+    // the next round's operand loads, issued behind this round's gathers
+    auto after = [&]() {
+      if (round + 1 < R && NB > 0) {
+        int64_t n0, n1;
+        range(seg + gridDim.x, n0, n1);
+        if (n1 - n0 <= 64 * NR) load_ops(n0, n1);
+      }
+    };
+    select_tail<G4, GT, decltype(word_at), kWaves, NR>(wr, c, cached, a0, a1, word_at, lane, wave, lb, epoch,
+                                                         row_offset, ids, total, G, R == 1 ? stamps : nullptr, dbg,
+                                                         nullptr, 0, wcount, wpre, stage, nullptr, 1, seg, nseg,
+                                                         after);
+    if (round + 1 < R) __syncthreads();  // LDS counts / stage reused by the next round
   }
-  select_tail<G4, GT>(wr, c, cached, a0, a1, word_at, lane, wave, lb, epoch, row_offset, ids, total, G, stamps, dbg,
-                      nullptr, 0, wcount, wpre, stage);
 }
 
 constexpr int kDefaultU = 2;
@@ -2465,7 +2511,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
-                                  int64_t* stamps, int32_t dbg, int64_t cap) {
+                                  int64_t* stamps, int32_t dbg, int64_t cap, int32_t rounds) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   if (nproj < 0 || nproj > kMaxProj) return hipErrorInvalidValue;
   // <= 4 four-byte columns: values prefetched in registers (Gather4); any
@@ -2495,11 +2541,39 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   // are 32-bit, so tables of >= 2^32 rows poll every predecessor, as does
   // select_dbg bit 7 (the A/B knob: MBX_SELECT_DBG=128)
   dbg = (dbg & ~8) | ((!(dbg & 8) && nbits < (int64_t(1) << 32)) ? 8 : 0);
+  // two rounds (tuning cnf_rounds = 2): the same blocks, segments of half
+  // the words, each block's second segment's operand loads in flight under
+  // its first segment's gathers; narrow projections of 1..4 operands with
+  // the chained look-back, and wave ranges within 4 x 64 words
+  // EXPERIMENT: block b completes segments b and b + grid, so round 2 waits
+  // on round-1 segments of every block: the grid must be resident at once
+  // (capped at the occupancy the runtime reports for the hungriest form)
+  static int resident = 0;
+  if (rounds == 2 && !resident) {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cnf_select<4, 4, Gather4, 2, 4>, kBlock, 0) ==
+            hipSuccess &&
+        hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      resident = per_cu * cus;
+    fprintf(stderr, "mbx: k_cnf_select two rounds: %d blocks per CU x %d CUs\n", per_cu, cus);
+  }
+  const int64_t gmax = resident < kLookbackBlocks ? resident : kLookbackBlocks;
+  const int64_t wpb2 = gmax > 0 ? (nwords + 2 * gmax - 1) / (2 * gmax) : 1;
+  const int64_t g2 = ((nwords + wpb2 - 1) / wpb2 + 1) / 2;
+  const bool two = rounds == 2 && gmax > 0 && g2 <= gmax && narrow && nbm >= 1 && nbm <= 4 && (dbg & 8) &&
+                   !stamps && (wpb2 + kWaves - 1) / kWaves <= 4 * 64;
   // the prefetch registers sized to the projection: <= 2 columns or <= 4
 #define MBX_CNF_SELECT(NB)                                                                                  \
   if (!narrow)                                                                                              \
     hipLaunchKernelGGL((k_cnf_select<kWide, NB, GatherW>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, \
                        nwords, tail_mask_of(nbits), wpb, lb, row_offset, ids, total, W, stamps, dbg);            \
+  else if (two && nproj <= 2)                                                                               \
+    hipLaunchKernelGGL((k_cnf_select<2, NB, Gather4, 2, 4>), dim3((unsigned)g2), dim3(kBlock), 0, s, c,     \
+                       deleted, nwords, tail_mask_of(nbits), wpb2, lb, row_offset, ids, total, G, stamps, dbg);  \
+  else if (two)                                                                                             \
+    hipLaunchKernelGGL((k_cnf_select<4, NB, Gather4, 2, 4>), dim3((unsigned)g2), dim3(kBlock), 0, s, c,     \
+                       deleted, nwords, tail_mask_of(nbits), wpb2, lb, row_offset, ids, total, G, stamps, dbg);  \
   else if (nproj <= 2)                                                                                      \
     hipLaunchKernelGGL((k_cnf_select<2, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
                        tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg);                    \

@@ -392,8 +392,10 @@ class Context:
 
     def group(self, table, cols):
         """mbx_table_group: a row-interleaved copy of 2..4 four-byte columns the
-        narrow gathers read (same results, fewer HBM lines when sparse)."""
-        arr = (ctypes.c_int32 * len(cols))(*cols)
+        narrow gathers read (same results, fewer HBM lines when sparse); cols = []: drop
+        the table's groups (a snapshot: rebuild after rewriting wrapped
+        columns)."""
+        arr = (ctypes.c_int32 * len(cols))(*cols) if cols else None
         _chk(lib().mbx_table_group(self.h, table.h, arr, len(cols)))
 
     def join(self, outer, outer_sel, inner, inner_sel, cnf, order, outer_block=0):

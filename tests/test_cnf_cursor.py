@@ -304,3 +304,32 @@ def test_cli_indexes_query_takes_the_one_launch_path():
     for g in GOLD["indexes_query"]:
         for r in g["rows"]:
             assert ", ".join(str(x) for x in r) in p.stdout
+
+
+def test_wide_rows_are_batched_by_bytes(m, ctx):
+    """a cursor batch is capped at 64 MiB of buffer whatever max_rows asks
+    (ADVICE r4): two char(256) columns are 8 + 2 x 256 bytes a row, so a
+    256 Ki-row request returns 129,055 rows per call; every row arrives once,
+    in position order, equal to the table's rows"""
+    n = 300_001
+    rng = np.random.default_rng(5)
+    s0 = rng.integers(ord("a"), ord("z") + 1, (n, 256), dtype=np.uint8)
+    s1 = rng.integers(ord("A"), ord("Z") + 1, (n, 256), dtype=np.uint8)
+    k = rng.integers(0, 3, n, dtype=np.int32)
+    cols = [(oracle.STRING, 256, s0), (oracle.STRING, 256, s1), (oracle.INTEGER, 4, k)]
+    t = ctx.stage(cols)
+    bms = ctx.index_build(t, 2, [("int", 0), ("int", 1)])
+    cur = ctx.cnf_cursor(t, [[bms[0], bms[1]]], [0, 1])
+    want = np.nonzero(k <= 1)[0]
+    cap = (64 << 20) // (8 + 256 + 256)
+    got_ids, got0, got1, sizes = [], [], [], []
+    while True:
+        ids, (a, b) = cur.next(262144)
+        if len(ids) == 0:
+            break
+        sizes.append(len(ids))
+        got_ids.append(ids), got0.append(a), got1.append(b)
+    assert sizes[:-1] == [cap] * (len(sizes) - 1) and 0 < sizes[-1] <= cap
+    assert np.array_equal(np.concatenate(got_ids), want)
+    assert np.array_equal(np.concatenate(got0), s0[want]) and np.array_equal(np.concatenate(got1), s1[want])
+    cur.close()

@@ -138,3 +138,41 @@ def test_group_errors(m, ctx):
     ctx.group(t, [0, 1])
     with pytest.raises(m.MbxError):
         ctx.group(t, [1, 2])     # column 1 is already grouped
+
+
+def test_group_of_wrapped_columns_is_a_snapshot_until_rebuilt(m, ctx):
+    """a table over caller memory (mbx_table_wrap): the group copies the
+    columns when it is built; after the caller rewrites a column, gathers
+    of the grouped columns return the snapshot until the groups are dropped
+    (cols = []) and built again"""
+    n = 200_003
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    c = [torch.randint(0, 10, (n,), dtype=torch.int32, device="cuda", generator=g) for _ in range(4)]
+    t = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [x.data_ptr() for x in c], n)
+    b2 = ctx.index_build(t, 2, [("int", 3)])[0]
+    b3 = ctx.index_build(t, 3, [("int", 7)])[0]
+    sel = (c[2] == 3) & (c[3] == 7)
+    k = int(sel.sum().item())
+
+    def rows():
+        o0 = torch.zeros(k + 1, dtype=torch.int32, device="cuda")
+        o1 = torch.zeros(k + 1, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        ctx.cnf_materialize_async(t, [[b2], [b3]], [0, 1], None, [o0.data_ptr(), o1.data_ptr()], cnt.data_ptr())
+        ctx.sync()
+        assert int(cnt.item()) == k
+        return o0[:k].clone(), o1[:k].clone()
+
+    ctx.group(t, [0, 1])
+    old0 = c[0][sel].clone()
+    assert bool((rows()[0] == old0).all())
+    c[0].add_(100)                      # the caller rewrites column 0 in place
+    torch.cuda.synchronize()
+    assert bool((rows()[0] == old0).all())          # the group's snapshot
+    ctx.group(t, [])                    # drop ...
+    assert bool((rows()[0] == c[0][sel]).all())     # ... the columns again
+    ctx.group(t, [0, 1])                # ... and rebuild
+    r0, r1 = rows()
+    assert bool((r0 == c[0][sel]).all()) and bool((r1 == c[1][sel]).all())

@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""C4 (ColumnarIndexScan: bm(c2=3) AND bm(c3=7) -> positions + c0, c1) in
+one k_cnf_select launch, per kernel form (tuning cnf_rounds 1 | 2), with and
+without the (c0, c1) column group: kernel time from a captured graph of 20
+launches (HIP events on the library stream), results checked against torch
+at several table sizes first.  One JSON line per (rows, form)."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", default="100000000")
+    ap.add_argument("--check-rows", default="1000,70001,1000003,10000000,33554431")
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    import mbx_pkg
+    m = mbx_pkg.load()
+    M = m.mbx
+    ctx = m.Context(0)
+    ext = torch.cuda.ExternalStream(ctx.stream)
+    torch.cuda.set_stream(ext)
+
+    def table(n, seed=42):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(seed)
+        c0 = torch.randint(0, 1 << 20, (n,), dtype=torch.int32, device="cuda", generator=g)
+        c1 = torch.randint(0, 1 << 20, (n,), dtype=torch.int32, device="cuda", generator=g)
+        c2 = torch.randint(0, 10, (n,), dtype=torch.int32, device="cuda", generator=g)
+        c3 = torch.randint(0, 10, (n,), dtype=torch.int32, device="cuda", generator=g)
+        t = ctx.wrap([(M.INTEGER, 4)] * 4, [x.data_ptr() for x in (c0, c1, c2, c3)], n, row_offset=64 * 3)
+        a = ctx.index_build(t, 2, [("int", 3)])[0]
+        b = ctx.index_build(t, 3, [("int", 7)])[0]
+        return (c0, c1, c2, c3), t, a, b
+
+    def run(n, rounds, group, timed):
+        cols, t, a, b = table(n)
+        if group:
+            ctx.group(t, [0, 1])
+        c0, c1, c2, c3 = cols
+        sel = (c2 == 3) & (c3 == 7)
+        want = int(sel.sum().item())
+        cap = max(64, want + 64)
+        ids = torch.zeros(cap, dtype=torch.int64, device="cuda")
+        o0 = torch.zeros(cap, dtype=torch.int32, device="cuda")
+        o1 = torch.zeros(cap, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        ctx.set_tuning("cnf_rounds", rounds)
+        f = lambda: ctx.cnf_materialize_async(t, [[a], [b]], [0, 1], ids.data_ptr(), [o0.data_ptr(), o1.data_ptr()],
+                                              cnt.data_ptr())
+        torch.cuda.synchronize()
+        f()
+        ctx.sync()
+        ok = (int(cnt.item()) == want and bool((ids[:want] == torch.nonzero(sel).flatten() + 192).all())
+              and bool((o0[:want] == c0[sel]).all()) and bool((o1[:want] == c1[sel]).all()))
+        res = {"rows": n, "rounds": rounds, "group": group, "selected": want, "ok": ok}
+        if timed:
+            ctx.graph_begin()
+            for _ in range(20):
+                f()
+            gr = ctx.graph_end()
+            gr.launch()
+            ctx.sync()
+            ms = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(ext)
+                gr.launch()
+                e1.record(ext)
+                ctx.sync()
+                ms.append(e0.elapsed_time(e1) / 20)
+            gr.close()
+            ok2 = int(cnt.item()) == want and bool((o0[:want] == c0[sel]).all())
+            res.update(us=sorted(ms)[len(ms) // 2] * 1e3, us_all=[round(x * 1e3, 2) for x in ms], ok_after=ok2)
+        ctx.set_tuning("cnf_rounds", 1)
+        del cols, t, a, b, ids, o0, o1, sel
+        torch.cuda.empty_cache()
+        return res
+
+    bad = 0
+    for n in map(int, args.check_rows.split(",")):
+        for rounds in (1, 2):
+            r = run(n, rounds, n % 2 == 0, False)
+            bad += not r["ok"]
+            print(json.dumps(r), flush=True)
+    for n in map(int, args.rows.split(",")):
+        for rep in range(2):
+            for group in (True, False):
+                for rounds in (1, 2):
+                    r = run(n, rounds, group, True)
+                    bad += not (r["ok"] and r["ok_after"])
+                    print(json.dumps(r), flush=True)
+    ctx.close()
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
