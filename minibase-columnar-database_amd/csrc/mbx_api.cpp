@@ -96,7 +96,6 @@ static void tuning_from_env(MbxTuning& t) {
   if (((t.select_dbg & 3) | ((t.select_dbg >> 4) & 983)) & ~kDiagDbg) t.select_dbg = 0;  // A/B forms: -DMBX_DIAG
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
   t.cursor_prefetch = (int32_t)env_knob("MBX_CURSOR_PREFETCH", 1);
-  t.cnf_rounds = env_knob("MBX_CNF_ROUNDS", 1) == 2 ? 2 : 1;
   t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 1);
   t.scan_select_waves = (int32_t)env_knob("MBX_SCAN_SELECT_WAVES", 16);
   t.select_flag_stride = (int32_t)env_knob("MBX_SELECT_FLAG_STRIDE", kFlagStride);
@@ -314,7 +313,6 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "gather_fused")) t.gather_fused = v;
   else if (!strcmp(knob, "select_blocks")) t.select_blocks = v < 1 ? 1024 : (int32_t)v;
   else if (!strcmp(knob, "cursor_prefetch")) t.cursor_prefetch = v;
-  else if (!strcmp(knob, "cnf_rounds")) t.cnf_rounds = v == 2 ? 2 : 1;
   else if (!strcmp(knob, "scan_select_fused")) t.scan_select_fused = v;
   else if (!strcmp(knob, "scan_select_waves")) t.scan_select_waves = v == 4 ? 4 : 16;
   else if (!strcmp(knob, "select_flag_stride")) t.select_flag_stride = v == 1 ? 1 : kFlagStride;
@@ -1764,7 +1762,7 @@ extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const m
   }
   HIPCHK(launch_cnf_materialize(C, deleted ? deleted->words : nullptr, nwords, t->nrows, c->lookback,
                                 t->row_offset, dev_ids, pc, dev_out, nproj, dev_count, c->stream, stamps,
-                                c->tune.select_dbg >> 4, INT64_MAX, c->tune.cnf_rounds));
+                                c->tune.select_dbg >> 4));
   return MBX_OK;
 }
 
@@ -2119,7 +2117,7 @@ extern "C" int mbx_cnf_cursor_launch(mbx_ctx* c, const mbx_table* t, const mbx_b
   }
   e = launch_cnf_materialize(C, deleted ? deleted->words : nullptr, (t->nrows + 63) >> 6, t->nrows, c->lookback,
                              t->row_offset, k->ids, pc, k->outs.data(), nproj, k->dcount, c->stream, nullptr,
-                             c->tune.select_dbg >> 4, bound, c->tune.cnf_rounds);
+                             c->tune.select_dbg >> 4, bound);
   if (e != hipSuccess) {
     mbx_cursor_close(k);
     return fail(MBX_E_DEVICE, "cnf_cursor: %s", hipGetErrorString(e));

@@ -1,4 +1,3 @@
-#include <cstdio>
 // mbx_kernels.hip -- CDNA4 (gfx950) kernels of the columnar scan path.
 //
 //   k_scan_fast      PredEval over 4-byte columns (ColumnarFileScan.get_next,
@@ -22,6 +21,8 @@
 //
 // No atomics on the data path: every reduction is per block into a partial
 // slot, then a single-block pass in a fixed order (bit-reproducible sums).
+#include <cstdlib>
+
 #include "mbx_internal.hpp"
 
 namespace mbx {
@@ -551,7 +552,38 @@ struct Gather4 {
   // words between rows of col[g]: 1 for a column, the group's width when the
   // column is read from a column group (its row's projected values share a line)
   int32_t stride[4] = {1, 1, 1, 1};
+  // two projected columns side by side in a group (C4's (c0, c1)): a row's
+  // values are one aligned 8-byte load (gather4_pairing)
+  int32_t pair = 0;
 };
+
+// the 8-byte pair form applies: 2 columns, adjacent words of one row of a
+// group (even stride, 8-byte aligned); MBX_GATHER_PAIR=0 keeps two 4-byte
+// loads per row (A/B)
+inline void gather4_pairing(Gather4& G) {
+  static const bool off = [] {
+    const char* e = getenv("MBX_GATHER_PAIR");
+    return e && atoi(e) == 0;
+  }();
+  G.pair = !off && G.n == 2 && G.col[1] == G.col[0] + 1 && G.stride[0] == G.stride[1] && G.stride[0] % 2 == 0 &&
+           ((uintptr_t)G.col[0] & 7) == 0;
+}
+
+// one row's projected values (every load issued before any is used)
+template <int G4>
+__device__ __forceinline__ void gather_row(const Gather4& G, int64_t p, uint32_t (&v)[G4 > 0 ? G4 : 1]) {
+  if constexpr (G4 >= 2) {
+    if (G.pair) {
+      const uint2 x = *reinterpret_cast<const uint2*>(G.col[0] + p * G.stride[0]);
+      v[0] = x.x;
+      v[1] = x.y;
+      return;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G4; ++g)
+    if (g < G.n) v[g] = (uint32_t)G.col[g][p * G.stride[g]];
+}
 
 // the narrow gather's source of a projected 4-byte column: its column group
 // when it has one, else the column
@@ -657,12 +689,8 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
         if (two) wide_row(G, p1, off + i1);
       } else {
         uint32_t v0[G4 > 0 ? G4 : 1], v1[G4 > 0 ? G4 : 1];
-#pragma unroll
-        for (int g = 0; g < G4; ++g)
-          if (g < G.n) {
-            v0[g] = (uint32_t)G.col[g][p0 * G.stride[g]];
-            v1[g] = (uint32_t)G.col[g][p1 * G.stride[g]];
-          }
+        gather_row<G4>(G, p0, v0);
+        gather_row<G4>(G, p1, v1);
         if (ids) {
           put(&ids[off + i0], row_offset + p0, wt);
           if (two) put(&ids[off + i1], row_offset + p1, wt);
@@ -691,9 +719,11 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
         if constexpr (G4 == kWide) {
           wide_row(G, p, o);
         } else {
+          uint32_t v[G4 > 0 ? G4 : 1];
+          gather_row<G4>(G, p, v);
 #pragma unroll
           for (int g = 0; g < G4; ++g)
-            if (g < G.n) put(&G.out[g][o], (uint32_t)G.col[g][p * G.stride[g]], wt);
+            if (g < G.n) put(&G.out[g][o], v[g], wt);
         }
       }
     }
@@ -1727,9 +1757,7 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
         const uint32_t i = (uint32_t)lane + 64u * k;
         if (i < tot) {
           const int64_t p = a0 * 64 + st[i];
-#pragma unroll
-          for (int g = 0; g < G4; ++g)
-            if (g < G.n) pv[k][g] = (uint32_t)G.col[g][p * G.stride[g]];
+          gather_row<G4>(G, p, pv[k]);
         }
       }
     }
@@ -1875,12 +1903,14 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   asm volatile("" ::"v"(flag_at), "v"(flag));  // the flag store's registers, live to here
 }
 
-// R rounds (1 or 2): the launch covers gridDim.x x R segments of
-// words_per_block words, block b completing segment b, then b + gridDim.x;
-// the next round's operand words are loaded while this round's gathers are
-// in flight (the after() hook of select_tail), so from the second round on
-// the bitmap reads overlap the gathers instead of preceding them.  NR: the
-// registers holding a wave's words per round (64 words each).
+// R rounds: the launch covers gridDim.x x R segments of words_per_block
+// words, block b completing segment b, then b + gridDim.x, the next round's
+// operand words loaded while this round's gathers are in flight (the after()
+// hook of select_tail); NR: the registers holding a wave's words per round.
+// Production launches R = 1 only: R = 2 measured slower at C4 (36.6 vs 31.8
+// us, profiles/r05/c: its extra registers cut residency from 4 to 3 blocks
+// per CU, and round 2 waits on every block's round 1, so the grid must be
+// resident at once -- DESIGN.md section 3).
 template <int G4, int NB, class GT = Gather4, int R = 1, int NR = kSelRegs>
 __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
                                                        int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
@@ -2487,6 +2517,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
       G.out[j] = (uint32_t*)out[j];
     }
     G.n = nproj;
+    gather4_pairing(G);
     hipLaunchKernelGGL(k_select_ids<4>, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, wpb, segc, S,
                        row_offset, ids, total, dbg, stamps, G);
     return hipGetLastError();
@@ -2511,7 +2542,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
-                                  int64_t* stamps, int32_t dbg, int64_t cap, int32_t rounds) {
+                                  int64_t* stamps, int32_t dbg, int64_t cap) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   if (nproj < 0 || nproj > kMaxProj) return hipErrorInvalidValue;
   // <= 4 four-byte columns: values prefetched in registers (Gather4); any
@@ -2531,6 +2562,7 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
     W.sw[j] = proj[j].stride_w;
   }
   G.n = narrow ? nproj : 0;
+  gather4_pairing(G);
   W.n = nproj;
   G.cap = W.cap = cap;
   // <= kLookbackBlocks blocks: one poll load per thread per 256 predecessors
@@ -2541,39 +2573,11 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   // are 32-bit, so tables of >= 2^32 rows poll every predecessor, as does
   // select_dbg bit 7 (the A/B knob: MBX_SELECT_DBG=128)
   dbg = (dbg & ~8) | ((!(dbg & 8) && nbits < (int64_t(1) << 32)) ? 8 : 0);
-  // two rounds (tuning cnf_rounds = 2): the same blocks, segments of half
-  // the words, each block's second segment's operand loads in flight under
-  // its first segment's gathers; narrow projections of 1..4 operands with
-  // the chained look-back, and wave ranges within 4 x 64 words
-  // EXPERIMENT: block b completes segments b and b + grid, so round 2 waits
-  // on round-1 segments of every block: the grid must be resident at once
-  // (capped at the occupancy the runtime reports for the hungriest form)
-  static int resident = 0;
-  if (rounds == 2 && !resident) {
-    int per_cu = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_cnf_select<4, 4, Gather4, 2, 4>, kBlock, 0) ==
-            hipSuccess &&
-        hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      resident = per_cu * cus;
-    fprintf(stderr, "mbx: k_cnf_select two rounds: %d blocks per CU x %d CUs\n", per_cu, cus);
-  }
-  const int64_t gmax = resident < kLookbackBlocks ? resident : kLookbackBlocks;
-  const int64_t wpb2 = gmax > 0 ? (nwords + 2 * gmax - 1) / (2 * gmax) : 1;
-  const int64_t g2 = ((nwords + wpb2 - 1) / wpb2 + 1) / 2;
-  const bool two = rounds == 2 && gmax > 0 && g2 <= gmax && narrow && nbm >= 1 && nbm <= 4 && (dbg & 8) &&
-                   !stamps && (wpb2 + kWaves - 1) / kWaves <= 4 * 64;
   // the prefetch registers sized to the projection: <= 2 columns or <= 4
 #define MBX_CNF_SELECT(NB)                                                                                  \
   if (!narrow)                                                                                              \
     hipLaunchKernelGGL((k_cnf_select<kWide, NB, GatherW>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, \
                        nwords, tail_mask_of(nbits), wpb, lb, row_offset, ids, total, W, stamps, dbg);            \
-  else if (two && nproj <= 2)                                                                               \
-    hipLaunchKernelGGL((k_cnf_select<2, NB, Gather4, 2, 4>), dim3((unsigned)g2), dim3(kBlock), 0, s, c,     \
-                       deleted, nwords, tail_mask_of(nbits), wpb2, lb, row_offset, ids, total, G, stamps, dbg);  \
-  else if (two)                                                                                             \
-    hipLaunchKernelGGL((k_cnf_select<4, NB, Gather4, 2, 4>), dim3((unsigned)g2), dim3(kBlock), 0, s, c,     \
-                       deleted, nwords, tail_mask_of(nbits), wpb2, lb, row_offset, ids, total, G, stamps, dbg);  \
   else if (nproj <= 2)                                                                                      \
     hipLaunchKernelGGL((k_cnf_select<2, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
                        tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg);                    \

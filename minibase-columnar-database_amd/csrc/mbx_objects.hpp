@@ -56,7 +56,6 @@ struct MbxTuning {
   int32_t gather_fused = 1;       // MBX_GATHER_FUSED: 0 = compaction, then k_gather (two launches)
   int32_t select_blocks = 1024;   // MBX_SELECT_BLOCKS: compaction blocks at most (segments per block = nseg / this)
   int32_t cursor_prefetch = 1;    // MBX_CURSOR_PREFETCH: 0 = mbx_cursor_next copies each batch on demand
-  int32_t cnf_rounds = 1;         // MBX_CNF_ROUNDS: 2 = k_cnf_select's segments in two rounds per block
   int32_t scan_select_fused = 1;  // MBX_SCAN_SELECT_FUSED: 1 = BitSet + positions in one launch (k_scan_select)
   int32_t scan_select_waves = 16; // MBX_SCAN_SELECT_WAVES: waves per k_scan_select block (4 or 16)
   int32_t select_flag_stride = 16; // MBX_SELECT_FLAG_STRIDE: 16 = k_scan_select's polled flags one per line, or 1

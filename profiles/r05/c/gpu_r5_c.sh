@@ -1,0 +1,16 @@
+# Round 5 (c): C4 two-round k_cnf_select (grid capped at resident blocks),
+# then the cursor / group / comm tests (incl. this round's new ones) in both
+# k_cnf_select forms.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-r5_c}
+mkdir -p $OUT
+timeout -k 10 150 python3 -u tools/c4_forms.py > $OUT/c4_forms.jsonl 2> $OUT/c4_forms.err || { echo C4_FAIL; tail -5 $OUT/c4_forms.err; cat $OUT/c4_forms.jsonl; exit 1; }
+cat $OUT/c4_forms.jsonl
+grep -h "two rounds" $OUT/c4_forms.err || true
+timeout -k 10 600 python -u -m pytest tests/test_cnf_cursor.py tests/test_cnf_materialize.py tests/test_column_group.py tests/test_comm.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest_r1.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest_r1.log; exit 1; }
+tail -1 $OUT/pytest_r1.log
+MBX_CNF_ROUNDS=2 timeout -k 10 600 python -u -m pytest tests/test_cnf_cursor.py tests/test_cnf_materialize.py tests/test_column_group.py tests/test_shards.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest_rounds2.log 2>&1 || { echo PYTEST2_FAIL; tail -40 $OUT/pytest_rounds2.log; exit 1; }
+tail -1 $OUT/pytest_rounds2.log
+echo R5_C_OK

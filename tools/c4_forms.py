@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """C4 (ColumnarIndexScan: bm(c2=3) AND bm(c3=7) -> positions + c0, c1) in
-one k_cnf_select launch, per kernel form (tuning cnf_rounds 1 | 2), with and
-without the (c0, c1) column group: kernel time from a captured graph of 20
-launches (HIP events on the library stream), results checked against torch
-at several table sizes first.  One JSON line per (rows, form)."""
+one k_cnf_select launch, with and without the (c0, c1) column group: kernel
+time from a captured graph of 20 launches (HIP events on the library stream),
+results checked against torch at several table sizes first.  One JSON line
+per (rows, layout); the process's kernel form is set by the environment
+(MBX_GATHER_PAIR=0: two 4-byte loads per grouped row instead of one 8-byte).
+Round 5 also A/B'd a two-rounds-per-block form here (profiles/r05/c)."""
 import argparse
 import json
 import os
@@ -39,7 +41,7 @@ def main():
         b = ctx.index_build(t, 3, [("int", 7)])[0]
         return (c0, c1, c2, c3), t, a, b
 
-    def run(n, rounds, group, timed):
+    def run(n, group, timed):
         cols, t, a, b = table(n)
         if group:
             ctx.group(t, [0, 1])
@@ -51,7 +53,6 @@ def main():
         o0 = torch.zeros(cap, dtype=torch.int32, device="cuda")
         o1 = torch.zeros(cap, dtype=torch.int32, device="cuda")
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
-        ctx.set_tuning("cnf_rounds", rounds)
         f = lambda: ctx.cnf_materialize_async(t, [[a], [b]], [0, 1], ids.data_ptr(), [o0.data_ptr(), o1.data_ptr()],
                                               cnt.data_ptr())
         torch.cuda.synchronize()
@@ -59,7 +60,8 @@ def main():
         ctx.sync()
         ok = (int(cnt.item()) == want and bool((ids[:want] == torch.nonzero(sel).flatten() + 192).all())
               and bool((o0[:want] == c0[sel]).all()) and bool((o1[:want] == c1[sel]).all()))
-        res = {"rows": n, "rounds": rounds, "group": group, "selected": want, "ok": ok}
+        res = {"rows": n, "group": group, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"), "selected": want,
+               "ok": ok}
         if timed:
             ctx.graph_begin()
             for _ in range(20):
@@ -78,24 +80,22 @@ def main():
             gr.close()
             ok2 = int(cnt.item()) == want and bool((o0[:want] == c0[sel]).all())
             res.update(us=sorted(ms)[len(ms) // 2] * 1e3, us_all=[round(x * 1e3, 2) for x in ms], ok_after=ok2)
-        ctx.set_tuning("cnf_rounds", 1)
         del cols, t, a, b, ids, o0, o1, sel
         torch.cuda.empty_cache()
         return res
 
     bad = 0
     for n in map(int, args.check_rows.split(",")):
-        for rounds in (1, 2):
-            r = run(n, rounds, n % 2 == 0, False)
+        for group in (True, False):
+            r = run(n, group, False)
             bad += not r["ok"]
             print(json.dumps(r), flush=True)
     for n in map(int, args.rows.split(",")):
         for rep in range(2):
             for group in (True, False):
-                for rounds in (1, 2):
-                    r = run(n, rounds, group, True)
-                    bad += not (r["ok"] and r["ok_after"])
-                    print(json.dumps(r), flush=True)
+                r = run(n, group, True)
+                bad += not (r["ok"] and r["ok_after"])
+                print(json.dumps(r), flush=True)
     ctx.close()
     sys.exit(1 if bad else 0)
 
