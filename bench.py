@@ -83,7 +83,7 @@ PRECHECK_EXIT = 3
 # the keys every config record carries (tests/test_bench_launch.py)
 CONFIG_KEYS = ("workload", "rows", "rows_per_gpu", "gpus", "selected", "ms_per_query", "rows_per_s", "kernel",
                "kernel_ms", "kernel_ms_max_over_ranks", "algorithmic_bytes_per_launch", "achieved_gbs", "frac",
-               "exchange", "pre_check", "timing")
+               "exchange", "pre_check", "timing", "traffic")
 
 
 def cpu_baseline(rows, min_seconds):
@@ -135,6 +135,18 @@ def load_traffic(rows, count_mode):
         e = d.get("shards", {}).get(f"{rows}:{count_mode}")
         return (e or {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
+        return None
+
+
+def load_config_traffic(name, rows_per_gpu):
+    """HBM bytes per launch of a config record's kernel at this shard size
+    (rocprofv3 PMC, profiles/config_pmc.json from tools/config_pmc.py), or
+    None when that size was not profiled."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "config_pmc.json")) as f:
+            e = json.load(f)["configs"].get(f"{name}:{rows_per_gpu}")
+        return (e or {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError, KeyError):
         return None
 
 
@@ -243,11 +255,15 @@ def config_record(workload, rows, rows_per_gpu, gpus, selected, ms_per_query, ke
     dominant kernel's time from graph replay and its fraction of 8 TB/s over
     SURVEY 8(d)'s algorithmic bytes of rank 0's launch."""
     gbs = algo_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    traffic = load_config_traffic(workload.split(":")[0], rows_per_gpu)
     rec = {"workload": workload, "rows": rows, "rows_per_gpu": rows_per_gpu, "gpus": gpus, "selected": selected,
            "ms_per_query": ms_per_query, "rows_per_s": rows / (ms_per_query * 1e-3) if ms_per_query > 0 else 0.0,
            "kernel": kernel, "kernel_ms": kernel_ms, "kernel_ms_max_over_ranks": kernel_ms_max,
            "algorithmic_bytes_per_launch": algo_bytes, "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
-           "exchange": exchange, "pre_check": pre_check, "timing": timing}
+           "exchange": exchange, "pre_check": pre_check, "timing": timing,
+           "traffic": traffic, "traffic_over_algorithmic": traffic / algo_bytes if traffic and algo_bytes else None,
+           "traffic_unit": "HBM bytes per launch of rank 0's kernel at this shard size (rocprofv3 PMC, "
+                           "profiles/config_pmc.json)"}
     rec.update(extra)
     return rec
 
@@ -260,7 +276,7 @@ def make_parser():
     ap.add_argument("--rows", type=int, default=100_000_000,
                     help="global rows (strong scaling) or rows per GPU (weak)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="weak")
-    ap.add_argument("--graph-steps", type=int, default=10, help="steps per captured HIP graph (0: eager launches)")
+    ap.add_argument("--graph-steps", type=int, default=20, help="steps per captured HIP graph (0: eager launches)")
     ap.add_argument("--kernel-graph", type=int, default=20, help="launches per graph timed for kernel_ms")
     ap.add_argument("--exchange-bucket", type=int, default=1,
                     help="steps whose COUNTs share one all-reduce (1, the default: one collective per query)")

@@ -100,6 +100,13 @@ def test_default_run_adds_every_config_record():
     assert set(b.CONFIG_KEYS) <= set(rec)
     assert abs(rec["achieved_gbs"] - 1100.0) < 1e-6 and abs(rec["frac"] - 1100.0 / 8000.0) < 1e-12
     assert abs(rec["rows_per_s"] - 100_000_000 / 40e-6) < 1
+    # PMC traffic of the profiled shard sizes (profiles/config_pmc.json)
+    assert rec["traffic"] is None
+    for name, rows in (("C2", 10_000_000), ("C4", 100_000_000), ("C5", 125_000_000)):
+        t = b.load_config_traffic(name, rows)
+        assert t and t > 0, name
+        r = b.config_record(f"{name}: x", rows, rows, 1, 1, 1.0, "k", 0.5, 0.5, 1000, "none", "ok", "g")
+        assert r["traffic"] == t and r["traffic_over_algorithmic"] == t / 1000
 
 
 def _frame(count, arrivals, nan=0, slots=32):
