@@ -295,6 +295,25 @@ def make_parser():
     return ap
 
 
+def agree(torch, dist, world, rank, reason):
+    """A collective verdict: every rank learns whether any rank's check
+    failed (reason not None); then each failing rank prints its one-line
+    reason, the others a line naming the cause, and ALL exit PRECHECK_EXIT --
+    no rank is left waiting in a later collective."""
+    bad = int(reason is not None)
+    if world > 1:
+        t = torch.tensor([bad], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        anybad = int(t[0])
+    else:
+        anybad = bad
+    if anybad:
+        print(f"bench: pre-check failed on rank {rank}: {reason}" if reason else
+              f"bench: rank {rank} stops: another rank's pre-check failed", file=sys.stderr, flush=True)
+        sys.stderr.flush()
+        os._exit(PRECHECK_EXIT)
+
+
 # ---------------------------------------------------------------- GPU side
 
 class Harness:
@@ -329,20 +348,7 @@ class Harness:
         return int(t[0])
 
     def agree(self, reason):
-        """Every rank learns whether any rank's check failed; then each
-        failing rank prints its one-line reason and all exit non-zero."""
-        bad = int(reason is not None)
-        if self.world > 1:
-            t = self.torch.tensor([bad], dtype=self.torch.int32)
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-            anybad = int(t[0])
-        else:
-            anybad = bad
-        if anybad:
-            print(f"bench: pre-check failed on rank {self.rank}: {reason}" if reason else
-                  f"bench: rank {self.rank} stops: another rank's pre-check failed", file=sys.stderr, flush=True)
-            sys.stderr.flush()
-            os._exit(PRECHECK_EXIT)
+        agree(self.torch, self.dist, self.world, self.rank, reason)
 
     def graphs(self, enqueue, k0, k1, per):
         """HIP graphs of `per` steps each covering steps k0..k1-1 (None when

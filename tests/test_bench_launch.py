@@ -152,3 +152,51 @@ def test_aggregate_check_tolerances():
     assert "sum" in b.check_aggregate("C5", dict(want, sum=1.0e6 * (1 + 2e-6)), want)
     assert "count" in b.check_aggregate("C5", dict(want, count=11), want)
     assert "min" in b.check_aggregate("C5", dict(want, min=0.2500001), want)
+
+
+AGREE = """
+import os, sys
+sys.path.insert(0, {root!r})
+import torch, torch.distributed as dist
+import bench
+dist.init_process_group("gloo")
+rank, world = dist.get_rank(), dist.get_world_size()
+bad = os.environ.get("BAD_RANK")
+bench.agree(torch, dist, world, rank, "C3 pre-check: frame arrivals [2047] != 2046" if bad == str(rank) else None)
+print("passed", rank, flush=True)
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("bad_rank", [None, "0", "1"])
+def test_precheck_verdict_is_collective(bad_rank):
+    """gloo world 2 (the bench's host-side group): a pre-check failure on ANY
+    rank makes every rank exit 3 before timing -- the failing rank with its
+    one-line reason, the other naming the cause -- and no failure lets both
+    go on"""
+    port = free_port_local()
+    procs = []
+    for r in range(2):
+        env = {k: v for k, v in os.environ.items() if k not in ("BAD_RANK",)}
+        env.update(RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if bad_rank is not None:
+            env["BAD_RANK"] = bad_rank
+        procs.append(subprocess.Popen([sys.executable, "-c", AGREE.format(root=ROOT)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=120) for p in procs]
+    for r, (p, (out, err)) in enumerate(zip(procs, outs)):
+        if bad_rank is None:
+            assert p.returncode == 0 and f"passed {r}" in out, err
+        else:
+            assert p.returncode == 3 and "passed" not in out, (r, err)
+            if str(r) == bad_rank:
+                assert f"pre-check failed on rank {r}: C3 pre-check: frame arrivals" in err
+            else:
+                assert "another rank's pre-check failed" in err
+
+
+def free_port_local():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
