@@ -1916,7 +1916,10 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
                                                        int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
                                                        int64_t* __restrict__ lb, int64_t row_offset,
                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                       GT G, int64_t* __restrict__ stamps, int32_t dbg) {
+                                                       GT G, int64_t* __restrict__ stamps, int32_t dbg,
+                                                       int32_t fs) {
+  // fs: int64 words between two blocks' count flags (the polling form: 16 =
+  // one 128-byte line per flag, or 1; the chained form: 1)
   // dbg bit 3: the chained look-back -- each block also publishes its
   // inclusive prefix, and wave 0 walks back 64 predecessors per round to the
   // nearest published one (~4 flag lines per block instead of every
@@ -2007,7 +2010,7 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
     };
     select_tail<G4, GT, decltype(word_at), kWaves, NR>(wr, c, cached, a0, a1, word_at, lane, wave, lb, epoch,
                                                          row_offset, ids, total, G, R == 1 ? stamps : nullptr, dbg,
-                                                         nullptr, 0, wcount, wpre, stage, nullptr, 1, seg, nseg,
+                                                         nullptr, 0, wcount, wpre, stage, nullptr, fs, seg, nseg,
                                                          after);
     if (round + 1 < R) __syncthreads();  // LDS counts / stage reused by the next round
   }
@@ -2542,7 +2545,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
-                                  int64_t* stamps, int32_t dbg, int64_t cap) {
+                                  int64_t* stamps, int32_t dbg, int64_t cap, int32_t blocks, int32_t flag_stride) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   if (nproj < 0 || nproj > kMaxProj) return hipErrorInvalidValue;
   // <= 4 four-byte columns: values prefetched in registers (Gather4); any
@@ -2565,25 +2568,32 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   gather4_pairing(G);
   W.n = nproj;
   G.cap = W.cap = cap;
-  // <= kLookbackBlocks blocks: one poll load per thread per 256 predecessors
-  const int64_t wpb = (nwords + kLookbackBlocks - 1) / kLookbackBlocks;
-  const int64_t g = (nwords + wpb - 1) / wpb;
-  const int nbm = c.conj_off[c.nconj];
   // kernel dbg bit 3 = the chained look-back (default): inclusive prefixes
   // are 32-bit, so tables of >= 2^32 rows poll every predecessor, as does
   // select_dbg bit 7 (the A/B knob: MBX_SELECT_DBG=128)
   dbg = (dbg & ~8) | ((!(dbg & 8) && nbits < (int64_t(1) << 32)) ? 8 : 0);
+  // <= kLookbackBlocks blocks for the polling form (one poll load per thread
+  // per 256 predecessors); the chained form takes up to kIncBase (tuning
+  // cnf_blocks: more blocks than the chip holds at once, so the later ones'
+  // operand loads run beside the earlier ones' gathers)
+  const int64_t want = blocks > 0 ? ((dbg & 8) ? (blocks < kIncBase ? blocks : kIncBase)
+                                                : (blocks < kLookbackBlocks ? blocks : kLookbackBlocks))
+                                   : kLookbackBlocks;
+  const int32_t fs = (dbg & 8) || flag_stride != kFlagStride ? 1 : kFlagStride;
+  const int64_t wpb = (nwords + want - 1) / want;
+  const int64_t g = (nwords + wpb - 1) / wpb;
+  const int nbm = c.conj_off[c.nconj];
   // the prefetch registers sized to the projection: <= 2 columns or <= 4
 #define MBX_CNF_SELECT(NB)                                                                                  \
   if (!narrow)                                                                                              \
     hipLaunchKernelGGL((k_cnf_select<kWide, NB, GatherW>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, \
-                       nwords, tail_mask_of(nbits), wpb, lb, row_offset, ids, total, W, stamps, dbg);            \
+                       nwords, tail_mask_of(nbits), wpb, lb, row_offset, ids, total, W, stamps, dbg, fs);            \
   else if (nproj <= 2)                                                                                      \
     hipLaunchKernelGGL((k_cnf_select<2, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
-                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg);                    \
+                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg, fs);                    \
   else                                                                                                      \
     hipLaunchKernelGGL((k_cnf_select<4, NB>), dim3((unsigned)g), dim3(kBlock), 0, s, c, deleted, nwords,    \
-                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg)
+                       tail_mask_of(nbits), wpb, lb, row_offset, ids, total, G, stamps, dbg, fs)
   switch (nbm) {
     case 1: MBX_CNF_SELECT(1); break;
     case 2: MBX_CNF_SELECT(2); break;

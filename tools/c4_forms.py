@@ -20,6 +20,9 @@ def main():
     ap.add_argument("--rows", default="100000000")
     ap.add_argument("--check-rows", default="1000,70001,1000003,10000000,33554431")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--blocks", default="0", help="comma list of tuning cnf_blocks values (0: the default grid)")
+    ap.add_argument("--lookback", default="default",
+                    help="comma list: default | chained | poll16 | poll1 (k_cnf_select's look-back form)")
     args = ap.parse_args()
     import torch
     import mbx_pkg
@@ -41,7 +44,9 @@ def main():
         b = ctx.index_build(t, 3, [("int", 7)])[0]
         return (c0, c1, c2, c3), t, a, b
 
-    def run(n, group, timed):
+    LB = {"default": None, "chained": (0, 1), "poll16": (128, 16), "poll1": (128, 1)}
+
+    def run(n, group, timed, blocks=0, lookback="default"):
         cols, t, a, b = table(n)
         if group:
             ctx.group(t, [0, 1])
@@ -53,6 +58,10 @@ def main():
         o0 = torch.zeros(cap, dtype=torch.int32, device="cuda")
         o1 = torch.zeros(cap, dtype=torch.int32, device="cuda")
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        ctx.set_tuning("cnf_blocks", blocks)
+        if LB[lookback]:
+            ctx.set_tuning("select_dbg", LB[lookback][0])
+            ctx.set_tuning("cnf_flag_stride", LB[lookback][1])
         f = lambda: ctx.cnf_materialize_async(t, [[a], [b]], [0, 1], ids.data_ptr(), [o0.data_ptr(), o1.data_ptr()],
                                               cnt.data_ptr())
         torch.cuda.synchronize()
@@ -60,8 +69,8 @@ def main():
         ctx.sync()
         ok = (int(cnt.item()) == want and bool((ids[:want] == torch.nonzero(sel).flatten() + 192).all())
               and bool((o0[:want] == c0[sel]).all()) and bool((o1[:want] == c1[sel]).all()))
-        res = {"rows": n, "group": group, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"), "selected": want,
-               "ok": ok}
+        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
+               "selected": want, "ok": ok}
         if timed:
             ctx.graph_begin()
             for _ in range(20):
@@ -80,22 +89,29 @@ def main():
             gr.close()
             ok2 = int(cnt.item()) == want and bool((o0[:want] == c0[sel]).all())
             res.update(us=sorted(ms)[len(ms) // 2] * 1e3, us_all=[round(x * 1e3, 2) for x in ms], ok_after=ok2)
+        ctx.set_tuning("reset")
         del cols, t, a, b, ids, o0, o1, sel
         torch.cuda.empty_cache()
         return res
 
     bad = 0
+    blocks = [int(x) for x in args.blocks.split(",")]
+    lbs = args.lookback.split(",")
     for n in map(int, args.check_rows.split(",")):
         for group in (True, False):
-            r = run(n, group, False)
-            bad += not r["ok"]
-            print(json.dumps(r), flush=True)
+            for b in blocks:
+                for lb in lbs:
+                    r = run(n, group, False, b, lb)
+                    bad += not r["ok"]
+                    print(json.dumps(r), flush=True)
     for n in map(int, args.rows.split(",")):
         for rep in range(2):
             for group in (True, False):
-                r = run(n, group, True)
-                bad += not (r["ok"] and r["ok_after"])
-                print(json.dumps(r), flush=True)
+                for b in blocks:
+                    for lb in lbs:
+                        r = run(n, group, True, b, lb)
+                        bad += not (r["ok"] and r["ok_after"])
+                        print(json.dumps(r), flush=True)
     ctx.close()
     sys.exit(1 if bad else 0)
 
