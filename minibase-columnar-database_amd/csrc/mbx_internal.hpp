@@ -339,7 +339,8 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
                                   int64_t* stamps = nullptr, int32_t dbg = 0,
-                                  int64_t cap = INT64_MAX, int32_t blocks = 0, int32_t flag_stride = 1);
+                                  int64_t cap = INT64_MAX, int32_t blocks = 0, int32_t flag_stride = 1,
+                                  int32_t lookback = 0);
 // epoch, per-block counts, per-block inclusive prefixes; the polling form's
 // counts may sit one per 128-byte line (kFlagStride words apart)
 constexpr int32_t kFlagStride = 16;

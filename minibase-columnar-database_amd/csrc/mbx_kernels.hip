@@ -2545,7 +2545,8 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
-                                  int64_t* stamps, int32_t dbg, int64_t cap, int32_t blocks, int32_t flag_stride) {
+                                  int64_t* stamps, int32_t dbg, int64_t cap, int32_t blocks, int32_t flag_stride,
+                                  int32_t lookback) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   if (nproj < 0 || nproj > kMaxProj) return hipErrorInvalidValue;
   // <= 4 four-byte columns: values prefetched in registers (Gather4); any
@@ -2568,10 +2569,23 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   gather4_pairing(G);
   W.n = nproj;
   G.cap = W.cap = cap;
-  // kernel dbg bit 3 = the chained look-back (default): inclusive prefixes
-  // are 32-bit, so tables of >= 2^32 rows poll every predecessor, as does
-  // select_dbg bit 7 (the A/B knob: MBX_SELECT_DBG=128)
-  dbg = (dbg & ~8) | ((!(dbg & 8) && nbits < (int64_t(1) << 32)) ? 8 : 0);
+  // kernel dbg bit 3 = the chained look-back: each block walks back 64
+  // predecessors per round to the nearest published inclusive prefix;
+  // without it every thread polls its share of the predecessors' counts, all
+  // in flight together.  Measured at C4 (100 M rows, 1 % AND, 1024 blocks,
+  // profiles/r05/h): with the projected pair gathered from a column group,
+  // polling (flags packed) 29.8 us vs chained 32.1 us; with the columns
+  // gathered separately (one more line per row) chained 45.1 vs polling
+  // 46.6-48.0.  So (lookback 0, auto) narrow projections read from column
+  // groups -- and positions-only launches -- poll, the rest walk the chain;
+  // inclusive prefixes are 32-bit, so tables of >= 2^32 rows always poll.
+  // lookback 1 / 2 (tuning cnf_lookback) force the chain / the polls, as
+  // select_dbg bit 7 (MBX_SELECT_DBG=128) forces the polls.
+  bool grouped = narrow;
+  for (int j = 0; j < nproj; ++j) grouped = grouped && proj[j].gstride > 0;
+  const bool chained = nbits < (int64_t(1) << 32) && !(dbg & 8) &&
+                       (lookback == 1 || (lookback == 0 && !grouped));
+  dbg = (dbg & ~8) | (chained ? 8 : 0);
   // <= kLookbackBlocks blocks for the polling form (one poll load per thread
   // per 256 predecessors); the chained form takes up to kIncBase (tuning
   // cnf_blocks: more blocks than the chip holds at once, so the later ones'
