@@ -326,6 +326,14 @@ class Harness:
         self.ext = torch.cuda.ExternalStream(ctx.stream)
         torch.cuda.set_stream(self.ext)
 
+    def solo(self):
+        """This rank alone (a 1-GPU config inside an N-rank run): the same
+        context and stream, no collectives, no exchange."""
+        import copy
+        h = copy.copy(self)
+        h.world, h.comm, h.exchange = 1, None, False
+        return h
+
     def barrier(self):
         self.ctx.sync()
         self.torch.cuda.synchronize()
@@ -417,8 +425,9 @@ class Harness:
         else:
             enqueue(warmup, warmup + steps)
         t_enq = time.perf_counter() - t0
-        drain()
-        self.torch.cuda.synchronize()
+        if self.exchange and self.comm is None:
+            drain()  # the same-device rehearsal's host exchange belongs to the steps
+        self.torch.cuda.synchronize()  # the whole device: the library stream's steps included
         if self.world > 1:
             self.dist.barrier()
         wall = time.perf_counter() - t0
@@ -935,7 +944,7 @@ def main():
     for name in configs:
         if name == "C2":
             if rank == 0:
-                crecs["C2"] = config_c2(Harness1(H), args)
+                crecs["C2"] = config_c2(H.solo(), args)
             H.barrier()
         elif name == "C4":
             crecs["C4"] = config_c4(H, args)
@@ -1024,14 +1033,6 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-
-
-class Harness1(Harness):
-    """Rank 0 alone (a 1-GPU config inside an N-rank run): no collectives."""
-
-    def __init__(self, H):  # noqa: super().__init__ not called: shares H's state
-        self.__dict__.update(H.__dict__)
-        self.world, self.comm, self.exchange = 1, None, False
 
 
 if __name__ == "__main__":
