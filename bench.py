@@ -63,7 +63,9 @@ importing torch (the launcher's CPU test, tests/test_bench_launch.py).
 Rehearsal knobs (never set by the driver): MBX_BENCH_SAME_DEVICE=1 (N ranks on
 one GPU, gloo exchange), MBX_BENCH_FORCE_EXCHANGE=1 (the exchange at N = 1),
 MBX_BENCH_CORRUPT=frame|count (rank 0 damages its pre-check frame: the
-pre-check must fire).
+pre-check must fire), MBX_BENCH_TORCH_EXCHANGE=1 (the fallback exchange --
+torch.distributed's RCCL group, taken when libmbx's communicator fails on any
+rank -- on purpose, at N = 1 too).
 """
 import argparse
 import json
@@ -319,9 +321,9 @@ def agree(torch, dist, world, rank, reason):
 class Harness:
     """One rank's clocks, barriers and collective verdicts."""
 
-    def __init__(self, torch, dist, m, ctx, world, rank, comm, same_device, exchange):
+    def __init__(self, torch, dist, m, ctx, world, rank, comm, same_device, exchange, torch_pg=None):
         self.torch, self.dist, self.m, self.ctx = torch, dist, m, ctx
-        self.world, self.rank, self.comm = world, rank, comm
+        self.world, self.rank, self.comm, self.torch_pg = world, rank, comm, torch_pg
         self.same_device, self.exchange = same_device, exchange
         self.ext = torch.cuda.ExternalStream(ctx.stream)
         torch.cuda.set_stream(self.ext)
@@ -331,7 +333,7 @@ class Harness:
         context and stream, no collectives, no exchange."""
         import copy
         h = copy.copy(self)
-        h.world, h.comm, h.exchange = 1, None, False
+        h.world, h.comm, h.torch_pg, h.exchange = 1, None, None, False
         return h
 
     def barrier(self):
@@ -546,6 +548,8 @@ def run_c3(H, args, cols, n, s, glob, label):
                 scan(k)
             if H.comm is not None:
                 H.comm.allreduce_count_async(base + 8 * FW * j, FW * (je - j))
+            elif H.torch_pg is not None:  # on the library stream (torch's current stream)
+                H.dist.all_reduce(counts[j:je], group=H.torch_pg)
             elif H.exchange:  # same-device rehearsal: gloo over host copies
                 gloo_works.extend(range(j, je))
 
@@ -601,6 +605,8 @@ def timing_label(G, steps):
 def exchange_name(H, what):
     if H.comm is not None:
         return what
+    if H.torch_pg is not None:
+        return "torch.distributed RCCL group (fallback: libmbx's communicator failed), eager"
     if H.exchange:
         return "gloo (same-device rehearsal)"
     return "none"
@@ -687,6 +693,8 @@ def config_c4(H, args):
             launch(k)
             if H.comm is not None:
                 H.comm.allgather_count_async(cnts.data_ptr() + 8 * k, alls[k].data_ptr())
+            elif H.torch_pg is not None:
+                H.dist.all_gather_into_tensor(alls[k], cnts[k:k + 1], group=H.torch_pg)
             elif world > 1:
                 gloo.append(k)
 
@@ -790,6 +798,9 @@ def config_c5(H, args):
             scan(k)
             if H.comm is not None:  # all-gather + rank-ordered fold into recs[k], on the device
                 H.comm.allreduce_agg_async(recs[k].data_ptr())
+            elif H.torch_pg is not None:  # the same all-gather + the same device fold
+                H.dist.all_gather_into_tensor(gathered.view(-1), recs[k], group=H.torch_pg)
+                ctx.agg_fold_async(gathered.data_ptr(), world, recs[k].data_ptr())
             elif world > 1:
                 gloo.append(k)
 
@@ -875,15 +886,23 @@ def main():
     same_device = os.environ.get("MBX_BENCH_SAME_DEVICE") == "1"
     device = 0 if same_device else local_rank
     torch.cuda.set_device(device)
-    exchange = world > 1 or os.environ.get("MBX_BENCH_FORCE_EXCHANGE") == "1"
+    # MBX_BENCH_TORCH_EXCHANGE=1 (rehearsal): the fallback exchange
+    # (torch.distributed's RCCL group) even where libmbx's communicator works;
+    # at N = 1 over a one-rank group
+    torch_exchange = os.environ.get("MBX_BENCH_TORCH_EXCHANGE") == "1"
+    exchange = world > 1 or os.environ.get("MBX_BENCH_FORCE_EXCHANGE") == "1" or torch_exchange
     if world > 1:
         # host-side bootstrap, barriers, verdicts and the max-over-ranks clock
         # only: the data-path exchange is libmbx's own RCCL communicator
         dist.init_process_group("gloo")
+    elif torch_exchange:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
     m = mbx_pkg.load()
     ctx = m.Context(device)
 
     comm = None
+    torch_pg = None  # fallback exchange: torch.distributed's own RCCL group (eager)
+    reason = None
     if exchange and not same_device:
         uid = m.mbx.comm_unique_id() if rank == 0 else None
         if world > 1:
@@ -891,13 +910,26 @@ def main():
             dist.broadcast_object_list(box, src=0)
             uid = box[0]
         try:
+            if torch_exchange:
+                raise m.MbxError(m.mbx.E_INVALID, "MBX_BENCH_TORCH_EXCHANGE=1")
             comm = ctx.comm_init_rank(world, rank, uid)
-            reason = None
         except m.MbxError as err:
             reason = f"libmbx RCCL communicator failed ({err})"
-    H = Harness(torch, dist, m, ctx, world, rank, comm, same_device, exchange)
-    if exchange and not same_device:
-        H.agree(reason)
+            print(f"rank {rank}: {reason}", file=sys.stderr)
+        if world > 1 or torch_exchange:
+            # every rank takes the same exchange: libmbx's communicator if it
+            # came up everywhere, else torch.distributed's RCCL group
+            flag = torch.tensor([int(comm is not None)], dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag[0]) == 0:
+                if comm is not None:
+                    comm.close()
+                    comm = None
+                torch_pg = dist.new_group(backend="nccl")
+                reason = None
+                print(f"rank {rank}: exchange falls back to torch.distributed (nccl = RCCL)", file=sys.stderr)
+    H = Harness(torch, dist, m, ctx, world, rank, comm, same_device, exchange, torch_pg)
+    H.agree(reason)
 
     # ---- headline: C3 ------------------------------------------------------
     if args.scaling == "strong":
@@ -961,7 +993,9 @@ def main():
         xchg = ((f"RCCL all-reduce of the COUNTs of every {B} steps (libmbx mbx_comm, after the scans)" if B > 1
                  else "RCCL all-reduce of every step's COUNT (one collective per query; libmbx mbx_comm, right "
                       "after the step's scan on the same stream)")
-                if comm is not None else None) or ("gloo all-reduce (same-device rehearsal)" if exchange else "none")
+                if comm is not None else None) or (
+            "torch.distributed RCCL all-reduce per step (fallback: libmbx's communicator failed), eager"
+            if torch_pg is not None else None) or ("gloo all-reduce (same-device rehearsal)" if exchange else "none")
         out = {
             "metric": METRIC,
             "value": n_global * steps / (ms_per_step * 1e-3 * steps),
@@ -1030,7 +1064,7 @@ def main():
         os.write(out_fd, (json.dumps(out) + "\n").encode())
 
     ctx.close()
-    if world > 1:
+    if world > 1 or torch_exchange:
         dist.barrier()
         dist.destroy_process_group()
 
