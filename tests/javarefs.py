@@ -235,7 +235,7 @@ def _tokens(s):
             break
         line += s.count("\n", pos, m.start(0) + len(m.group(0)) - len((m.group(1) or m.group(2) or m.group(3))))
         t = m.group(1) or m.group(2) or m.group(3)
-        toks.append((t, line))
+        toks.append((t, line, m.end() - len(t)))
         pos = m.end()
     return toks
 
@@ -260,18 +260,78 @@ def _match_paren(toks, i):
     raise ValueError("unbalanced")
 
 
-def _var_types(s):
-    """name -> set of declared (base) types in one source: fields, params,
-    locals, for-each variables"""
-    out = {}
-    pat = re.compile(r"(?<![\w.])([A-Za-z_][\w.]*)\s*(<(?:[^<>]|<[^<>]*>)*>)?\s*((?:\[\s*\])*)\s+"
-                     r"([A-Za-z_]\w*)\s*((?:\[\s*\])*)\s*(?=[=;,:)])")
-    for m in pat.finditer(s):
+_DECL = re.compile(r"(?<![\w.])([A-Za-z_][\w.]*)\s*(<(?:[^<>]|<[^<>]*>)*>)?\s*((?:\[\s*\])*)\s+"
+                   r"([A-Za-z_]\w*)\s*((?:\[\s*\])*)\s*(?=[=;,:)])")
+
+
+def _decls(s):
+    """[(position, name, declared base type)] of every field, parameter,
+    local and for-each variable in one source"""
+    out = []
+    for m in _DECL.finditer(s):
         typ, dims1, name, dims2 = m.group(1), m.group(3).count("["), m.group(4), m.group(5).count("[")
         if typ in ("return", "new", "throw", "else", "case", "package", "import") or name in KEYWORDS:
             continue
-        out.setdefault(name, set()).add(typ + "[]" * (dims1 + dims2))
+        out.append((m.start(4), name, typ + "[]" * (dims1 + dims2)))
     return out
+
+
+def _var_types(s):
+    """name -> set of declared (base) types in one source (any scope)"""
+    out = {}
+    for _, name, typ in _decls(s):
+        out.setdefault(name, set()).add(typ)
+    return out
+
+
+def _member_ranges(s):
+    """[(start, end)] of each member of the top-level class body: from the end
+    of the previous member (its header, parameters included) to its closing
+    brace -- the scope of its parameters and locals"""
+    out = []
+    m = re.search(r"\bclass\s+\w+[^{]*\{", s)
+    if not m:
+        return out
+    depth, start = 1, m.end()
+    for i in range(m.end(), len(s)):
+        ch = s[i]
+        if ch == "{":
+            depth += 1
+        elif ch == "}":
+            depth -= 1
+            if depth == 1:
+                out.append((start, i + 1))
+                start = i + 1
+            elif depth == 0:
+                break
+        elif ch == ";" and depth == 1:
+            start = i + 1
+    return out
+
+
+class Scope:
+    """A use's declared type: the nearest declaration before it in the same
+    member (parameters and locals), else the class's fields; None when that
+    is still ambiguous."""
+
+    def __init__(self, s):
+        self.decls = _decls(s)
+        self.ranges = _member_ranges(s)
+
+    def _range(self, pos):
+        for a, b in self.ranges:
+            if a <= pos < b:
+                return a, b
+        return None
+
+    def type_of(self, name, pos):
+        r = self._range(pos)
+        if r:
+            local = [(p, t) for p, n, t in self.decls if n == name and r[0] <= p < pos]
+            if local:
+                return max(local)[1]
+        fields = {t for p, n, t in self.decls if n == name and self._range(p) is None}
+        return next(iter(fields)) if len(fields) == 1 else None
 
 
 class Resolver:
@@ -418,6 +478,7 @@ def references(src, resolver, path=""):
                     rep(0, f"implements abstract {c}.{name}({mm['arity']} args)", ok,
                         "abstract method not implemented (or with weaker access)")
     vars_ = _var_types(s)
+    scope = Scope(s)
     toks = _tokens(s)
     # skip the package / import statements
     k = 0
@@ -432,7 +493,7 @@ def references(src, resolver, path=""):
             break
     i = 0
     while i < len(toks):
-        t, line = toks[i]
+        t, line, tpos = toks[i]
         prev = toks[i - 1][0] if i else ""
         if t == "new" and i + 1 < len(toks):
             # new C(...) [.chain]
@@ -489,11 +550,10 @@ def references(src, resolver, path=""):
             if nxt in (".", "["):
                 base = None
                 if t in vars_:
-                    types = vars_[t]
-                    qs = [R.type_of(x, ctx) for x in types]
-                    qs = [x for x in qs if x[0]]
-                    if len(qs) == 1 and len(types) == 1:
-                        base = (qs[0], False)
+                    typ = scope.type_of(t, tpos)
+                    q = R.type_of(typ, ctx) if typ else (None, 0)
+                    if q[0]:
+                        base = (q, False)
                 elif re.match(r"[A-Z]", t):
                     name, j = t, i
                     q = R.lookup_class(name, ctx)
@@ -540,7 +600,7 @@ def _chain(R, toks, i, cur, static_ctx, ctx, rep, subclass=False):
             continue
         if t != "." or i + 1 >= len(toks):
             return i
-        name, line = toks[i + 1]
+        name, line, _ = toks[i + 1]
         if q is None:
             return i
         if dims > 0:  # arrays: .length / clone()

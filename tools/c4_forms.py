@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--blocks", default="0", help="comma list of tuning cnf_blocks values (0: the default grid)")
     ap.add_argument("--positions-only", action="store_true", help="no projection: positions + COUNT only")
+    ap.add_argument("--select-dbg", default="0",
+                    help="comma list of tuning select_dbg values (512: flip the write-through choice of the outputs)")
     ap.add_argument("--lookback", default="default",
                     help="comma list: default | chained | poll16 | poll1 (k_cnf_select's look-back form)")
     args = ap.parse_args()
@@ -47,7 +49,7 @@ def main():
 
     LB = {"default": None, "chained": (1, 1), "poll16": (2, 16), "poll1": (2, 1)}  # (cnf_lookback, flag stride)
 
-    def run(n, group, timed, blocks=0, lookback="default"):
+    def run(n, group, timed, blocks=0, lookback="default", sdbg=0):
         cols, t, a, b = table(n)
         if group:
             ctx.group(t, [0, 1])
@@ -60,6 +62,7 @@ def main():
         o1 = torch.zeros(cap, dtype=torch.int32, device="cuda")
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
         ctx.set_tuning("cnf_blocks", blocks)
+        ctx.set_tuning("select_dbg", sdbg)
         if LB[lookback]:
             ctx.set_tuning("cnf_lookback", LB[lookback][0])
             ctx.set_tuning("cnf_flag_stride", LB[lookback][1])
@@ -71,7 +74,7 @@ def main():
         ctx.sync()
         ok = (int(cnt.item()) == want and bool((ids[:want] == torch.nonzero(sel).flatten() + 192).all())
               and (args.positions_only or (bool((o0[:want] == c0[sel]).all()) and bool((o1[:want] == c1[sel]).all()))))
-        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "positions_only": args.positions_only, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
+        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "select_dbg": sdbg, "positions_only": args.positions_only, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
                "selected": want, "ok": ok}
         if timed:
             ctx.graph_begin()
@@ -99,21 +102,24 @@ def main():
     bad = 0
     blocks = [int(x) for x in args.blocks.split(",")]
     lbs = args.lookback.split(",")
+    sdbgs = [int(x) for x in args.select_dbg.split(",")]
     for n in map(int, args.check_rows.split(",")):
         for group in (True, False):
             for b in blocks:
                 for lb in lbs:
-                    r = run(n, group, False, b, lb)
-                    bad += not r["ok"]
-                    print(json.dumps(r), flush=True)
+                    for sd in sdbgs:
+                        r = run(n, group, False, b, lb, sd)
+                        bad += not r["ok"]
+                        print(json.dumps(r), flush=True)
     for n in map(int, args.rows.split(",")):
         for rep in range(2):
             for group in (True, False):
                 for b in blocks:
                     for lb in lbs:
-                        r = run(n, group, True, b, lb)
-                        bad += not (r["ok"] and r["ok_after"])
-                        print(json.dumps(r), flush=True)
+                        for sd in sdbgs:
+                            r = run(n, group, True, b, lb, sd)
+                            bad += not (r["ok"] and r["ok_after"])
+                            print(json.dumps(r), flush=True)
     ctx.close()
     sys.exit(1 if bad else 0)
 
