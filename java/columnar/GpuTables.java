@@ -170,7 +170,8 @@ public final class GpuTables {
    * Stage (if needed) a Columnarfile and add a column group over 2..4 of its
    * 4-byte columns (0-based): index / file scans projecting them gather one
    * 128-byte line per selected row (DESIGN.md section 2).  Lives with the
-   * staged table (dropped by invalidate).
+   * staged table (dropped by invalidate); an empty cols array drops the
+   * table's groups (mbx_table_group with ncols = 0).
    */
   public static synchronized void group(String columnarFile, int[] cols) throws Exception {
     Native.tableGroup(GpuContext.ctx(), get(columnarFile), cols);
