@@ -469,10 +469,11 @@ def full_count(torch, n_global, seed_base):
     return c
 
 
-def read_probe(H, table, reps=30):
+def read_probe(H, table, reps=20):
     """Best read bandwidth of k_read_probe (mbx_probe_read: the C3 kernel's
     tiles and non-temporal dwordx4 loads over c0, c1 with no predicate) over a
-    few block mappings, timed with HIP events on the library stream."""
+    few block mappings, timed like the scan: one captured graph of `reps`
+    launches replayed between HIP events on the library stream."""
     torch, ctx = H.torch, H.ctx
     n = table.nrows
     nbytes = 2 * 4 * (n // 256 * 256)
@@ -482,15 +483,7 @@ def read_probe(H, table, reps=30):
                 ("grid-stride 2048 blocks", dict(interleave=True, grid=2048))]
     res = {}
     for name, kw in variants:
-        for _ in range(3):
-            ctx.probe_read(table, [0, 1], **kw)
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(H.ext)
-        for _ in range(reps):
-            ctx.probe_read(table, [0, 1], **kw)
-        b.record(H.ext)
-        ctx.sync()
-        ms = a.elapsed_time(b) / reps
+        ms, _ = H.solo().kernel_ms(lambda i: ctx.probe_read(table, [0, 1], **kw), reps)
         res[name] = nbytes / (ms * 1e-3) / 1e9
     best = max(res, key=res.get)
     return {"best_gbs": res[best], "best": best, "gbs": res}
