@@ -104,6 +104,7 @@ static void tuning_from_env(MbxTuning& t) {
   t.cnf_blocks = (int32_t)env_knob("MBX_CNF_BLOCKS", 0);
   t.cnf_flag_stride = env_knob("MBX_CNF_FLAG_STRIDE", 1) == kFlagStride ? kFlagStride : 1;
   t.cnf_lookback = (int32_t)env_knob("MBX_CNF_LOOKBACK", 0);
+  t.cnf_store = (int32_t)env_knob("MBX_CNF_STORE", 0) & 3;
   if (t.cnf_lookback < 0 || t.cnf_lookback > 2) t.cnf_lookback = 0;
   t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
   if (t.select_blocks < 1) t.select_blocks = 1024;  // as mbx_set_tuning: never a zero / negative grid divisor
@@ -319,6 +320,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "cnf_blocks")) t.cnf_blocks = v < 0 ? 0 : (int32_t)v;
   else if (!strcmp(knob, "cnf_flag_stride")) t.cnf_flag_stride = v == kFlagStride ? kFlagStride : 1;
   else if (!strcmp(knob, "cnf_lookback")) t.cnf_lookback = v >= 0 && v <= 2 ? (int32_t)v : 0;
+  else if (!strcmp(knob, "cnf_store")) t.cnf_store = v >= 0 && v <= 3 ? (int32_t)v : 0;
   else if (!strcmp(knob, "cursor_prefetch")) t.cursor_prefetch = v;
   else if (!strcmp(knob, "scan_select_fused")) t.scan_select_fused = v;
   else if (!strcmp(knob, "scan_select_waves")) t.scan_select_waves = v == 4 ? 4 : 16;
@@ -1748,6 +1750,15 @@ static int cnf_proj_args(const mbx_table* t, const int32_t* proj, int32_t nproj,
   return MBX_OK;
 }
 
+static CnfTune cnf_tune(const mbx_ctx* c) {
+  CnfTune k;
+  k.blocks = c->tune.cnf_blocks;
+  k.flag_stride = c->tune.cnf_flag_stride;
+  k.lookback = c->tune.cnf_lookback;
+  k.store = c->tune.cnf_store;
+  return k;
+}
+
 extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* const* bms,
                                          const int32_t* conj_offsets, int32_t nconj, const mbx_bitmap* deleted,
                                          const int32_t* proj, int32_t nproj, int64_t* dev_ids,
@@ -1767,10 +1778,11 @@ extern "C" int mbx_cnf_materialize_async(mbx_ctx* c, const mbx_table* t, const m
     if (!c->stamps) HIPCHK(hipMalloc(&c->stamps, sizeof(int64_t) * 4 * kMaxStampBlocks));
     stamps = c->stamps;
   }
+  CnfTune ct = cnf_tune(c);
+  if (stamps) ct.blocks = 0;  // the stamps buffer holds <= 1024 blocks
   HIPCHK(launch_cnf_materialize(C, deleted ? deleted->words : nullptr, nwords, t->nrows, c->lookback,
                                 t->row_offset, dev_ids, pc, dev_out, nproj, dev_count, c->stream, stamps,
-                                c->tune.select_dbg >> 4, INT64_MAX, stamps ? 0 : c->tune.cnf_blocks,
-                                c->tune.cnf_flag_stride, c->tune.cnf_lookback));
+                                c->tune.select_dbg >> 4, INT64_MAX, &ct));
   return MBX_OK;
 }
 
@@ -2123,10 +2135,10 @@ extern "C" int mbx_cnf_cursor_launch(mbx_ctx* c, const mbx_table* t, const mbx_b
   for (int32_t j = 0; j < nproj; j++) {
     pc[j] = proj_col(t, proj[j]);
   }
+  const CnfTune ct = cnf_tune(c);
   e = launch_cnf_materialize(C, deleted ? deleted->words : nullptr, (t->nrows + 63) >> 6, t->nrows, c->lookback,
                              t->row_offset, k->ids, pc, k->outs.data(), nproj, k->dcount, c->stream, nullptr,
-                             c->tune.select_dbg >> 4, bound, c->tune.cnf_blocks, c->tune.cnf_flag_stride,
-                             c->tune.cnf_lookback);
+                             c->tune.select_dbg >> 4, bound, &ct);
   if (e != hipSuccess) {
     mbx_cursor_close(k);
     return fail(MBX_E_DEVICE, "cnf_cursor: %s", hipGetErrorString(e));

@@ -335,12 +335,17 @@ hipError_t launch_finalize(const Partial* partials, int64_t nblocks, int32_t agg
 // one launch: words of the CNF (never stored) -> positions (ids may be null)
 // + <= 4 projected 4-byte columns; lb = kLookbackWords int64 look-back words,
 // zeroed once at allocation (k_cnf_select)
+// k_cnf_select's A/B knobs (MbxTuning cnf_*): grid (0: 1024 blocks), polled
+// flag stride (1 or kFlagStride), look-back form (0 auto, 1 chained, 2
+// polled), output stores (0 default, 1 plain, 2 write-through, 3 nontemporal)
+struct CnfTune {
+  int32_t blocks = 0, flag_stride = 1, lookback = 0, store = 0;
+};
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
                                   int64_t* stamps = nullptr, int32_t dbg = 0,
-                                  int64_t cap = INT64_MAX, int32_t blocks = 0, int32_t flag_stride = 1,
-                                  int32_t lookback = 0);
+                                  int64_t cap = INT64_MAX, const struct CnfTune* tune = nullptr);
 // epoch, per-block counts, per-block inclusive prefixes; the polling form's
 // counts may sit one per 128-byte line (kFlagStride words apart)
 constexpr int32_t kFlagStride = 16;

@@ -618,10 +618,13 @@ struct GatherW {
 // (C4) it is neutral for the projection and +1.2 us with positions, so
 // those stay plain.  Kernel dbg bit 5 (select_dbg 512) flips the choice
 // (profiles/r03/lb/wt_*).
+// wt: 0 plain, 1 write-through, 2 nontemporal (the line is not kept in L2)
 template <class T>
-__device__ __forceinline__ void put(T* p, T v, bool wt) {
-  if (wt)
+__device__ __forceinline__ void put(T* p, T v, int wt) {
+  if (wt == 1)
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else if (wt == 2)
+    __builtin_nontemporal_store(v, p);
   else
     *p = v;
 }
@@ -650,7 +653,7 @@ __device__ __forceinline__ void wide_row(const GatherW& G, int64_t p, int64_t o)
 template <int G4, class GT = Gather4>
 __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const StepScan& r, int64_t& off,
                                            int64_t row_offset, int64_t* __restrict__ ids, const uint16_t* st,
-                                           int lane, const GT& G, uint32_t first = 0, bool wt = false,
+                                           int lane, const GT& G, uint32_t first = 0, int wt = 0,
                                            bool nt = false) {
   if (r.total == 0) return;
   const int64_t lbase = base * 64;  // table-local row of bit 0 of word `base`
@@ -734,7 +737,7 @@ __device__ __forceinline__ void store_step(int64_t base, uint64_t mw, const Step
 template <int G4 = 0, class GT = Gather4>
 __device__ __forceinline__ void emit_step(int64_t base, uint64_t mw, int64_t& off, int64_t row_offset,
                                           int64_t* __restrict__ ids, uint16_t* st, int lane, const GT& G,
-                                          bool wt = false) {
+                                          int wt = 0) {
   const StepScan r = stage_step(mw, st, lane);
   store_step<G4, GT>(base, mw, r, off, row_offset, ids, st, lane, G, 0, wt);
 }
@@ -1833,7 +1836,11 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   // cost, for the C2 anatomy)
   const bool fits = off + bc <= G.cap && !(dbg & (64 | 16));
   off += wpos;
-  const bool wt = (G4 == 0) != ((dbg & 32) != 0);
+  // the outputs' stores (dbg bits 12-13, tuning cnf_store): 0 the default --
+  // write-through for positions only, plain with gathered values (dbg bit 5
+  // flips it) -- 1 plain, 2 write-through, 3 nontemporal
+  const int smode = (dbg >> 12) & 3;
+  const int wt = smode == 0 ? ((G4 == 0) != ((dbg & 32) != 0) ? 1 : 0) : (smode == 1 ? 0 : (smode == 2 ? 1 : 2));
   if (!fits) {
   } else if (cached) {
     // the prefetched rows, then the rest of the staged ones, then the steps
@@ -2545,9 +2552,11 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                                   void* const* out, int32_t nproj, int64_t* total, hipStream_t s,
-                                  int64_t* stamps, int32_t dbg, int64_t cap, int32_t blocks, int32_t flag_stride,
-                                  int32_t lookback) {
+                                  int64_t* stamps, int32_t dbg, int64_t cap, const CnfTune* tune) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
+  const CnfTune knobs = tune ? *tune : CnfTune{};
+  const int32_t blocks = knobs.blocks, flag_stride = knobs.flag_stride, lookback = knobs.lookback;
+  dbg = (dbg & ~(3 << 12)) | ((knobs.store & 3) << 12);
   if (nproj < 0 || nproj > kMaxProj) return hipErrorInvalidValue;
   // <= 4 four-byte columns: values prefetched in registers (Gather4); any
   // other projection (char(n) rows, more columns): row copies (GatherW)

@@ -22,8 +22,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--blocks", default="0", help="comma list of tuning cnf_blocks values (0: the default grid)")
     ap.add_argument("--positions-only", action="store_true", help="no projection: positions + COUNT only")
-    ap.add_argument("--select-dbg", default="0",
-                    help="comma list of tuning select_dbg values (512: flip the write-through choice of the outputs)")
+    ap.add_argument("--store", default="0",
+                    help="comma list of tuning cnf_store values (0 default, 1 plain, 2 write-through, 3 nontemporal)")
     ap.add_argument("--lookback", default="default",
                     help="comma list: default | chained | poll16 | poll1 (k_cnf_select's look-back form)")
     args = ap.parse_args()
@@ -49,7 +49,7 @@ def main():
 
     LB = {"default": None, "chained": (1, 1), "poll16": (2, 16), "poll1": (2, 1)}  # (cnf_lookback, flag stride)
 
-    def run(n, group, timed, blocks=0, lookback="default", sdbg=0):
+    def run(n, group, timed, blocks=0, lookback="default", store=0):
         cols, t, a, b = table(n)
         if group:
             ctx.group(t, [0, 1])
@@ -62,7 +62,7 @@ def main():
         o1 = torch.zeros(cap, dtype=torch.int32, device="cuda")
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
         ctx.set_tuning("cnf_blocks", blocks)
-        ctx.set_tuning("select_dbg", sdbg)
+        ctx.set_tuning("cnf_store", store)
         if LB[lookback]:
             ctx.set_tuning("cnf_lookback", LB[lookback][0])
             ctx.set_tuning("cnf_flag_stride", LB[lookback][1])
@@ -74,7 +74,7 @@ def main():
         ctx.sync()
         ok = (int(cnt.item()) == want and bool((ids[:want] == torch.nonzero(sel).flatten() + 192).all())
               and (args.positions_only or (bool((o0[:want] == c0[sel]).all()) and bool((o1[:want] == c1[sel]).all()))))
-        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "select_dbg": sdbg, "positions_only": args.positions_only, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
+        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "store": store, "positions_only": args.positions_only, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
                "selected": want, "ok": ok}
         if timed:
             ctx.graph_begin()
@@ -102,7 +102,7 @@ def main():
     bad = 0
     blocks = [int(x) for x in args.blocks.split(",")]
     lbs = args.lookback.split(",")
-    sdbgs = [int(x) for x in args.select_dbg.split(",")]
+    sdbgs = [int(x) for x in args.store.split(",")]
     for n in map(int, args.check_rows.split(",")):
         for group in (True, False):
             for b in blocks:
