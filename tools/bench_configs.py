@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
-"""Per-config throughput of the other BASELINE.json workloads (the bench line
-itself is C3, bench.py).  Inputs resident in HBM; each query is timed with
+"""Per-config throughput of the other BASELINE.json workloads, with their A/B
+variants (one-launch vs two-launch forms, look-back forms, segment sizes).
+Since round 5 the driver's own bench line carries one record per config
+(bench.py `configs`: C2, C4 with its column group, C5 per GPU, sharded with
+their RCCL exchange at N > 1); this tool keeps the variant sweeps.  Inputs resident in HBM; each query is timed with
 HIP events on the library stream over K async steps, and its result checked
 against a torch reduction of the same device data.
 
