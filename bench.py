@@ -592,7 +592,8 @@ def run_c3(H, args, cols, n, s, glob, label):
 
 
 def timing_label(G, steps):
-    return f"HIP graphs of {G} queries replayed, {steps} timed" if G else f"{steps} eager queries (gloo exchange)"
+    return f"HIP graphs of {G} queries replayed, {steps} timed" if G else \
+        f"{steps} eager queries (host-side or torch.distributed exchange)"
 
 
 def exchange_name(H, what):

@@ -1837,10 +1837,13 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
   const bool fits = off + bc <= G.cap && !(dbg & (64 | 16));
   off += wpos;
   // the outputs' stores (dbg bits 12-13, tuning cnf_store): 0 the default --
-  // write-through for positions only, plain with gathered values (dbg bit 5
-  // flips it) -- 1 plain, 2 write-through, 3 nontemporal
+  // write-through for positions only (k_cnf_select with no projected column
+  // too: 13.7-14.0 vs 14.9 us at C4's 1 M positions, profiles/r05/l), plain
+  // with gathered values (write-through 33.1 vs 30.0 us, nontemporal 30.4-30.7;
+  // dbg bit 5 flips the default) -- 1 plain, 2 write-through, 3 nontemporal
   const int smode = (dbg >> 12) & 3;
-  const int wt = smode == 0 ? ((G4 == 0) != ((dbg & 32) != 0) ? 1 : 0) : (smode == 1 ? 0 : (smode == 2 ? 1 : 2));
+  const bool positions_only = G4 == 0 || G.n == 0;
+  const int wt = smode == 0 ? ((positions_only != ((dbg & 32) != 0)) ? 1 : 0) : (smode == 1 ? 0 : (smode == 2 ? 1 : 2));
   if (!fits) {
   } else if (cached) {
     // the prefetched rows, then the rest of the staged ones, then the steps
