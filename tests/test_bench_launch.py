@@ -93,7 +93,7 @@ def test_default_run_adds_every_config_record():
     with kernel time from graph replay."""
     b = _bench_module()
     a = b.make_parser().parse_args([])
-    assert a.configs == "C2,C4,C5" and a.scaling == "weak" and not a.no_strong
+    assert sorted(a.configs.split(",")) == ["C2", "C4", "C5"] and a.scaling == "weak" and not a.no_strong
     assert a.c4_rows == 100_000_000 and a.c5_rows == 125_000_000 and a.kernel_graph >= 10
     rec = b.config_record("C4", 100_000_000, 50_000_000, 2, 1_000_000, 0.040, "k", 0.030, 0.031, 33_000_000,
                           "RCCL", "ok", "graph replay")
