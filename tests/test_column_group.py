@@ -176,3 +176,40 @@ def test_group_of_wrapped_columns_is_a_snapshot_until_rebuilt(m, ctx):
     ctx.group(t, [0, 1])                # ... and rebuild
     r0, r1 = rows()
     assert bool((r0 == c[0][sel]).all()) and bool((r1 == c[1][sel]).all())
+
+
+@pytest.mark.parametrize("lookback,store,blocks", [(1, 0, 0), (2, 0, 0), (0, 1, 0), (0, 2, 0), (0, 3, 0),
+                                                   (1, 3, 2048), (2, 2, 512), (1, 0, 8192)])
+@pytest.mark.parametrize("group", [False, True])
+def test_cnf_select_knobs_keep_results(m, ctx, lookback, store, blocks, group):
+    """every A/B form of the one-launch ColumnarIndexScan (look-back chained /
+    polled, output stores plain / write-through / nontemporal, grids below
+    and above the resident one) returns the same positions and rows"""
+    n = 1_500_007
+    cols = table(n, seed=21)
+    t = ctx.stage(cols)
+    if group:
+        ctx.group(t, [0, 5])
+    r2 = helpers.index_registry(ctx, cols, t, 2)
+    r3 = helpers.index_registry(ctx, cols, t, 3)
+    sel = (cols[2][2] == 3) & (cols[3][2] == 7)
+    k = int(sel.sum())
+    try:
+        ctx.set_tuning("cnf_lookback", lookback)
+        ctx.set_tuning("cnf_store", store)
+        ctx.set_tuning("cnf_blocks", blocks)
+        for proj in ([5, 0], []):
+            ids = torch.full((k + 8,), -1, dtype=torch.int64, device="cuda")
+            outs = [torch.zeros(k + 8, dtype=torch.int32, device="cuda") for _ in proj]
+            cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            for _ in range(2):  # twice: the second launch reads the first one's look-back words
+                ctx.cnf_materialize_async(t, [[r2[3]], [r3[7]]], proj, ids.data_ptr(), [o.data_ptr() for o in outs],
+                                          cnt.data_ptr())
+            ctx.sync()
+            assert int(cnt.item()) == k
+            assert np.array_equal(ids[:k].cpu().numpy(), np.nonzero(sel)[0])
+            for j, o in zip(proj, outs):
+                assert np.array_equal(o[:k].cpu().numpy(), cols[j][2][sel])
+    finally:
+        ctx.set_tuning("reset")
