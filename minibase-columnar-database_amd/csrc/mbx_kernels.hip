@@ -1921,8 +1921,13 @@ __device__ __forceinline__ void select_tail(const uint64_t (&wr)[NR], int64_t c,
 // us, profiles/r05/c: its extra registers cut residency from 4 to 3 blocks
 // per CU, and round 2 waits on every block's round 1, so the grid must be
 // resident at once -- DESIGN.md section 3).
-template <int G4, int NB, class GT = Gather4, int R = 1, int NR = kSelRegs>
-__global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
+// NW: waves per block.  Production launches 4: workgroups reach the CUs at
+// ~220 per us, so C4's 1024 four-wave blocks take ~4.6 us to all start
+// (profiles/r05/o) -- 256 sixteen-wave blocks start within ~2 us but run the
+// query in 41 vs 30 us: a block's count waits for its slowest of 16 waves
+// while its other waves' gathers already load HBM (profiles/r05/p)
+template <int G4, int NB, class GT = Gather4, int R = 1, int NR = kSelRegs, int NW = kWaves>
+__global__ __launch_bounds__(64 * NW) void k_cnf_select(BitmapCnf C, const uint64_t* __restrict__ del,
                                                        int64_t nwords, uint64_t tail_mask, int64_t words_per_block,
                                                        int64_t* __restrict__ lb, int64_t row_offset,
                                                        int64_t* __restrict__ ids, int64_t* __restrict__ total,
@@ -1940,9 +1945,9 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   // stamps (diagnostic, select_dbg bit 3): per block wall_clock64() at start /
   // count published / offset known / end
   if (stamps && threadIdx.x == 0) stamps[4 * blockIdx.x] = wall_clock64();
-  __shared__ int64_t wcount[kWaves];
-  __shared__ int64_t wpre[kWaves];
-  __shared__ uint16_t stage[kWaves][32 * 64];
+  __shared__ int64_t wcount[NW];
+  __shared__ int64_t wpre[NW];
+  __shared__ uint16_t stage[NW][32 * 64];
   const int lane = threadIdx.x & 63;
   const int wave = (int)uniform(threadIdx.x >> 6);
   // epochs 1 .. 2^31 - 1: epoch << 32 stays a positive int64
@@ -1952,7 +1957,7 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
   auto range = [&](int64_t seg, int64_t& a0, int64_t& a1) {
     const int64_t s0 = min(seg * words_per_block, nwords);
     const int64_t s1 = min(s0 + words_per_block, nwords);
-    const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
+    const int64_t per = (s1 - s0 + NW - 1) / NW;
     a0 = min(s0 + wave * per, s1);
     a1 = min(a0 + per, s1);
   };
@@ -2018,7 +2023,7 @@ __global__ __launch_bounds__(kBlock) void k_cnf_select(BitmapCnf C, const uint64
         if (n1 - n0 <= 64 * NR) load_ops(n0, n1);
       }
     };
-    select_tail<G4, GT, decltype(word_at), kWaves, NR>(wr, c, cached, a0, a1, word_at, lane, wave, lb, epoch,
+    select_tail<G4, GT, decltype(word_at), NW, NR>(wr, c, cached, a0, a1, word_at, lane, wave, lb, epoch,
                                                          row_offset, ids, total, G, R == 1 ? stamps : nullptr, dbg,
                                                          nullptr, 0, wcount, wpre, stage, nullptr, fs, seg, nseg,
                                                          after);

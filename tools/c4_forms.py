@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--blocks", default="0", help="comma list of tuning cnf_blocks values (0: the default grid)")
     ap.add_argument("--positions-only", action="store_true", help="no projection: positions + COUNT only")
+    ap.add_argument("--waves", default="4", help="comma list of tuning cnf_waves values (4 or 16)")
     ap.add_argument("--store", default="0",
                     help="comma list of tuning cnf_store values (0 default, 1 plain, 2 write-through, 3 nontemporal)")
     ap.add_argument("--lookback", default="default",
@@ -49,7 +50,7 @@ def main():
 
     LB = {"default": None, "chained": (1, 1), "poll16": (2, 16), "poll1": (2, 1)}  # (cnf_lookback, flag stride)
 
-    def run(n, group, timed, blocks=0, lookback="default", store=0):
+    def run(n, group, timed, blocks=0, lookback="default", store=0, waves=4):
         cols, t, a, b = table(n)
         if group:
             ctx.group(t, [0, 1])
@@ -63,6 +64,8 @@ def main():
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
         ctx.set_tuning("cnf_blocks", blocks)
         ctx.set_tuning("cnf_store", store)
+        if waves != 4:
+            ctx.set_tuning("cnf_waves", waves)  # round 5's 16-wave A/B (profiles/r05/p); knob since removed
         if LB[lookback]:
             ctx.set_tuning("cnf_lookback", LB[lookback][0])
             ctx.set_tuning("cnf_flag_stride", LB[lookback][1])
@@ -74,7 +77,7 @@ def main():
         ctx.sync()
         ok = (int(cnt.item()) == want and bool((ids[:want] == torch.nonzero(sel).flatten() + 192).all())
               and (args.positions_only or (bool((o0[:want] == c0[sel]).all()) and bool((o1[:want] == c1[sel]).all()))))
-        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "store": store, "positions_only": args.positions_only, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
+        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "store": store, "waves": waves, "positions_only": args.positions_only, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
                "selected": want, "ok": ok}
         if timed:
             ctx.graph_begin()
@@ -103,23 +106,26 @@ def main():
     blocks = [int(x) for x in args.blocks.split(",")]
     lbs = args.lookback.split(",")
     sdbgs = [int(x) for x in args.store.split(",")]
+    wavess = [int(x) for x in args.waves.split(",")]
     for n in map(int, args.check_rows.split(",")):
         for group in (True, False):
             for b in blocks:
                 for lb in lbs:
                     for sd in sdbgs:
-                        r = run(n, group, False, b, lb, sd)
-                        bad += not r["ok"]
-                        print(json.dumps(r), flush=True)
+                        for wv in wavess:
+                            r = run(n, group, False, b, lb, sd, wv)
+                            bad += not r["ok"]
+                            print(json.dumps(r), flush=True)
     for n in map(int, args.rows.split(",")):
         for rep in range(2):
             for group in (True, False):
                 for b in blocks:
                     for lb in lbs:
                         for sd in sdbgs:
-                            r = run(n, group, True, b, lb, sd)
-                            bad += not (r["ok"] and r["ok_after"])
-                            print(json.dumps(r), flush=True)
+                            for wv in wavess:
+                                r = run(n, group, True, b, lb, sd, wv)
+                                bad += not (r["ok"] and r["ok_after"])
+                                print(json.dumps(r), flush=True)
     ctx.close()
     sys.exit(1 if bad else 0)
 
