@@ -434,8 +434,10 @@ int mbx_probe_read(mbx_ctx *ctx, const mbx_table *t, const int32_t *cols, int32_
  * counterpart.  mbx_init reads their MBX_* environment defaults once; no
  * launch reads the environment.  knob: "tiles_per_block", "force_generic",
  * "scan_hoist", "scan_ri", "sink_lds", "ticket_groups", "fin_mode",
- * "join_plain", "distinct_lds_probes", "gather_fused", "select_blocks", "select_dbg", "cursor_prefetch", "scan_select_fused", "scan_select_waves", "select_flag_stride"; "reset"
- * restores the defaults. */
+ * "join_plain", "distinct_lds_probes", "gather_fused", "select_blocks", "select_dbg", "cursor_prefetch", "scan_select_fused", "scan_select_waves", "select_flag_stride",
+ * "comm_same_stream", "scan_words_wt", and the one-launch ColumnarIndexScan's (k_cnf_select) "cnf_lookback" (0 auto,
+ * 1 chained, 2 polled), "cnf_flag_stride" (1 or 16), "cnf_blocks" (0: 1024), "cnf_store" (0 default, 1 plain,
+ * 2 write-through, 3 nontemporal); "reset" restores the defaults (MBX_<KNOB> environment values read at mbx_init). */
 int mbx_set_tuning(mbx_ctx *ctx, const char *knob, int64_t value);
 /* per-block wall_clock64() stamps (start, loads in, after the block barrier,
  * end) of the last compaction launched with select_dbg bit 3: 4 * nblocks
