@@ -187,6 +187,9 @@ def test_fused_interleaved_with_cnf_select(ctx):
             want = np.nonzero(np.isin(np.asarray(cols[2][2]), [3, 5]))[0]
             got, (v0,) = cur.next(max(1, n))
             assert np.array_equal(got, want) and np.array_equal(v0, c0[want]), n
+            # positions only: the polled look-back whatever the knobs (cnf_lookback auto)
+            got2, _ = ctx.cnf_cursor(t, [[bms[3], bms[5]]], []).next(max(1, n))
+            assert np.array_equal(got2, want), n
     del rng
 
 
@@ -231,3 +234,6 @@ def test_lookback_epoch_wrap(m, ctx, tune, lookback):
             want = np.nonzero(np.isin(np.asarray(cols[2][2]), [3, 5]))[0]
             got, (v0,) = cur.next(max(1, n))
             assert np.array_equal(got, want) and np.array_equal(v0, c0[want]), n
+            # positions only: the polled look-back whatever the knobs (cnf_lookback auto)
+            got2, _ = ctx.cnf_cursor(t, [[bms[3], bms[5]]], []).next(max(1, n))
+            assert np.array_equal(got2, want), n
