@@ -200,3 +200,8 @@ def free_port_local():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def test_unknown_config_exits_before_any_gpu_work():
+    r = run_bench(["--configs", "C2,C9"])
+    assert r.returncode == 2 and "C9" in r.stderr and not r.stdout.strip()
