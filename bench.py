@@ -1054,9 +1054,9 @@ def main():
             "configs": crecs,
             "cpu_baseline": None,
         }
-        if not args.no_cpu_baseline:
-            # rank 0, after the timed regions, over rank 0's shard (the other
-            # ranks wait at the closing barrier)
+        if not args.no_cpu_baseline and world == 1:
+            # rank 0 at N = 1 only, after the timed regions (at N > 1 the
+            # line carries null: the baseline is the single-GPU comparison)
             out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
         os.write(out_fd, (json.dumps(out) + "\n").encode())
 

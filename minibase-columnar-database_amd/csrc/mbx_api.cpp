@@ -105,8 +105,6 @@ static void tuning_from_env(MbxTuning& t) {
   t.cnf_flag_stride = env_knob("MBX_CNF_FLAG_STRIDE", 1) == kFlagStride ? kFlagStride : 1;
   t.cnf_lookback = (int32_t)env_knob("MBX_CNF_LOOKBACK", 0);
   t.cnf_store = (int32_t)env_knob("MBX_CNF_STORE", 0) & 3;
-  t.cnf_dyn = (int32_t)env_knob("MBX_CNF_DYN", 0);
-  if (t.cnf_dyn < 0) t.cnf_dyn = 0;
   if (t.cnf_lookback < 0 || t.cnf_lookback > 2) t.cnf_lookback = 0;
   t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
   if (t.select_blocks < 1) t.select_blocks = 1024;  // as mbx_set_tuning: never a zero / negative grid divisor
@@ -224,8 +222,8 @@ extern "C" int mbx_init(int32_t device, mbx_ctx** out) {
     if (e == hipSuccess) e = hipMalloc(&c->ticket, sizeof(uint32_t) * kTicketWords);
     if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(uint32_t) * kTicketWords);
     if (e == hipSuccess) e = hipHostMalloc(&c->pinned, 256, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipMalloc(&c->lookback, sizeof(int64_t) * kLookbackAlloc);
-    if (e == hipSuccess) e = hipMemset(c->lookback, 0, sizeof(int64_t) * kLookbackAlloc);
+    if (e == hipSuccess) e = hipMalloc(&c->lookback, sizeof(int64_t) * kLookbackWords);
+    if (e == hipSuccess) e = hipMemset(c->lookback, 0, sizeof(int64_t) * kLookbackWords);
     if (e != hipSuccess) {
       rc = fail(MBX_E_DEVICE, "mbx_init: %s", hipGetErrorString(e));
       break;
@@ -323,7 +321,6 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   else if (!strcmp(knob, "cnf_flag_stride")) t.cnf_flag_stride = v == kFlagStride ? kFlagStride : 1;
   else if (!strcmp(knob, "cnf_lookback")) t.cnf_lookback = v >= 0 && v <= 2 ? (int32_t)v : 0;
   else if (!strcmp(knob, "cnf_store")) t.cnf_store = v >= 0 && v <= 3 ? (int32_t)v : 0;
-  else if (!strcmp(knob, "cnf_dyn")) t.cnf_dyn = v < 0 ? 0 : (int32_t)v;
   else if (!strcmp(knob, "cursor_prefetch")) t.cursor_prefetch = v;
   else if (!strcmp(knob, "scan_select_fused")) t.scan_select_fused = v;
   else if (!strcmp(knob, "scan_select_waves")) t.scan_select_waves = v == 4 ? 4 : 16;
@@ -1759,7 +1756,6 @@ static CnfTune cnf_tune(const mbx_ctx* c) {
   k.flag_stride = c->tune.cnf_flag_stride;
   k.lookback = c->tune.cnf_lookback;
   k.store = c->tune.cnf_store;
-  k.dyn = c->tune.cnf_dyn;
   return k;
 }
 

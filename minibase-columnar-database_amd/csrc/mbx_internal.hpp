@@ -339,7 +339,7 @@ hipError_t launch_finalize(const Partial* partials, int64_t nblocks, int32_t agg
 // flag stride (1 or kFlagStride), look-back form (0 auto, 1 chained, 2
 // polled), output stores (0 default, 1 plain, 2 write-through, 3 nontemporal)
 struct CnfTune {
-  int32_t blocks = 0, flag_stride = 1, lookback = 0, store = 0, dyn = 0;
+  int32_t blocks = 0, flag_stride = 1, lookback = 0, store = 0;
 };
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
@@ -350,11 +350,6 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
 // counts may sit one per 128-byte line (kFlagStride words apart)
 constexpr int32_t kFlagStride = 16;
 constexpr int64_t kLookbackWords = 1 + kFlagStride * 1024;
-// the allocation: the look-back words, then (one 128-byte line each) the 8
-// segment counters of the dynamically scheduled k_cnf_select (0 between launches)
-constexpr int64_t kLookbackCounter = kLookbackWords;
-constexpr int kDynCounters = 8;
-constexpr int64_t kLookbackAlloc = kLookbackWords + 16 * kDynCounters;
 // BitSet + positions + COUNT of a plan in one launch (k_scan_select): plans of
 // 1..4 int literal terms on 4-byte columns, tables whose segments fit the
 // one-launch form (scan_select_fusable); L as for a kModeBitmap scan (its

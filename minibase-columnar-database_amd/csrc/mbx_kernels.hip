@@ -2031,101 +2031,6 @@ __global__ __launch_bounds__(64 * NW) void k_cnf_select(BitmapCnf C, const uint6
   }
 }
 
-// Dynamically scheduled ColumnarIndexScan (tuning cnf_dyn = S segments, an
-// A/B form): gridDim.x resident-sized blocks take segments 0..S-1 as they
-// become free, so blocks that start early (the ~4.6 us dispatch ramp) or
-// finish early take more of them.  Block b takes from counter x = b % 8
-// (one returning atomic saturates at ~88 takes per us, MI355X_MICROARCH.md
-// "dequeue"): its k-th take is segment 8k + x.  The smallest unfinished
-// segment is always taken by a running block or about to be (its counter's
-// earlier segments are all finished), so the chained look-back cannot
-// deadlock while every counter has a resident block.  Each block takes its
-// next id while it still works on the current segment.  Every block makes
-// exactly one failing take; the last take of a counter sets it back to 0.
-template <int G4, int NB, int NR>
-__global__ __launch_bounds__(kBlock) void k_cnf_select_dyn(BitmapCnf C, const uint64_t* __restrict__ del,
-                                                           int64_t nwords, uint64_t tail_mask, int64_t wps, int64_t S,
-                                                           int64_t* __restrict__ lb, int64_t row_offset,
-                                                           int64_t* __restrict__ ids, int64_t* __restrict__ total,
-                                                           Gather4 G, int32_t dbg) {
-  __shared__ int64_t wcount[kWaves];
-  __shared__ int64_t wpre[kWaves];
-  __shared__ uint16_t stage[kWaves][32 * 64];
-  __shared__ int64_t next_sh;
-  const int lane = threadIdx.x & 63;
-  const int wave = (int)uniform(threadIdx.x >> 6);
-  const uint32_t prev = (uint32_t)lb[0];
-  const int64_t epoch = prev >= 0x7fffffffu ? 1 : (int64_t)prev + 1;
-  const int x = (int)(blockIdx.x % kDynCounters);
-  unsigned long long* const ctr = reinterpret_cast<unsigned long long*>(lb + kLookbackCounter + 16 * x);
-  // this counter's segments and blocks: its last take returns their sum - 1
-  const uint64_t segs_x = S > x ? (uint64_t)((S - x + kDynCounters - 1) / kDynCounters) : 0;
-  const uint64_t blocks_x = (gridDim.x - x + kDynCounters - 1) / kDynCounters;
-  const uint64_t last_take = segs_x + blocks_x - 1;
-  auto take = [&]() -> int64_t {
-    const uint64_t v = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (v == last_take) __hip_atomic_store(ctr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (int64_t)v * kDynCounters + x;  // >= S: no segment left
-  };
-  if (threadIdx.x == 0) next_sh = take();
-  __syncthreads();
-  int64_t seg = next_sh;
-  auto word_at = [&](int64_t w) -> uint64_t {
-    uint64_t r = cnf_word(C, w);
-    if (del) r &= ~del[w];
-    if (w == nwords - 1) r &= tail_mask;
-    return r;
-  };
-  while (seg < S) {
-    __syncthreads();  // every wave has read next_sh (and left the previous segment's LDS)
-    int64_t nxt = 0;
-    if (threadIdx.x == 0) nxt = take();  // consumed at the end of this segment
-    const int64_t s0 = min(seg * wps, nwords);
-    const int64_t s1 = min(s0 + wps, nwords);
-    const int64_t per = (s1 - s0 + kWaves - 1) / kWaves;
-    const int64_t a0 = min(s0 + wave * per, s1);
-    const int64_t a1 = min(a0 + per, s1);
-    const bool cached = a1 - a0 <= 64 * NR;
-    uint64_t q[NR][NB];
-    uint64_t wr[NR];
-    int64_t c = 0;
-    if (cached) {
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int64_t w = a0 + r * 64 + lane;
-#pragma unroll
-        for (int k = 0; k < NB; ++k) q[r][k] = w < a1 ? C.bms[k][w] : 0ull;
-      }
-#pragma unroll
-      for (int r = 0; r < NR; ++r) {
-        const int64_t w = a0 + r * 64 + lane;
-        uint64_t x = ~0ull;
-        for (int cj = 0; cj < C.nconj; ++cj) {
-          uint64_t o = 0;
-#pragma unroll
-          for (int k = 0; k < NB; ++k)
-            if (k >= C.conj_off[cj] && k < C.conj_off[cj + 1]) o |= q[r][k];
-          x &= o;
-        }
-        if (del && w < a1) x &= ~del[w];
-        if (w == nwords - 1) x &= tail_mask;
-        wr[r] = w < a1 ? x : 0ull;
-        c += __popcll(wr[r]);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < NR; ++r) wr[r] = 0ull;
-      for (int64_t w = a0 + lane; w < a1; w += 64) c += __popcll(word_at(w));
-    }
-    select_tail<G4, Gather4, decltype(word_at), kWaves, NR>(wr, c, cached, a0, a1, word_at, lane, wave, lb, epoch,
-                                                             row_offset, ids, total, G, nullptr, dbg | 8, nullptr, 0,
-                                                             wcount, wpre, stage, nullptr, 1, seg, S);
-    if (threadIdx.x == 0) next_sh = nxt;
-    __syncthreads();
-    seg = next_sh;
-  }
-}
-
 constexpr int kDefaultU = 2;
 // measured on MI355X (profiles/r01/sweep3.log, C3 100M rows): U=2 tiles in
 // flight per wave with non-temporal loads, 4 blocks per CU, write-through
@@ -2693,7 +2598,6 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   // inclusive prefixes are 32-bit, so tables of >= 2^32 rows always poll.
   // lookback 1 / 2 (tuning cnf_lookback) force the chain / the polls, as
   // select_dbg bit 7 (MBX_SELECT_DBG=128) forces the polls.
-  const int nbm1 = c.conj_off[c.nconj];
   bool grouped = narrow;
   for (int j = 0; j < nproj; ++j) grouped = grouped && proj[j].gstride > 0;
   const bool chained = nbits < (int64_t(1) << 32) && !(dbg & 8) &&
@@ -2706,27 +2610,6 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
   const int64_t want = blocks > 0 ? ((dbg & 8) ? (blocks < kIncBase ? blocks : kIncBase)
                                                 : (blocks < kLookbackBlocks ? blocks : kLookbackBlocks))
                                    : kLookbackBlocks;
-  // dynamically scheduled form (tuning cnf_dyn = S segments; narrow, 1..4
-  // operands, < 2^32 rows): 1024 blocks take the S segments in grab order
-  if (knobs.dyn > 0 && narrow && nbm1 >= 1 && nbm1 <= 4 && nbits < (int64_t(1) << 32) && !stamps) {
-    const int64_t S = knobs.dyn < kIncBase ? knobs.dyn : kIncBase;
-    const int64_t wps = (nwords + S - 1) / S;
-    const int64_t nseg = (nwords + wps - 1) / wps;
-    const int64_t gb = nseg < kLookbackBlocks ? nseg : kLookbackBlocks;
-    const int32_t dd = dbg & ~8;
-#define MBX_CNF_DYN(NB, NR)                                                                                  \
-  hipLaunchKernelGGL((k_cnf_select_dyn<2, NB, NR>), dim3((unsigned)gb), dim3(kBlock), 0, s, c, deleted, nwords, \
-                     tail_mask_of(nbits), wps, nseg, lb, row_offset, ids, total, G, dd)
-    const bool two = (wps + kWaves - 1) / kWaves <= 2 * 64;
-    switch (nbm1) {
-      case 1: if (two) MBX_CNF_DYN(1, 2); else MBX_CNF_DYN(1, 8); break;
-      case 2: if (two) MBX_CNF_DYN(2, 2); else MBX_CNF_DYN(2, 8); break;
-      case 3: if (two) MBX_CNF_DYN(3, 2); else MBX_CNF_DYN(3, 8); break;
-      default: if (two) MBX_CNF_DYN(4, 2); else MBX_CNF_DYN(4, 8); break;
-    }
-#undef MBX_CNF_DYN
-    return hipGetLastError();
-  }
   const int32_t fs = (dbg & 8) || flag_stride != kFlagStride ? 1 : kFlagStride;
   const int64_t wpb = (nwords + want - 1) / want;
   const int64_t g = (nwords + wpb - 1) / wpb;

@@ -54,7 +54,6 @@ struct MbxTuning {
   int32_t join_plain = 0;         // MBX_JOIN_PLAIN: k_join_matrix instead of the fast form
   int32_t distinct_lds_probes = -1;  // MBX_DISTINCT_LDS_PROBES
   int32_t gather_fused = 1;       // MBX_GATHER_FUSED: 0 = compaction, then k_gather (two launches)
-  int32_t cnf_dyn = 0;            // MBX_CNF_DYN: k_cnf_select_dyn with this many segments (0: off; A/B form)
   int32_t cnf_store = 0;          // MBX_CNF_STORE: k_cnf_select outputs 0 default, 1 plain, 2 write-through, 3 nontemporal
   int32_t cnf_lookback = 0;       // MBX_CNF_LOOKBACK: k_cnf_select look-back 0 auto, 1 chained, 2 polled
   int32_t cnf_flag_stride = 1;    // MBX_CNF_FLAG_STRIDE: k_cnf_select's polled count flags 16 words apart, or 1

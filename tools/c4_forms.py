@@ -23,8 +23,6 @@ def main():
     ap.add_argument("--blocks", default="0", help="comma list of tuning cnf_blocks values (0: the default grid)")
     ap.add_argument("--positions-only", action="store_true", help="no projection: positions + COUNT only")
     ap.add_argument("--waves", default="4", help="comma list of tuning cnf_waves values (4 or 16)")
-    ap.add_argument("--dyn", default="0", help="comma list of tuning cnf_dyn values (0: static grid; S: S segments "
-                                               "taken dynamically)")
     ap.add_argument("--store", default="0",
                     help="comma list of tuning cnf_store values (0 default, 1 plain, 2 write-through, 3 nontemporal)")
     ap.add_argument("--lookback", default="default",
@@ -52,7 +50,7 @@ def main():
 
     LB = {"default": None, "chained": (1, 1), "poll16": (2, 16), "poll1": (2, 1)}  # (cnf_lookback, flag stride)
 
-    def run(n, group, timed, blocks=0, lookback="default", store=0, waves=4, dyn=0):
+    def run(n, group, timed, blocks=0, lookback="default", store=0, waves=4):
         cols, t, a, b = table(n)
         if group:
             ctx.group(t, [0, 1])
@@ -66,7 +64,6 @@ def main():
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
         ctx.set_tuning("cnf_blocks", blocks)
         ctx.set_tuning("cnf_store", store)
-        ctx.set_tuning("cnf_dyn", dyn)
         if waves != 4:
             ctx.set_tuning("cnf_waves", waves)  # round 5's 16-wave A/B (profiles/r05/p); knob since removed
         if LB[lookback]:
@@ -80,7 +77,7 @@ def main():
         ctx.sync()
         ok = (int(cnt.item()) == want and bool((ids[:want] == torch.nonzero(sel).flatten() + 192).all())
               and (args.positions_only or (bool((o0[:want] == c0[sel]).all()) and bool((o1[:want] == c1[sel]).all()))))
-        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "store": store, "waves": waves, "dyn": dyn, "positions_only": args.positions_only, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
+        res = {"rows": n, "group": group, "blocks": blocks, "lookback": lookback, "store": store, "waves": waves, "positions_only": args.positions_only, "gather_pair": os.environ.get("MBX_GATHER_PAIR", "1"),
                "selected": want, "ok": ok}
         if timed:
             ctx.graph_begin()
@@ -110,17 +107,15 @@ def main():
     lbs = args.lookback.split(",")
     sdbgs = [int(x) for x in args.store.split(",")]
     wavess = [int(x) for x in args.waves.split(",")]
-    dyns = [int(x) for x in args.dyn.split(",")]
     for n in map(int, args.check_rows.split(",")):
         for group in (True, False):
             for b in blocks:
                 for lb in lbs:
                     for sd in sdbgs:
                         for wv in wavess:
-                            for dy in dyns:
-                                r = run(n, group, False, b, lb, sd, wv, dy)
-                                bad += not r["ok"]
-                                print(json.dumps(r), flush=True)
+                            r = run(n, group, False, b, lb, sd, wv)
+                            bad += not r["ok"]
+                            print(json.dumps(r), flush=True)
     for n in map(int, args.rows.split(",")):
         for rep in range(2):
             for group in (True, False):
@@ -128,10 +123,9 @@ def main():
                     for lb in lbs:
                         for sd in sdbgs:
                             for wv in wavess:
-                                for dy in dyns:
-                                    r = run(n, group, True, b, lb, sd, wv, dy)
-                                    bad += not (r["ok"] and r["ok_after"])
-                                    print(json.dumps(r), flush=True)
+                                r = run(n, group, True, b, lb, sd, wv)
+                                bad += not (r["ok"] and r["ok_after"])
+                                print(json.dumps(r), flush=True)
     ctx.close()
     sys.exit(1 if bad else 0)
 
