@@ -16,6 +16,8 @@
 //                   per-XCD counters
 //   Steal   G x W : hybrid whose blocks move on to the other XCDs' counters
 //                   when their own is drained (at most 8 failing takes)
+//   u / plain / wseg : static with U tiles in flight / plain loads / one
+//                   contiguous sub-range per wave
 // and records per-block start / end stamps (wall_clock64, 100 MHz) of one
 // launch of each: the spread of end times by XCD and by eighth of blockIdx.
 // Findings (profiles/r05/t, 4 boxes): on an idle GPU all 1024 blocks start
@@ -25,7 +27,10 @@
 // 0.9 / 4 tiles flattens the blockIdx spread but wins <= 1 % on slow boxes
 // and loses 2-3 % on fast ones; Steal flattens the XCD spread too and is
 // 8-30 % slower (stolen chunks and per-take atomics cost more bandwidth than
-// the tail they recover); dyn is 4-22 % slower.  Standalone:
+// the tail they recover); dyn is 4-22 % slower.  Load shapes (ramp5): U = 3
+// / 4 tiles in flight within +-1 % of U = 2, plain loads 13 % slower than
+// nontemporal, one contiguous sub-range per wave (4 streams per block) 2-5 %
+// slower, 768 / 1280 / 1536 blocks 2-6 % slower.  Standalone:
 // hipcc -O3 --offload-arch=gfx950 -o tools/ramp_probe tools/ramp_probe.hip
 #include <hip/hip_runtime.h>
 
@@ -99,6 +104,47 @@ __device__ __forceinline__ void finish(const Args& A, v4i acc, int lane, int wav
     A.sink[blockIdx.x] = (uint32_t)r;
     if (A.stamps) A.stamps[2 * blockIdx.x + 1] = wall_clock64();
   }
+}
+
+// tiles first, first + stride, ... (< t1), U in flight; NT: nontemporal
+template <int U, bool NT>
+__device__ __forceinline__ v4i stream(const Args& A, int64_t first, int64_t t1, int64_t stride, int lane, v4i acc) {
+  for (int64_t base = first; base < t1; base += stride * U) {
+    v4i q[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int64_t t = base + (int64_t)u * stride;
+      const bool ok = t < t1;
+      t = ok ? t : base;
+      const int32_t* p0 = A.c0 + t * kTileRows + lane * 4;
+      const int32_t* p1 = A.c1 + t * kTileRows + lane * 4;
+      q[u][0] = NT ? ld(p0) : *(gv4i*)p0;
+      q[u][1] = NT ? ld(p1) : *(gv4i*)p1;
+      if (!ok) q[u][0] = q[u][1] = v4i{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= q[u][0] ^ q[u][1];
+  }
+  return acc;
+}
+
+// static segments, U tiles in flight (kind "u"), plain loads (kind "p"), or
+// one contiguous sub-range per wave (kind "w": 4 streams per block)
+template <int NW, int U, bool NT, bool WSEG>
+__global__ __launch_bounds__(64 * NW) void k_var(Args A) {
+  if (A.stamps && threadIdx.x == 0) A.stamps[2 * blockIdx.x] = wall_clock64();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t t0 = (int64_t)blockIdx.x * A.tpb;
+  const int64_t t1 = min(t0 + A.tpb, A.ntiles);
+  v4i acc;
+  if (WSEG) {
+    const int64_t per = (A.tpb + NW - 1) / NW;
+    const int64_t w0 = min(t0 + wave * per, t1);
+    acc = stream<U, NT>(A, w0, min(w0 + per, t1), 1, lane, v4i{0, 0, 0, 0});
+  } else {
+    acc = stream<U, NT>(A, t0 + wave, t1, NW, lane, v4i{0, 0, 0, 0});
+  }
+  finish<NW>(A, acc, lane, wave);
 }
 
 template <int NW>
@@ -266,6 +312,12 @@ static void launch(const Variant& v, Args A, hipStream_t s) {
   else if (v.kind[0] == 'x') L3(k_xcd);
   else if (v.kind[0] == 'h') L3(k_hybrid);
   else if (v.kind[0] == 'S') L3(k_steal);
+  else if (v.kind[0] == 'u' && v.chunk == 3) hipLaunchKernelGGL((k_var<4, 3, true, false>), g, b, 0, s, A);
+  else if (v.kind[0] == 'u' && v.chunk == 4) hipLaunchKernelGGL((k_var<4, 4, true, false>), g, b, 0, s, A);
+  else if (v.kind[0] == 'u') hipLaunchKernelGGL((k_var<4, 2, true, false>), g, b, 0, s, A);
+  else if (v.kind[0] == 'p') hipLaunchKernelGGL((k_var<4, 2, false, false>), g, b, 0, s, A);
+  else if (v.kind[0] == 'w' && v.chunk == 4) hipLaunchKernelGGL((k_var<4, 4, true, true>), g, b, 0, s, A);
+  else if (v.kind[0] == 'w') hipLaunchKernelGGL((k_var<4, 2, true, true>), g, b, 0, s, A);
   else L3(k_dyn);
   CHK(hipGetLastError());
 }
@@ -299,11 +351,10 @@ int main(int argc, char** argv) {
 
   // reference XOR of everything, from the static baseline
   std::vector<Variant> vs = {
-      {"static", 1024, 4, 0, 0.f},  {"hybrid", 1024, 4, 4, 0.90f}, {"Steal", 1024, 4, 4, 0.90f},
-      {"Steal", 1024, 4, 4, 0.80f}, {"Steal", 1024, 4, 8, 0.80f},  {"Steal", 1024, 4, 2, 0.90f},
-      {"Steal", 1024, 4, 4, 0.95f}, {"Steal", 1024, 4, 8, 0.70f},  {"Steal", 1024, 4, 16, 0.5f},
-      {"hybrid", 1024, 4, 4, 0.85f}, {"hybrid", 1024, 4, 6, 0.90f}, {"hybrid", 1024, 4, 4, 0.93f},
-      {"static", 1024, 4, 0, 0.f},  {"hybrid", 1024, 4, 4, 0.90f}, {"Steal", 1024, 4, 4, 0.90f},
+      {"static", 1024, 4, 0, 0.f}, {"u", 1024, 4, 2, 0.f},    {"u", 1024, 4, 3, 0.f},   {"u", 1024, 4, 4, 0.f},
+      {"plain", 1024, 4, 2, 0.f},  {"wseg", 1024, 4, 2, 0.f}, {"wseg", 1024, 4, 4, 0.f}, {"wseg", 512, 4, 2, 0.f},
+      {"wseg", 2048, 4, 2, 0.f},   {"u", 768, 4, 2, 0.f},     {"u", 1280, 4, 2, 0.f},   {"u", 1536, 4, 2, 0.f},
+      {"static", 1024, 4, 0, 0.f}, {"wseg", 1024, 4, 2, 0.f}, {"u", 1024, 4, 3, 0.f},
   };
   uint32_t want = 0;
   bool have_want = false;
