@@ -775,6 +775,27 @@ __device__ __forceinline__ void str16_cmp4(const uint32_t (&rows)[4][4], const u
   }
 }
 
+// A string term of the range-test body (IR = 2) over four zero-padded
+// 16-byte rows: rs[j] = the term holds for row j.  Each row is two 64-bit
+// big-endian keys (hi = bytes 0..7, lo = bytes 8..15), so its compareTo sign
+// against the literal (lhi, llo) comes from two 64-bit compares per key, and
+// the range test of that sign is the acceptance of lt / eq / gt (a_lt, a_eq,
+// a_gt: uniform, from the term's rlo / rspan / rneg) -- the same results as
+// str16_cmp4 + the range test, a third of the VALU instructions (C5's
+// aggregate scan was 62 % VALU-busy, profiles/r05/u).
+__device__ __forceinline__ void str16_accept4(const uint32_t (&rows)[4][4], uint64_t lhi, uint64_t llo, bool a_lt,
+                                              bool a_eq, bool a_gt, bool (&rs)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t hi = ((uint64_t)__builtin_bswap32(rows[j][0]) << 32) | __builtin_bswap32(rows[j][1]);
+    const uint64_t lo = ((uint64_t)__builtin_bswap32(rows[j][2]) << 32) | __builtin_bswap32(rows[j][3]);
+    const bool heq = hi == lhi;
+    const bool lt = hi < lhi || (heq && lo < llo);
+    const bool eq = heq && lo == llo;
+    rs[j] = lt ? a_lt : (eq ? a_eq : a_gt);
+  }
+}
+
 // per-tile body shared by every unroll depth: folds the CNF, applies deleted
 // rows and emits the requested output.
 // TQ > 0: the first TQ terms were hoisted into registers (th) before the
@@ -820,14 +841,16 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
         uint32_t lit[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) lit[i] = i < T.swords ? __builtin_bswap32(P->pool[T.soff + i]) : 0u;
-        int32_t c[4];
-        if (KS == 1 || lhs == K)
-          str16_cmp4(D.s[0], lit, c);
-        else
-          str16_cmp4(D.s[KS > 1 ? 1 : 0], lit, c);
+        const uint64_t lhi = ((uint64_t)lit[0] << 32) | lit[1], llo = ((uint64_t)lit[2] << 32) | lit[3];
+        // the range test of each compareTo sign, decided once per term
+        const bool a_lt = (0xffffffffu - lo <= span) != neg;
+        const bool a_eq = (0u - lo <= span) != neg;
+        const bool a_gt = (1u - lo <= span) != neg;
         bool rs[4];  // rs[j] is row 64j + lane (string slots load row-interleaved)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) rs[j] = (((uint32_t)c[j] - lo) <= span) != neg;
+        if (KS == 1 || lhs == K)
+          str16_accept4(D.s[0], lhi, llo, a_lt, a_eq, a_gt, rs);
+        else
+          str16_accept4(D.s[KS > 1 ? 1 : 0], lhi, llo, a_lt, a_eq, a_gt, rs);
         if (RI) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) r[j] = rs[j];
@@ -850,12 +873,18 @@ __device__ __forceinline__ void fast_tile(const ScanLaunch& L, const KPlan* __re
             for (int j = 0; j < 4; ++j) a[j] = D.v[s][j];
           }
         if (T.kind == kReal) {
-          const uint32_t below = T.req_below, own = T.conj_bit;
+          // PredEval's NaN reach, worked out only for a tile that holds a
+          // NaN (or a NaN literal): one compare per row otherwise
+          bool isn[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float f = __int_as_float(a[j]);
-            const bool reach = ((cb[j] & below) == below) && !(cb[j] & own);
-            nanr[j] = nanr[j] || (reach && (T.nan_lit || f != f));
+          for (int j = 0; j < 4; ++j) isn[j] = __int_as_float(a[j]) != __int_as_float(a[j]);
+          if (T.nan_lit || __ballot(isn[0] || isn[1] || isn[2] || isn[3]) != 0ull) {
+            const uint32_t below = T.req_below, own = T.conj_bit;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const bool reach = ((cb[j] & below) == below) && !(cb[j] & own);
+              nanr[j] = nanr[j] || (reach && (T.nan_lit || isn[j]));
+            }
           }
         }
         const uint32_t rm = T.rm31;

@@ -98,6 +98,29 @@ def test_string_literals(m, ctx, op):
             _both(m, ctx, t, ot, cnf)
 
 
+LONG_NAMES = ["Abcdefgh", "Abcdefgha", "AbcdefghZ", "Abcdefghé", "Abcdefghéa", "Abcdefghijklmnop",
+              "Abcdefghijklmnoo", "Abcdefghijklmnoq", "Abcdefghijklmno", "Abcdefgh\u0000x", "Abcdefg￿",
+              "Abcdefgi", "Abcdefg", "ébcdefghijklmno", "zzzzzzzzzzzzzzzz"]
+
+
+@pytest.mark.parametrize("op", [LT, LE, GT, GE, EQ, NE])
+def test_string_literals_past_the_first_eight_bytes(m, ctx, op):
+    """Rows and literals that agree on their first 8 bytes and differ after
+    them (the scan compares each 16-byte row as two 64-bit big-endian keys),
+    including bytes >= 0x80 (UTF-8 / U+FFFF) and an embedded U+0000."""
+    rng = np.random.Generator(np.random.PCG64(11))
+    n = 30_011
+    s = helpers.encode_strings([LONG_NAMES[i] for i in rng.integers(0, len(LONG_NAMES), n)], 16)
+    i0 = rng.integers(0, 1 << 20, n, dtype=np.int32)
+    cols = [(oracle.INTEGER, 4, i0), (oracle.STRING, 16, s)]
+    t = ctx.stage(cols)
+    ot = oracle.Table(cols)
+    for lit in LONG_NAMES + ["Abcdefghè", "Abcdefghijklmnoa", "Abcdefgh\u0000"]:
+        for cnf in ([[(op, ("sym", 2), ("str", lit))]], [[(op, ("str", lit), ("sym", 2))]],
+                    [[(op, ("sym", 2), ("str", lit))], [(LT, ("sym", 1), ("int", 1 << 19))]]):
+            _both(m, ctx, t, ot, cnf, agg_col=0)
+
+
 def test_c5_shaped_cnfs(m, ctx):
     """(c0 < 2^19) ^ (c1 >= 0.25) ^ (c2 >= "M") and random mixed CNFs of <= 4
     literal terms, with deleted rows"""
