@@ -1,13 +1,16 @@
 # Round 5 (u): C5's aggregate scan VALU load (SQ instruction counters beside
 # the kernel trace) -- run before and after the 64-bit-key string terms and
-# the NaN-free tile skip; with TESTS=1 the whole GPU suite runs first.
+# the NaN-free tile skip; with TESTS=1 the whole GPU suite runs first (or
+# TESTS='tests/a.py tests/b.py').
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r5_u}
 mkdir -p $OUT
-if [ "${TESTS:-0}" = 1 ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest_gpu.log; exit 1; }
+if [ "${TESTS:-0}" != 0 ]; then
+  # TESTS=1: the whole GPU suite; otherwise the test paths it names
+  T=tests; [ "$TESTS" != 1 ] && T="$TESTS"
+  timeout -k 10 600 python -u -m pytest $T -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 $OUT/pytest_gpu.log; exit 1; }
   tail -1 $OUT/pytest_gpu.log
 fi
 CMD="python3 bench.py --steps 5 --warmup 1 --kernel-graph 5 --no-cpu-baseline --configs C5"
