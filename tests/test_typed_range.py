@@ -121,6 +121,39 @@ def test_string_literals_past_the_first_eight_bytes(m, ctx, op):
             _both(m, ctx, t, ot, cnf, agg_col=0)
 
 
+@pytest.mark.parametrize("with_int", [False, True])
+def test_two_string_slots(m, ctx, with_int):
+    """Terms on both 16-byte string slots of a plan (the second slot's rows,
+    D.s[1]), with and without a 4-byte column: every operator, both literal
+    sides, one- and two-term conjuncts."""
+    rng = np.random.Generator(np.random.PCG64(12))
+    n = 20_011
+    a = helpers.encode_strings([LONG_NAMES[i] for i in rng.integers(0, len(LONG_NAMES), n)], 16)
+    b = helpers.encode_strings([LONG_NAMES[i] for i in rng.integers(0, len(LONG_NAMES), n)], 16)
+    cols = [(oracle.STRING, 16, a), (oracle.STRING, 16, b)]
+    if with_int:
+        cols.append((oracle.INTEGER, 4, rng.integers(0, 1 << 20, n, dtype=np.int32)))
+    t = ctx.stage(cols)
+    ot = oracle.Table(cols)
+    ops = [LT, LE, GT, GE, EQ, NE]
+    for k, op in enumerate(ops):
+        la, lb = LONG_NAMES[(3 * k) % len(LONG_NAMES)], LONG_NAMES[(3 * k + 7) % len(LONG_NAMES)]
+        cnfs = [[[(op, ("sym", 2), ("str", lb))]],
+                [[(op, ("str", la), ("sym", 1))], [(ops[(k + 1) % 6], ("sym", 2), ("str", lb))]],
+                [[(op, ("sym", 1), ("str", la)), (ops[(k + 3) % 6], ("str", lb), ("sym", 2))]]]
+        if with_int:
+            cnfs.append([[(op, ("sym", 2), ("str", lb))], [(LT, ("sym", 3), ("int", 1 << 19))]])
+        for cnf in cnfs:
+            want = oracle.filescan_count(ot, cnf)
+            plan = ctx.compile(t, cnf)
+            for knob in (2, 0):
+                ctx.set_tuning("scan_int_range", knob)
+                assert ctx.scan_count(plan) == want, (knob, cnf)
+                if with_int:
+                    _agg_eq(ctx.scan_aggregate(plan, 2), oracle.aggregate(ot, cnf, 2))
+            ctx.set_tuning("scan_int_range", 2)
+
+
 def test_c5_shaped_cnfs(m, ctx):
     """(c0 < 2^19) ^ (c1 >= 0.25) ^ (c2 >= "M") and random mixed CNFs of <= 4
     literal terms, with deleted rows"""
