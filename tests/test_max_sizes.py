@@ -48,6 +48,13 @@ def test_file_scan_past_2_31_rows(m, ctx):
     plan = ctx.compile(t, [[(m.mbx.LT, ("sym", 1), ("int", lit))]])
     want = int((c0 < lit).sum().item())
     assert ctx.scan_count(plan) == want
+    # COUNT / SUM / MIN / MAX of the selected rows (int64 sum)
+    sel = c0 < lit  # (boolean indexing of > 2^31 elements fails in torch: masked reductions instead)
+    agg = ctx.scan_aggregate(plan, 0)
+    assert agg == dict(count=want, sum=int(torch.where(sel, c0, 0).sum(dtype=torch.int64).item()),
+                       min=int(torch.where(sel, c0, (1 << 31) - 1).min().item()),
+                       max=int(torch.where(sel, c0, -(1 << 31)).max().item()))
+    del sel
     bm = ctx.bitmap_alloc(N31)
     ids = torch.zeros(want + 64, dtype=torch.int64, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
