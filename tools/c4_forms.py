@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--blocks", default="0", help="comma list of tuning cnf_blocks values (0: the default grid)")
     ap.add_argument("--positions-only", action="store_true", help="no projection: positions + COUNT only")
-    ap.add_argument("--waves", default="4", help="comma list of tuning cnf_waves values (4 or 16)")
+    ap.add_argument("--waves", default="4", help="4 (the 16-wave A/B knob cnf_waves was removed after round 5's profiles/r05/p)")
     ap.add_argument("--store", default="0",
                     help="comma list of tuning cnf_store values (0 default, 1 plain, 2 write-through, 3 nontemporal)")
     ap.add_argument("--lookback", default="default",
@@ -64,8 +64,8 @@ def main():
         cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
         ctx.set_tuning("cnf_blocks", blocks)
         ctx.set_tuning("cnf_store", store)
-        if waves != 4:
-            ctx.set_tuning("cnf_waves", waves)  # round 5's 16-wave A/B (profiles/r05/p); knob since removed
+        if waves != 4:  # round 5's 16-wave A/B (profiles/r05/p) ran a build with the cnf_waves knob, since removed
+            raise SystemExit("c4_forms: the library launches 4-wave blocks only (knob cnf_waves removed)")
         if LB[lookback]:
             ctx.set_tuning("cnf_lookback", LB[lookback][0])
             ctx.set_tuning("cnf_flag_stride", LB[lookback][1])

@@ -37,9 +37,9 @@ def main():
     o1 = torch.zeros(k + 64, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
     waves = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    if waves != 4:
-        ctx.set_tuning("cnf_waves", waves)  # round 5's 16-wave A/B (profiles/r05/p); knob since removed
-    nb = 1024 if waves == 4 else 256
+    if waves != 4:  # round 5's 16-wave A/B (profiles/r05/p) ran a build with the cnf_waves knob, since removed
+        raise SystemExit("c4_stamps: the library launches 4-wave blocks only (knob cnf_waves removed)")
+    nb = 1024
     for proj, outs in (([0, 1], [o0.data_ptr(), o1.data_ptr()]), ([], [])):
         for rep in range(3):
             ctx.set_tuning("select_dbg", 8)
@@ -49,8 +49,6 @@ def main():
             st = np.zeros(4 * nb, dtype=np.int64)
             M._chk(L.mbx_diag_select_stamps(ctx.h, st.ctypes.data, nb))
             ctx.set_tuning("select_dbg", 0)
-            if waves != 4:
-                ctx.set_tuning("cnf_waves", waves)
             st = st.reshape(nb, 4).astype(np.float64) / 100.0  # 100 MHz -> us
             st = st[st[:, 0] > 0]
             st -= st[:, 0].min()
