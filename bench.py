@@ -293,6 +293,8 @@ def make_parser():
     ap.add_argument("--c4-rows", type=int, default=100_000_000, help="C4 global rows (sharded)")
     ap.add_argument("--c5-rows", type=int, default=125_000_000, help="C5 rows per GPU")
     ap.add_argument("--no-strong", action="store_true", help="no strong sub-record at N > 1")
+    ap.add_argument("--no-bucketed", action="store_true",
+                    help="no bucketed sub-records at N > 1 (the COUNTs of each captured graph's steps in one all-reduce)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-launch", action="store_true",
@@ -492,7 +494,7 @@ def read_probe(H, table, reps=20):
     return {"best_gbs": res[best], "best": best, "gbs": res}
 
 
-def run_c3(H, args, cols, n, s, glob, label):
+def run_c3(H, args, cols, n, s, glob, label, bucket=None):
     """The C3 query over one rank's shard (`cols`, rows [s, s + n)), whose
     global COUNT over all ranks is `glob`: pre-check of one exchanged step,
     `args.steps` timed steps (graph replay), kernel time, every step's count
@@ -526,7 +528,7 @@ def run_c3(H, args, cols, n, s, glob, label):
     steps, warmup = args.steps, args.warmup
     counts = torch.zeros((steps + warmup, FW), dtype=torch.int64, device="cuda")
     base = counts.data_ptr()
-    B = max(1, args.exchange_bucket)
+    B = max(1, bucket if bucket is not None else args.exchange_bucket)
     gloo_works = []
 
     def scan(k, buf=base):
@@ -847,6 +849,23 @@ def config_c5(H, args):
     return rec
 
 
+def bucketed_form(args, world, exchange):
+    """The bucketed sub-records: only at N > 1 (the exchange is real), only
+    when the headline itself keeps one collective per query and graphs of
+    several steps are captured."""
+    return world > 1 and exchange and args.exchange_bucket == 1 and args.graph_steps > 1 and not args.no_bucketed
+
+
+def bucketed_record(r, rows):
+    """value / step / phases of a run_c3 result whose COUNTs of every
+    captured graph share one all-reduce (bucket_steps = graph steps)."""
+    return {"bucket_steps": r["B"], "value": rows / (r["ms_step"] * 1e-3), "unit": "rows/s",
+            "ms_per_step": r["ms_step"], "graph_steps": r["G"],
+            "phases_us": {"step_wall": r["ms_step"] * 1e3, "scan_kernel_max_over_ranks": r["kern_max"] * 1e3,
+                          "exchange_and_overlap": max(0.0, (r["ms_step"] - r["kern_max"]) * 1e3)},
+            "exchange": "one RCCL all-reduce of the COUNT frames of every bucket_steps queries"}
+
+
 def main():
     args = make_parser().parse_args()
     if args.gpus < 1:
@@ -946,6 +965,16 @@ def main():
     probe = read_probe(H, r3["table"]) if rank == 0 else None
     r3["table"].close()
     r3["plan"].close()
+    # at N > 1 with one collective per query (the headline, SURVEY 8(e)'s
+    # per-query t_reduce), the same steps again with the COUNTs of each
+    # captured graph's steps sharing ONE all-reduce: the throughput form for a
+    # stream of queries (xGMI collectives cost their latency, not their bytes)
+    bucketed = None
+    if bucketed_form(args, world, exchange):
+        rb = run_c3(H, args, cols, n, s, glob, "C3 bucketed", bucket=args.graph_steps)
+        rb["table"].close()
+        rb["plan"].close()
+        bucketed = bucketed_record(rb, n_global)
     del cols
     torch.cuda.empty_cache()
 
@@ -958,13 +987,20 @@ def main():
         rs = run_c3(H, args, scols, se - ss, ss, sglob, "C3 strong")
         rs["table"].close()
         rs["plan"].close()
+        sb = None
+        if bucketed_form(args, world, exchange):
+            rsb = run_c3(H, args, scols, se - ss, ss, sglob, "C3 strong bucketed", bucket=args.graph_steps)
+            rsb["table"].close()
+            rsb["plan"].close()
+            sb = bucketed_record(rsb, args.rows)
         del scols
         torch.cuda.empty_cache()
         strong = {"rows": args.rows, "rows_per_gpu_rank0": se - ss if rank == 0 else None,
                   "value": args.rows / (rs["ms_step"] * 1e-3), "unit": "rows/s", "ms_per_step": rs["ms_step"],
                   "phases_us": {"step_wall": rs["ms_step"] * 1e3, "scan_kernel_max_over_ranks": rs["kern_max"] * 1e3,
                                 "exchange_and_overlap": max(0.0, (rs["ms_step"] - rs["kern_max"]) * 1e3)},
-                  "count": "frame" if rs["frames"] else "finalize", "graph_steps": rs["G"], "pre_check": "ok"}
+                  "count": "frame" if rs["frames"] else "finalize", "graph_steps": rs["G"], "pre_check": "ok",
+                  "bucketed": sb}
         if rank == 0:
             strong["rows_per_gpu_rank0"] = se - ss
 
@@ -1050,6 +1086,7 @@ def main():
                 "frac_of_measured_read_peak": achieved / probe["best_gbs"],
                 "read_probe": probe,
             },
+            "bucketed": bucketed,
             "strong": strong,
             "configs": crecs,
             "cpu_baseline": None,

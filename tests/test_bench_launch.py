@@ -109,6 +109,24 @@ def test_default_run_adds_every_config_record():
         assert r["traffic"] == t and r["traffic_over_algorithmic"] == t / 1000
 
 
+def test_bucketed_sub_records_only_beside_a_per_query_headline():
+    """At N > 1 the line adds `bucketed` (and strong.bucketed): the same steps
+    with each captured graph's COUNTs in one all-reduce; never at N = 1, never
+    when the headline is bucketed itself, and --no-bucketed turns it off."""
+    b = _bench_module()
+    p = b.make_parser()
+    a = p.parse_args([])
+    assert a.exchange_bucket == 1 and a.graph_steps > 1
+    assert b.bucketed_form(a, 2, True) and b.bucketed_form(a, 8, True)
+    assert not b.bucketed_form(a, 1, False) and not b.bucketed_form(a, 1, True)
+    assert not b.bucketed_form(p.parse_args(["--exchange-bucket", "20"]), 8, True)
+    assert not b.bucketed_form(p.parse_args(["--graph-steps", "0"]), 8, True)
+    assert not b.bucketed_form(p.parse_args(["--no-bucketed"]), 8, True)
+    r = b.bucketed_record(dict(B=20, ms_step=0.125, kern_max=0.118, G=20), 800_000_000)
+    assert r["bucket_steps"] == 20 and abs(r["value"] - 800_000_000 / 125e-6) < 1
+    assert abs(r["phases_us"]["exchange_and_overlap"] - 7.0) < 1e-9
+
+
 def _frame(count, arrivals, nan=0, slots=32):
     import numpy as np
     f = np.zeros(512, dtype=np.int64)
