@@ -297,6 +297,9 @@ def make_parser():
                     help="no bucketed sub-records at N > 1 (the COUNTs of each captured graph's steps in one all-reduce)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--watchdog", type=float, default=480.0,
+                    help="seconds after which a still-running rank prints every thread's traceback and exits 1 "
+                         "(a hung collective fails with its place named, inside the driver's budget); 0: off")
     ap.add_argument("--dry-launch", action="store_true",
                     help="ranks print their rank env as JSON and exit before importing torch (launcher test)")
     return ap
@@ -893,6 +896,9 @@ def main():
         print(f"bench: unknown config(s) {bad}", file=sys.stderr)
         sys.exit(2)
     out_fd = quiet_stdout()
+    if args.watchdog > 0:
+        import faulthandler
+        faulthandler.dump_traceback_later(args.watchdog, exit=True)
 
     import torch
     import torch.distributed as dist

@@ -109,6 +109,18 @@ def test_default_run_adds_every_config_record():
         assert r["traffic"] == t and r["traffic_over_algorithmic"] == t / 1000
 
 
+def test_watchdog_names_a_hang_and_exits():
+    """A rank still running after --watchdog seconds prints every thread's
+    traceback and exits 1 (faulthandler), so a hung collective at N > 1 fails
+    inside the driver's budget with its place named."""
+    b = _bench_module()
+    assert 0 < b.make_parser().parse_args([]).watchdog < 600
+    code = ("import faulthandler, time; faulthandler.dump_traceback_later(0.5, exit=True); "
+            "time.sleep(30)")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and ("sleep" in r.stderr or "Thread" in r.stderr), r.stderr
+
+
 def test_bucketed_sub_records_only_beside_a_per_query_headline():
     """At N > 1 the line adds `bucketed` (and strong.bucketed): the same steps
     with each captured graph's COUNTs in one all-reduce; never at N = 1, never
