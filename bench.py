@@ -859,14 +859,14 @@ def bucketed_form(args, world, exchange):
     return world > 1 and exchange and args.exchange_bucket == 1 and args.graph_steps > 1 and not args.no_bucketed
 
 
-def bucketed_record(r, rows):
+def bucketed_record(r, rows, exchange="one RCCL all-reduce of the COUNT frames of every bucket_steps queries"):
     """value / step / phases of a run_c3 result whose COUNTs of every
     captured graph share one all-reduce (bucket_steps = graph steps)."""
     return {"bucket_steps": r["B"], "value": rows / (r["ms_step"] * 1e-3), "unit": "rows/s",
             "ms_per_step": r["ms_step"], "graph_steps": r["G"],
             "phases_us": {"step_wall": r["ms_step"] * 1e3, "scan_kernel_max_over_ranks": r["kern_max"] * 1e3,
                           "exchange_and_overlap": max(0.0, (r["ms_step"] - r["kern_max"]) * 1e3)},
-            "exchange": "one RCCL all-reduce of the COUNT frames of every bucket_steps queries"}
+            "exchange": exchange}
 
 
 def main():
@@ -980,7 +980,8 @@ def main():
         rb = run_c3(H, args, cols, n, s, glob, "C3 bucketed", bucket=args.graph_steps)
         rb["table"].close()
         rb["plan"].close()
-        bucketed = bucketed_record(rb, n_global)
+        bucketed = bucketed_record(rb, n_global, exchange_name(
+            H, "one RCCL all-reduce of the COUNT frames of every bucket_steps queries (libmbx mbx_comm)"))
     del cols
     torch.cuda.empty_cache()
 
@@ -998,7 +999,8 @@ def main():
             rsb = run_c3(H, args, scols, se - ss, ss, sglob, "C3 strong bucketed", bucket=args.graph_steps)
             rsb["table"].close()
             rsb["plan"].close()
-            sb = bucketed_record(rsb, args.rows)
+            sb = bucketed_record(rsb, args.rows, exchange_name(
+                H, "one RCCL all-reduce of the COUNT frames of every bucket_steps queries (libmbx mbx_comm)"))
         del scols
         torch.cuda.empty_cache()
         strong = {"rows": args.rows, "rows_per_gpu_rank0": se - ss if rank == 0 else None,
