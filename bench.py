@@ -22,6 +22,9 @@ headline reports weak scaling:
       same run also times the STRONG form and reports it as the `strong`
       sub-record: the metric's ONE 100M-row table in N 64-aligned shards
       (mbx_shard_bounds), with its phases (scan max over ranks, exchange).
+      Both forms are also timed with the COUNTs of each captured graph's
+      steps in ONE all-reduce (`bucketed`, `strong.bucketed`: the throughput
+      form for a stream of queries; --no-bucketed drops them).
   --scaling strong: the headline itself is the strong form.
 The timed steps replay HIP graphs (mbx_graph_*) of --graph-steps captured
 steps (scans + their exchange), so small shards do not wait on the host.
@@ -49,7 +52,9 @@ heap C3 leaves, profiles/r05/m):
       at N > 1 + the RCCL all-gather of the 48-byte records + the device
       rank-ordered fold (k_fold_agg)
 Each is checked against torch reductions of the same device data before
-and after its timing.  stdout carries only the JSON line.
+and after its timing.  stdout carries only the JSON line.  A rank still
+running after --watchdog seconds (480) prints its threads' tracebacks and
+exits 1.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak] [--configs C2,C4,C5|none]
 
