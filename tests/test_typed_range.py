@@ -121,6 +121,41 @@ def test_string_literals_past_the_first_eight_bytes(m, ctx, op):
             _both(m, ctx, t, ot, cnf, agg_col=0)
 
 
+def _random_names(rng, k):
+    """k random strings whose modified UTF-8 fits 16 bytes, drawn from ASCII,
+    2- and 3-byte characters, U+0000 and supplementary characters (surrogate
+    pairs: 6 bytes), many sharing long prefixes."""
+    alphabet = ["a", "b", "M", "z", "é", "ÿ", "Ā", "中", "￿", "\u0000", "\U0001F600"]
+    prefixes = ["", "Abcdefgh", "Abcdefg", "M", "Maine"]
+    out = []
+    while len(out) < k:
+        s = prefixes[int(rng.integers(0, len(prefixes)))]
+        for _ in range(int(rng.integers(0, 12))):
+            s += alphabet[int(rng.integers(0, len(alphabet)))]
+        if len(oracle.java_mutf8(s)) <= 16:
+            out.append(s)
+    return out
+
+
+def test_string_fuzz(m, ctx):
+    """Random rows and literals (ragged lengths, bytes >= 0x80, U+0000,
+    supplementary characters, shared prefixes): every operator, both literal
+    sides, the range body (knob 2) and the branchy body (knob 0) vs the
+    oracle."""
+    rng = np.random.Generator(np.random.PCG64(13))
+    pool = _random_names(rng, 300)
+    n = 30_007
+    s = helpers.encode_strings([pool[i] for i in rng.integers(0, len(pool), n)], 16)
+    cols = [(oracle.INTEGER, 4, rng.integers(0, 1 << 20, n, dtype=np.int32)), (oracle.STRING, 16, s)]
+    t = ctx.stage(cols)
+    ot = oracle.Table(cols)
+    lits = [pool[i] for i in rng.integers(0, len(pool), 10)] + _random_names(rng, 10)
+    for k, lit in enumerate(lits):
+        for op in [LT, LE, GT, GE, EQ, NE]:
+            cnf = [[(op, ("sym", 2), ("str", lit))]] if k % 2 == 0 else [[(op, ("str", lit), ("sym", 2))]]
+            _both(m, ctx, t, ot, cnf, agg_col=0)
+
+
 @pytest.mark.parametrize("with_int", [False, True])
 def test_two_string_slots(m, ctx, with_int):
     """Terms on both 16-byte string slots of a plan (the second slot's rows,
