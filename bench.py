@@ -53,8 +53,8 @@ heap C3 leaves, profiles/r05/m):
       rank-ordered fold (k_fold_agg)
 Each is checked against torch reductions of the same device data before
 and after its timing.  stdout carries only the JSON line.  A rank still
-running after --watchdog seconds (480) prints its threads' tracebacks and
-exits 1.
+running --watchdog seconds (420) after its imports prints its threads'
+tracebacks and exits 1.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak] [--configs C2,C4,C5|none]
 
@@ -302,7 +302,7 @@ def make_parser():
                     help="no bucketed sub-records at N > 1 (the COUNTs of each captured graph's steps in one all-reduce)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--watchdog", type=float, default=480.0,
+    ap.add_argument("--watchdog", type=float, default=420.0,
                     help="seconds after which a still-running rank prints every thread's traceback and exits 1 "
                          "(a hung collective fails with its place named, inside the driver's budget); 0: off")
     ap.add_argument("--dry-launch", action="store_true",
@@ -901,14 +901,15 @@ def main():
         print(f"bench: unknown config(s) {bad}", file=sys.stderr)
         sys.exit(2)
     out_fd = quiet_stdout()
-    if args.watchdog > 0:
-        import faulthandler
-        faulthandler.dump_traceback_later(args.watchdog, exit=True)
 
     import torch
     import torch.distributed as dist
 
     import mbx_pkg
+
+    if args.watchdog > 0:  # armed after the imports (a cold box's first `import torch` takes minutes)
+        import faulthandler
+        faulthandler.dump_traceback_later(args.watchdog, exit=True)
 
     same_device = os.environ.get("MBX_BENCH_SAME_DEVICE") == "1"
     device = 0 if same_device else local_rank
