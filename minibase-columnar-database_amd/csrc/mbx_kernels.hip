@@ -2414,7 +2414,14 @@ static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
   constexpr int TQ = KS == 0 ? kHoistTerms : 0;
   // one 4-byte column: 4 tiles in flight per wave (the same bytes in flight as
   // two columns at U=2); 100M rows: COUNT 69.7 -> 67.3 us, BitSet 87.5 -> 81.0 us
-  constexpr int kU = K == 1 && KS == 0 ? 4 : kDefaultU;
+  // two-column COUNT scans (C3): 3 tiles in flight per wave -- 117.4 vs
+  // 117.8-119.4 us (U = 2) and 120.3-120.7 (U = 4) at 100M rows, alternating
+  // A/B builds on one box (profiles/r05/ak; MBX_SCAN_U2 overrides it in
+  // tools/build_variant.sh builds)
+#ifndef MBX_SCAN_U2
+#define MBX_SCAN_U2 3
+#endif
+  constexpr int kU = K == 1 && KS == 0 ? 4 : (K == 2 && KS == 0 && MODE == kModeCount ? MBX_SCAN_U2 : kDefaultU);
   const unsigned lds = L.sink_lds ? (unsigned)(L.tiles_per_block * kWordsPerTile * sizeof(uint64_t)) : 0u;
   // int literal terms as branch-free range tests
   if constexpr (KS == 0) {
