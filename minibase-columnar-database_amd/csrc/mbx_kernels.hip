@@ -2421,7 +2421,13 @@ static void prod_launch(const ScanLaunch& L, dim3 grid, hipStream_t s) {
 #ifndef MBX_SCAN_U2
 #define MBX_SCAN_U2 3
 #endif
-  constexpr int kU = K == 1 && KS == 0 ? 4 : (K == 2 && KS == 0 && MODE == kModeCount ? MBX_SCAN_U2 : kDefaultU);
+  // MBX_SCAN_U_AGG (A/B builds): tiles in flight for aggregate scans
+#ifndef MBX_SCAN_U_AGG
+#define MBX_SCAN_U_AGG kDefaultU
+#endif
+  constexpr int kU = K == 1 && KS == 0 ? 4
+                     : (K == 2 && KS == 0 && MODE == kModeCount ? MBX_SCAN_U2
+                                                                : (MODE == kModeAgg ? MBX_SCAN_U_AGG : kDefaultU));
   const unsigned lds = L.sink_lds ? (unsigned)(L.tiles_per_block * kWordsPerTile * sizeof(uint64_t)) : 0u;
   // int literal terms as branch-free range tests
   if constexpr (KS == 0) {
