@@ -94,21 +94,20 @@ CONFIG_KEYS = ("workload", "rows", "rows_per_gpu", "gpus", "selected", "ms_per_q
                "exchange", "pre_check", "timing", "traffic")
 
 
-def cpu_baseline(rows, min_seconds):
+def cpu_baseline(host_cols, gpu_count, min_seconds):
     """The oracle (C restatement of ColumnarFileScan + PredEval) timed on the
-    same workload definition: a host copy of the C3 table (numpy PCG64, seeds
-    42..45), full passes until min_seconds elapsed -- row ranges split over the
-    host cores this process may use (OMP_NUM_THREADS, 16 per GPU on the box;
-    SURVEY 8(d)(ii)), each range evaluated row by row exactly like the
-    single-thread oracle."""
+    GPU run's own C3 table: `host_cols` are the 4 device columns copied to
+    host memory after the timed regions (the same arrays), full
+    passes until min_seconds elapsed -- row ranges split over the host cores
+    this process may use (OMP_NUM_THREADS, 16 per GPU on the box; SURVEY
+    8(d)(ii)), each range evaluated row by row exactly like the single-thread
+    oracle.  Its COUNT must equal the GPU's verified COUNT of that table."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import helpers
     import oracle
 
+    rows = len(host_cols[0])
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    cols = [(oracle.INTEGER, 4, c) for c in helpers.synthetic_int_table(rows, 4, 1 << 20, 42)]
-    t = oracle.Table(cols)
+    t = oracle.Table([(oracle.INTEGER, 4, c) for c in host_cols])
     cnf = [[(oracle.LT, ("sym", 1), ("int", THRESH))], [(oracle.GE, ("sym", 2), ("int", THRESH))]]
     t0 = time.perf_counter()
     count1 = oracle.filescan_count(t, cnf)          # one single-thread pass, for the record
@@ -119,14 +118,20 @@ def cpu_baseline(rows, min_seconds):
         count = oracle.filescan_count_mt(t, cnf, threads)
         elapsed += time.perf_counter() - t0
         passes += 1
-    assert count == count1
+    if not (count == count1 == gpu_count):
+        print(f"bench: cpu_baseline COUNT {count1} / {count} (1 / {threads} threads) != GPU COUNT {gpu_count}",
+              file=sys.stderr, flush=True)
+        os._exit(5)
     return {
         "value": rows * passes / elapsed,
         "unit": "rows/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{passes} full pass(es) over a {rows:,}-row 4xint32 host table (same C3 predicate, count {count}); "
-                  f"oracle/oracle.c orc_filescan_count_mt, {threads} OpenMP threads, {elapsed:.1f} s total; "
+        "count": count,
+        "count_equals_gpu": True,
+        "sample": f"{passes} full pass(es) over the GPU run's own {rows:,}-row 4xint32 C3 table, copied from HBM "
+                  f"after timing (same predicate; COUNT {count} = the GPU's verified COUNT); oracle/oracle.c "
+                  f"orc_filescan_count_mt, {threads} OpenMP threads, {elapsed:.1f} s total; "
                   f"single thread: {rows / one:.3g} rows/s",
     }
 
@@ -165,20 +170,54 @@ def free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n, argv, dry):
-    """Start n rank processes of this script (one per GPU; none of this
-    process's code has touched a GPU), relay rank 0's stdout (every rank's
-    with --dry-launch) and return the exit status: 0, or the first failing
-    rank's status, after the remaining ranks were stopped by their PIDs."""
+# ---------------------------------------------------------------- launchers
+# Neither launcher touches a GPU: they only start rank ("worker") processes,
+# watch their exit codes and, once, start fresh ones.  A worker that finds the
+# first replay of a captured graph (the timed steps' form: scans + their RCCL
+# exchange) hung or wrong exits GRAPH_EXIT after writing a one-line reason to
+# $MBX_BENCH_STATUS; the launcher then stops every rank and starts fresh rank
+# processes ONCE with --graph-steps 0 (every step eager, the same exchange
+# issued step by step), and $MBX_BENCH_FALLBACK carries the reason into the
+# line's `exchange_form`.  Any other failure is final.
+
+GRAPH_EXIT = 4
+KILLED = -9
+
+
+def fallback_argv(argv):
+    """the relaunch's arguments: the same, every step eager"""
+    return list(argv) + ["--graph-steps", "0"]
+
+
+def read_reason(path):
+    try:
+        with open(path) as f:
+            return f.read().strip().splitlines()[0][:300]
+    except (OSError, IndexError):
+        return "no reason recorded"
+
+
+def worker_cmd(argv):
+    return [sys.executable, os.path.abspath(__file__)] + list(argv)
+
+
+def run_local_attempt(n, argv, env_extra, status_dir, attempt):
+    """n worker processes on this node; returns (status, failing rank): 0 or
+    the first failing rank's exit status, the others stopped by PID.  Rank
+    0's stdout is this process's (the JSON line), the others' go to stderr
+    (--dry-launch: every rank's to stdout)."""
     import subprocess
     port = free_port()
+    dry = "--dry-launch" in argv
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        out = subprocess.PIPE if (r == 0 or dry) else sys.stderr
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, stdout=out))
-    status = 0
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MBX_BENCH_WORKER="1",
+                   MBX_BENCH_STATUS=os.path.join(status_dir, f"a{attempt}_rank{r}.txt"), **env_extra)
+        out = None if (r == 0 or dry) else sys.stderr
+        procs.append(subprocess.Popen(worker_cmd(argv), env=env, stdout=out))
+    status, bad = 0, None
+    codes = {}
     live = list(procs)
     while live:
         for p in list(live):
@@ -186,19 +225,197 @@ def launch_ranks(n, argv, dry):
             if rc is None:
                 continue
             live.remove(p)
+            codes[procs.index(p)] = rc
             if rc != 0 and status == 0:
                 status = rc if rc > 0 else 128 - rc
-                print(f"bench launcher: rank {procs.index(p)} exited with {rc}; stopping the others",
-                      file=sys.stderr)
+                bad = procs.index(p)
+                print(f"bench launcher: rank {bad} exited with {rc}; stopping the others", file=sys.stderr)
                 for q in live:
                     q.kill()
         time.sleep(0.05)
-    for p in procs:
-        if p.stdout is not None:
-            data = p.stdout.read()
-            if data:
-                os.write(1, data)
-    return status
+    # a graph-phase failure wins over the peers it left failing in a collective
+    graph = [r for r in sorted(codes) if codes[r] == GRAPH_EXIT]
+    if graph:
+        return GRAPH_EXIT, graph[0]
+    return status, bad
+
+
+def launch_ranks(n, argv):
+    """this node's N ranks (WORLD_SIZE unset, --gpus N > 1)"""
+    import shutil
+    import tempfile
+    status_dir = tempfile.mkdtemp(prefix="mbx_bench_")
+    try:
+        status, bad = run_local_attempt(n, argv, {}, status_dir, 0)
+        if status == GRAPH_EXIT:
+            reason = read_reason(os.path.join(status_dir, f"a0_rank{bad}.txt"))
+            print(f"bench launcher: graph replay failed on rank {bad} ({reason}); fresh ranks, eager steps",
+                  file=sys.stderr, flush=True)
+            status, _ = run_local_attempt(n, fallback_argv(argv), {"MBX_BENCH_FALLBACK": f"rank {bad}: {reason}"},
+                                          status_dir, 1)
+        return status
+    finally:
+        shutil.rmtree(status_dir, ignore_errors=True)
+
+
+def supervise_rank(argv):
+    """Under an external launcher (torch.distributed.run: WORLD_SIZE, RANK,
+    MASTER_* set), this process supervises ONE worker: it starts it, shares
+    its exit code with the other ranks' supervisors through a TCPStore (torch
+    run's own agent store when TORCHELASTIC_USE_AGENT_STORE, else one hosted by
+    rank 0), stops its worker when another rank's worker failed, and on a
+    graph-phase failure anywhere every supervisor starts one fresh worker with
+    --graph-steps 0.  Workers rendezvous on a fresh port per attempt (rank 0's
+    worker hosts that store).  Returns the exit status."""
+    import datetime
+    import shutil
+    import subprocess
+    import tempfile
+
+    import torch.distributed as dist  # host side only: no GPU is touched here
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
+    store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"), int(os.environ["MASTER_PORT"]), world,
+                          is_master=(rank == 0 and not agent), timeout=datetime.timedelta(seconds=600),
+                          wait_for_workers=False)
+    run_id = os.environ.get("TORCHELASTIC_RUN_ID", "") + os.environ.get("TORCHELASTIC_RESTART_COUNT", "")
+    key = lambda a, r: f"mbx_bench/{run_id}/a{a}/rank{r}"  # noqa: E731
+    status_dir = tempfile.mkdtemp(prefix="mbx_bench_")
+    extra, args_now = {}, list(argv)
+    try:
+        for attempt in (0, 1):
+            if rank == 0:
+                store.set(f"mbx_bench/{run_id}/a{attempt}/port", str(free_port()))
+            port = store.get(f"mbx_bench/{run_id}/a{attempt}/port").decode()
+            env = dict(os.environ, MASTER_PORT=port, MBX_BENCH_WORKER="1",
+                       MBX_BENCH_STATUS=os.path.join(status_dir, f"a{attempt}.txt"), **extra)
+            env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the workers' store is hosted by rank 0's worker
+            p = subprocess.Popen(worker_cmd(args_now), env=env, stdout=None if rank == 0 else sys.stderr)
+            peers = [key(attempt, r) for r in range(world) if r != rank]
+            killed = False
+            while p.poll() is None:
+                for k in peers:  # a peer's worker already failed: this one would wait on it
+                    if store.check([k]) and not store.get(k).decode().startswith("0|"):
+                        p.kill()
+                        killed = True
+                        break
+                time.sleep(0.1)
+            rc = p.wait()
+            rc = KILLED if killed else rc
+            reason = read_reason(env["MBX_BENCH_STATUS"]) if rc == GRAPH_EXIT else ""
+            store.set(key(attempt, rank), f"{rc}|{reason}")
+            deadline = time.time() + 600
+            while not store.check([key(attempt, r) for r in range(world)]):
+                if time.time() > deadline:
+                    print(f"bench supervisor {rank}: peers never reported", file=sys.stderr)
+                    return 1
+                time.sleep(0.1)
+            codes = []
+            for r in range(world):
+                c, _, why = store.get(key(attempt, r)).decode().partition("|")
+                codes.append((r, int(c), why))
+            graph = [(r, why) for r, c, why in codes if c == GRAPH_EXIT]
+            if graph and attempt == 0:
+                r0, why = graph[0]
+                if rank == 0:
+                    print(f"bench supervisor: graph replay failed on rank {r0} ({why}); fresh workers, eager steps",
+                          file=sys.stderr, flush=True)
+                extra = {"MBX_BENCH_FALLBACK": f"rank {r0}: {why}"}
+                args_now = fallback_argv(argv)
+                continue
+            fails = [c for _, c, _ in codes if c not in (0, KILLED)]
+            if fails:
+                return fails[0] if fails[0] > 0 else 128 - fails[0]
+            return 1 if any(c == KILLED for _, c, _ in codes) else 0
+        return 1
+    finally:
+        shutil.rmtree(status_dir, ignore_errors=True)
+
+
+def fake_worker(args, world, rank):
+    """MBX_BENCH_FAKE=graph:R (launcher tests, no GPU): rank R's first attempt
+    fails its graph phase, the other ranks wait as if inside a collective; the
+    eager relaunch prints a line as rank 0 would."""
+    mode, _, who = os.environ["MBX_BENCH_FAKE"].partition(":")
+    fallback = os.environ.get("MBX_BENCH_FALLBACK")
+    if mode == "graph" and args.graph_steps and not fallback:
+        if str(rank) == who:
+            time.sleep(0.5)
+            graph_failed("C3: first replay of the captured graphs did not finish within 60 s (fake)")
+        time.sleep(60)
+        sys.exit(1)
+    if mode == "fail":  # any other failure is final
+        time.sleep(0.5)
+        if str(rank) == who:
+            sys.exit(7)
+        time.sleep(60)
+        sys.exit(1)
+    if rank == 0:
+        print(json.dumps({"fake": True, "n_gpus": world, "graph_steps": args.graph_steps,
+                          "exchange_form": exchange_form(args.graph_steps, fallback)}), flush=True)
+
+
+def graph_failed(reason):
+    """a graph-phase failure: the reason into $MBX_BENCH_STATUS, exit GRAPH_EXIT"""
+    path = os.environ.get("MBX_BENCH_STATUS")
+    if path:
+        try:
+            with open(path, "w") as f:
+                f.write(reason + "\n")
+        except OSError:
+            pass
+    print(f"bench: graph phase failed: {reason}", file=sys.stderr, flush=True)
+    sys.stderr.flush()
+    os._exit(GRAPH_EXIT)
+
+
+def exchange_form(graph_steps, fallback):
+    if fallback:
+        return f"eager (graph replay failed: {fallback})"
+    return f"HIP graphs of {graph_steps} steps (first replay verified)" if graph_steps else "eager"
+
+
+class PhaseClock:
+    """Per-phase deadlines: a daemon thread that, when the armed phase outlives
+    its budget, prints the phase and every thread's traceback and exits with
+    the phase's code (GRAPH_EXIT for a graph replay, 1 otherwise).  Ctypes and
+    torch calls release the GIL while they wait, so the thread runs while the
+    main thread is stuck in a HIP / RCCL call; faulthandler's --watchdog stays
+    as the backstop for a wait that holds the GIL."""
+
+    def __init__(self):
+        import threading
+        self.phase, self.deadline, self.code = None, None, 1
+        self.lock = threading.Lock()
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def arm(self, phase, seconds, code=1):
+        with self.lock:
+            self.phase, self.deadline, self.code = phase, time.monotonic() + seconds, code
+
+    def _run(self):
+        import faulthandler
+        while True:
+            time.sleep(0.25)
+            with self.lock:
+                late = self.deadline is not None and time.monotonic() > self.deadline
+                phase, code = self.phase, self.code
+            if late:
+                print(f"bench: phase `{phase}` outlived its budget", file=sys.stderr, flush=True)
+                faulthandler.dump_traceback(all_threads=True)
+                if code == GRAPH_EXIT:
+                    graph_failed(f"{phase}: did not finish within its budget")
+                os._exit(code)
+
+
+PHASE_S = {"setup": 240, "c3": 120, "probe": 60, "config": 150, "cpu": 120}  # DESIGN.md section 5
+GRAPH_WAIT_S = 60.0
+CLOCK = None
+
+
+def arm(phase, seconds, code=1):
+    if CLOCK is not None:
+        CLOCK.arm(phase, seconds, code)
 
 
 def quiet_stdout():
@@ -416,20 +633,59 @@ class Harness:
             g.close()
         return ms, self.rmax(ms)
 
-    def timed(self, enqueue, drain, steps, warmup, graph_steps, reset=None):
+    def first_replay(self, gr, drain, verify, k0, k1, label):
+        """The captured graphs' first replay, before anything is timed: every
+        graph launched, then a HIP event on the library stream polled against
+        GRAPH_WAIT_S (a collective that never completes inside a replay is
+        caught here, not by the timed region), then the replayed steps
+        verified (verify(k0, k1, kind) -> None | reason) on every rank.  A
+        hang or a wrong result exits GRAPH_EXIT (the launcher then starts fresh
+        ranks with eager steps).  MBX_BENCH_FORCE_GRAPH_FAIL=timeout|verify
+        (rehearsal) makes rank 0 report that failure."""
+        torch = self.torch
+        force = os.environ.get("MBX_BENCH_FORCE_GRAPH_FAIL", "") if self.rank == 0 else ""
+        phase = f"{label}: first replay of {len(gr)} captured graph(s)"
+        arm(phase, GRAPH_WAIT_S + 30, GRAPH_EXIT)
+        for g in gr:
+            g.launch()
+        ev = torch.cuda.Event()
+        ev.record(self.ext)
+        t0 = time.monotonic()
+        while not ev.query():
+            if time.monotonic() - t0 > GRAPH_WAIT_S:
+                graph_failed(f"{phase} did not finish within {GRAPH_WAIT_S:.0f} s")
+            time.sleep(0.0005)
+        if force == "timeout":
+            graph_failed(f"{phase} did not finish within {GRAPH_WAIT_S:.0f} s (MBX_BENCH_FORCE_GRAPH_FAIL)")
+        drain()
+        reason = verify(k0, k1, f"{label} first graph replay") if verify else None
+        if force == "verify":
+            reason = f"{label} first graph replay: forced mismatch (MBX_BENCH_FORCE_GRAPH_FAIL)"
+        bad = int(reason is not None)
+        if self.world > 1:
+            t = torch.tensor([bad], dtype=torch.int32)
+            try:
+                self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+            except Exception as err:  # a peer left the group inside its graph phase
+                graph_failed(f"{phase}: verdict all-reduce failed ({type(err).__name__}: {err})")
+            bad = int(t[0])
+        if bad:
+            graph_failed(reason or f"{label}: another rank's first graph replay failed")
+        arm(f"{label}: timed steps", PHASE_S["c3"])
+
+    def timed(self, enqueue, drain, steps, warmup, graph_steps, reset=None, verify=None, label=""):
         """warmup steps (eager), graphs of graph_steps captured and replayed
-        once untimed, reset(), then EXACTLY `steps` steps between barrier +
-        synchronize on both sides; (max-over-ranks ms per step, host enqueue
-        us per step, graph steps used)."""
+        once untimed (first_replay: bounded wait + verified), reset(), then
+        EXACTLY `steps` steps between barrier + synchronize on both sides;
+        (max-over-ranks ms per step, host enqueue us per step, graph steps
+        used)."""
         enqueue(0, warmup)
         drain()
         gr = None
         if graph_steps and (self.comm is not None or not self.exchange):  # gloo exchanges run eagerly
             gr = self.graphs(enqueue, warmup, warmup + steps, graph_steps)
             if gr:
-                for g in gr:
-                    g.launch()
-                drain()
+                self.first_replay(gr, drain, verify, warmup, warmup + steps, label)
         if reset:
             reset()
         self.barrier()
@@ -508,6 +764,7 @@ def run_c3(H, args, cols, n, s, glob, label, bucket=None):
     `args.steps` timed steps (graph replay), kernel time, every step's count
     checked.  Returns the measurements (the table stays open for the probe)."""
     torch, ctx, m, world, rank = H.torch, H.ctx, H.m, H.world, H.rank
+    arm(f"{label}: pre-check, graph capture", PHASE_S["c3"])
     table = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [col.data_ptr() for col in cols], n, None, row_offset=s)
     cnf = [[(m.mbx.LT, ("sym", 1), ("int", THRESH))], [(m.mbx.GE, ("sym", 2), ("int", THRESH))]]
     plan = ctx.compile(table, cnf)
@@ -589,7 +846,7 @@ def run_c3(H, args, cols, n, s, glob, label, bucket=None):
     torch.cuda.synchronize()
 
     ms_step, enq_us, G = H.timed(enqueue, drain, steps, warmup, args.graph_steps,
-                                 reset=lambda: (counts.zero_(), torch.cuda.synchronize()))
+                                 reset=lambda: (counts.zero_(), torch.cuda.synchronize()), verify=verify, label=label)
     reason = verify(warmup, warmup + steps, f"{label} timed steps")
     H.agree(reason)
 
@@ -651,7 +908,7 @@ def config_c2(H, args):
     ctx.sync()
     H.agree(verify(0, 1, "C2 pre-check"))
     ms, _, G = H.timed(lambda a, b: [query(k) for k in range(a, b)], ctx.sync, steps, warmup, args.graph_steps,
-                       reset=lambda: (cnt.zero_(), ids.zero_(), torch.cuda.synchronize()))
+                       reset=lambda: (cnt.zero_(), ids.zero_(), torch.cuda.synchronize()), verify=verify, label="C2")
     H.agree(verify(warmup, warmup + steps, "C2 timed steps"))
     kms, kmax = H.kernel_ms(lambda i: query(0), max(1, args.kernel_graph))
     byts = n * 4 + n // 8 + want * 8
@@ -737,7 +994,7 @@ def config_c4(H, args):
         cnts.zero_(), alls.zero_(), o0.zero_(), o1.zero_(), ids.zero_()
         torch.cuda.synchronize()
 
-    ms, _, G = H.timed(enqueue, drain, steps, warmup, args.graph_steps, reset=reset)
+    ms, _, G = H.timed(enqueue, drain, steps, warmup, args.graph_steps, reset=reset, verify=verify, label="C4")
     H.agree(verify(warmup, warmup + steps, "C4 timed steps"))
     kms, kmax = H.kernel_ms(lambda i: launch(0), max(1, args.kernel_graph))
     byts = 2 * ((n + 63) // 64) * 8 + want * (8 + 8)
@@ -842,7 +1099,7 @@ def config_c5(H, args):
     drain()
     H.agree(verify(0, 1, "C5 pre-check"))
     ms, _, G = H.timed(enqueue, drain, steps, warmup, args.graph_steps,
-                       reset=lambda: (recs.zero_(), torch.cuda.synchronize()))
+                       reset=lambda: (recs.zero_(), torch.cuda.synchronize()), verify=verify, label="C5")
     H.agree(verify(warmup, warmup + steps, "C5 timed steps"))
     kms, kmax = H.kernel_ms(lambda i: scan(0), max(1, args.kernel_graph))
     glob = D.fold_aggregates(recs[-1].cpu().numpy())
@@ -880,12 +1137,20 @@ def main():
         print(f"bench: --gpus {args.gpus}", file=sys.stderr)
         sys.exit(2)
 
+    configs = [c.strip().upper() for c in args.configs.split(",") if c.strip() and c.strip().lower() != "none"]
+    bad = [c for c in configs if c not in ("C2", "C4", "C5")]
+    if bad:
+        print(f"bench: unknown config(s) {bad}", file=sys.stderr)
+        sys.exit(2)
+    worker = os.environ.get("MBX_BENCH_WORKER") == "1"
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
-            sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.dry_launch))
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     elif int(os.environ["WORLD_SIZE"]) != args.gpus:
         print(f"bench: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}", file=sys.stderr)
         sys.exit(2)
+    elif not worker and not args.dry_launch:
+        sys.exit(supervise_rank(sys.argv[1:]))  # under torch.distributed.run
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -895,11 +1160,10 @@ def main():
         print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world, "gpus": args.gpus,
                           "torch_imported": "torch" in sys.modules, "env": env}), flush=True)
         return
-    configs = [c.strip().upper() for c in args.configs.split(",") if c.strip() and c.strip().lower() != "none"]
-    bad = [c for c in configs if c not in ("C2", "C4", "C5")]
-    if bad:
-        print(f"bench: unknown config(s) {bad}", file=sys.stderr)
-        sys.exit(2)
+    if os.environ.get("MBX_BENCH_FAKE"):
+        fake_worker(args, world, rank)
+        return
+    fallback = os.environ.get("MBX_BENCH_FALLBACK")
     out_fd = quiet_stdout()
 
     import torch
@@ -907,9 +1171,12 @@ def main():
 
     import mbx_pkg
 
+    global CLOCK
     if args.watchdog > 0:  # armed after the imports (a cold box's first `import torch` takes minutes)
         import faulthandler
         faulthandler.dump_traceback_later(args.watchdog, exit=True)
+        CLOCK = PhaseClock()
+    arm("setup: communicators, tables", PHASE_S["setup"])
 
     same_device = os.environ.get("MBX_BENCH_SAME_DEVICE") == "1"
     device = 0 if same_device else local_rank
@@ -974,7 +1241,13 @@ def main():
     if glob is None and exchange:  # weak: the sum of every rank's own torch count
         glob = H.rsum(int(((cols[0] < THRESH) & (cols[1] >= THRESH)).sum().item()))
     r3 = run_c3(H, args, cols, n, s, glob, "C3")
+    arm("read probe", PHASE_S["probe"])
     probe = read_probe(H, r3["table"]) if rank == 0 else None
+    # the CPU baseline scans THIS table (the GPU run's arrays): one
+    # device -> host copy of the 4 columns, outside every timed region
+    host_cols = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        host_cols = [c.cpu().numpy() for c in cols]
     r3["table"].close()
     r3["plan"].close()
     # at N > 1 with one collective per query (the headline, SURVEY 8(e)'s
@@ -1021,6 +1294,7 @@ def main():
     # ---- the other BASELINE configs ------------------------------------------
     crecs = {}
     for name in configs:
+        arm(f"config {name}", PHASE_S["config"])
         if name == "C2":
             if rank == 0:
                 crecs["C2"] = config_c2(H.solo(), args)
@@ -1073,6 +1347,7 @@ def main():
             },
             "pre_check": "ok: one exchanged step verified on every rank before timing" if exchange else
                          "ok: one step verified before timing",
+            "exchange_form": exchange_form(r3["G"], fallback),
             "phases_us": {
                 "step_wall": ms_per_step * 1e3,
                 "scan_kernel_max_over_ranks": kern_max * 1e3,
@@ -1105,12 +1380,14 @@ def main():
             "configs": crecs,
             "cpu_baseline": None,
         }
-        if not args.no_cpu_baseline and world == 1:
+        if host_cols is not None:
             # rank 0 at N = 1 only, after the timed regions (at N > 1 the
             # line carries null: the baseline is the single-GPU comparison)
-            out["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds)
+            arm("cpu baseline", PHASE_S["cpu"])
+            out["cpu_baseline"] = cpu_baseline(host_cols, r3["want"], args.cpu_seconds)
         os.write(out_fd, (json.dumps(out) + "\n").encode())
 
+    arm("teardown", 60)
     ctx.close()
     if world > 1 or torch_exchange:
         dist.barrier()

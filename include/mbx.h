@@ -354,7 +354,7 @@ int mbx_cnf_cursor_launch(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *co
  *                        offsets; shard order = ascending global positions)
  * Stream order: a collective runs after everything already enqueued on the
  * context stream -- on the context stream itself (the default), or with the
- * tuning knob comm_same_stream = 0 (MBX_COMM_SAME_STREAM=0) on the
+ * tuning knob comm_same_stream = 0 (mbx_set_tuning) on the
  * communicator's exchange stream, which the context stream does not wait for
  * (the next scans may overlap it; inside a captured HIP graph on this ROCm
  * they do not, and the fork costs more than it hides).  mbx_sync waits for
@@ -431,13 +431,15 @@ int mbx_dev_download(mbx_ctx *ctx, const void *dev, void *host, int64_t bytes);
 int mbx_probe_read(mbx_ctx *ctx, const mbx_table *t, const int32_t *cols, int32_t ncols,
                    int64_t tiles_per_block, int32_t interleave, int64_t grid);
 /* A/B tuning knobs of this context, no reference
- * counterpart.  mbx_init reads their MBX_* environment defaults once; no
- * launch reads the environment.  knob: "tiles_per_block", "force_generic",
+ * counterpart.  Every context starts on the production defaults: the library
+ * reads no environment (a -DMBX_DIAG build, tools/build_diag.sh, also takes
+ * MBX_<KNOB> environment values at mbx_init).  knob: "tiles_per_block", "force_generic",
  * "scan_hoist", "scan_ri", "sink_lds", "ticket_groups", "fin_mode",
- * "join_plain", "distinct_lds_probes", "gather_fused", "select_blocks", "select_dbg", "cursor_prefetch", "scan_select_fused", "scan_select_waves", "select_flag_stride",
+ * "join_plain", "distinct_lds_probes", "gather_fused", "gather_pair" (0: two 4-byte loads per grouped pair row),
+ * "select_blocks", "select_dbg", "cursor_prefetch", "scan_select_fused", "scan_select_waves", "select_flag_stride",
  * "comm_same_stream", "scan_words_wt", and the one-launch ColumnarIndexScan's (k_cnf_select) "cnf_lookback" (0 auto,
  * 1 chained, 2 polled), "cnf_flag_stride" (1 or 16), "cnf_blocks" (0: 1024), "cnf_store" (0 default, 1 plain,
- * 2 write-through, 3 nontemporal); "reset" restores the defaults (MBX_<KNOB> environment values read at mbx_init). */
+ * 2 write-through, 3 nontemporal); "reset" restores the defaults. */
 int mbx_set_tuning(mbx_ctx *ctx, const char *knob, int64_t value);
 /* per-block wall_clock64() stamps (start, loads in, after the block barrier,
  * end) of the last compaction launched with select_dbg bit 3: 4 * nblocks

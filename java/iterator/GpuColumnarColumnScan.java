@@ -1,5 +1,7 @@
 package iterator;
 
+import java.io.IOException;
+
 import columnar.Columnarfile;
 import columnar.GpuTables;
 import global.AttrType;
@@ -36,7 +38,8 @@ public class GpuColumnarColumnScan extends Iterator implements GpuSelection {
   private int n, i;
 
   public GpuColumnarColumnScan(Columnarfile columnarfile, int colNo, int n_out_flds, int[] out_indexes,
-                               FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
+                               FldSpec[] proj_list, CondExpr[] outFilter)
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
     this(false, columnarfile, colNo, n_out_flds, out_indexes, proj_list, outFilter);
   }
 
@@ -46,38 +49,50 @@ public class GpuColumnarColumnScan extends Iterator implements GpuSelection {
    * fails with the NullPointerException the reference's null outIndexes
    * raises (:166).
    */
-  public GpuColumnarColumnScan(Columnarfile columnarfile, int colNo, CondExpr[] outFilter) throws Exception {
+  public GpuColumnarColumnScan(Columnarfile columnarfile, int colNo, CondExpr[] outFilter)
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
     this(true, columnarfile, colNo, 0, null, null, outFilter);
   }
 
   private GpuColumnarColumnScan(boolean deleteQuery, Columnarfile columnarfile, int colNo, int n_out_flds,
-                                int[] out_indexes, FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
-    this.deleteQuery = deleteQuery;
-    AttrType[] in1 = columnarfile.getAttributeTypes();
-    fieldCount = columnarfile.getFieldCount();
-    if (!deleteQuery) {
-      AttrType[] jtypes = new AttrType[n_out_flds];
-      TupleUtils.setup_op_tuple(Jtuple, jtypes, in1, (short) fieldCount, columnarfile.getStringSizes(), proj_list,
-                                n_out_flds);
-    }
-    perm_mat = proj_list;
-    ctx = GpuContext.ctx();
-    table = GpuTables.get(columnarfile.get_fileName());
-    outIdx = new int[n_out_flds];
-    projTypes = new int[n_out_flds];
-    projSizes = new short[n_out_flds];
-    for (int k = 0; k < n_out_flds; k++) {
-      outIdx[k] = out_indexes[k];
-      projTypes[k] = in1[outIdx[k]].attrType;
-      projSizes[k] = projTypes[k] == AttrType.attrString ? columnarfile.getAttrSizes()[outIdx[k]] : 4;
-    }
-    plan = Native.planCompile(ctx, table, onColumn(outFilter, colNo));   // PredEvalException on type errors
+                                int[] out_indexes, FldSpec[] proj_list, CondExpr[] outFilter)
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
+    // the reference's checked exceptions only (R/iterator/ColumnarColumnScan.java:39,91): a device or plan
+    // failure (PredEvalException on operand types included) is a FileScanException
     try {
-      selection = Native.scanBitmap(ctx, plan);
-      cursor = Native.cursorOpen(ctx, table, selection, outIdx);
+      this.deleteQuery = deleteQuery;
+      AttrType[] in1 = columnarfile.getAttributeTypes();
+      fieldCount = columnarfile.getFieldCount();
+      if (!deleteQuery) {
+        AttrType[] jtypes = new AttrType[n_out_flds];
+        TupleUtils.setup_op_tuple(Jtuple, jtypes, in1, (short) fieldCount, columnarfile.getStringSizes(), proj_list,
+                                  n_out_flds);
+      }
+      perm_mat = proj_list;
+      ctx = GpuContext.ctx();
+      table = GpuTables.get(columnarfile.get_fileName());
+      outIdx = new int[n_out_flds];
+      projTypes = new int[n_out_flds];
+      projSizes = new short[n_out_flds];
+      for (int k = 0; k < n_out_flds; k++) {
+        outIdx[k] = out_indexes[k];
+        projTypes[k] = in1[outIdx[k]].attrType;
+        projSizes[k] = projTypes[k] == AttrType.attrString ? columnarfile.getAttrSizes()[outIdx[k]] : 4;
+      }
+      plan = Native.planCompile(ctx, table, onColumn(outFilter, colNo));   // PredEvalException on type errors
+      try {
+        selection = Native.scanBitmap(ctx, plan);
+        cursor = Native.cursorOpen(ctx, table, selection, outIdx);
+      } catch (Exception e) {
+        close();
+        throw new FileScanException(e, "GPU column scan failed");
+      }
+    } catch (IOException | FileScanException | TupleUtilsException | InvalidRelation | RuntimeException e) {
+      close();
+      throw e;
     } catch (Exception e) {
       close();
-      throw new FileScanException(e, "GPU column scan failed");
+      throw new FileScanException(e, "GPU scan setup failed");
     }
   }
 

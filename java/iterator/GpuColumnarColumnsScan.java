@@ -1,5 +1,7 @@
 package iterator;
 
+import java.io.IOException;
+
 import columnar.Columnarfile;
 import columnar.GpuTables;
 import global.AttrType;
@@ -40,51 +42,64 @@ public class GpuColumnarColumnsScan extends Iterator implements GpuSelection {
   private int n, i;
 
   public GpuColumnarColumnsScan(Columnarfile columnarfile, int[] colNos, int n_out_flds, int[] out_indexes,
-                                FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
+                                FldSpec[] proj_list, CondExpr[] outFilter)
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
     this(false, columnarfile, colNos, n_out_flds, out_indexes, proj_list, outFilter);
   }
 
   /** the delete-query form (:104-157): no projection, for get_next_tid() */
-  public GpuColumnarColumnsScan(Columnarfile columnarfile, int[] colNos, CondExpr[] outFilter) throws Exception {
+  public GpuColumnarColumnsScan(Columnarfile columnarfile, int[] colNos, CondExpr[] outFilter)
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
     this(true, columnarfile, colNos, 0, null, null, outFilter);
   }
 
   private GpuColumnarColumnsScan(boolean deleteQuery, Columnarfile columnarfile, int[] colNos, int n_out_flds,
-                                 int[] out_indexes, FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
-    this.deleteQuery = deleteQuery;
-    this.colNos = colNos.clone();
-    AttrType[] in1 = columnarfile.getAttributeTypes();
-    fieldCount = columnarfile.getFieldCount();
-    if (!deleteQuery) {
-      AttrType[] jtypes = new AttrType[n_out_flds];
-      TupleUtils.setup_op_tuple(Jtuple, jtypes, in1, (short) fieldCount, columnarfile.getStringSizes(), proj_list,
-                                n_out_flds);                                                   // :57-60
-    }
-    perm_mat = proj_list;
-    // destType / dest_s_sizes exactly as :68-82 (its index quirk included)
-    int nstr = 0;
-    for (int c : colNos)
-      if (in1[c].attrType == AttrType.attrString) nstr++;
-    short[] destSizes = new short[nstr];
-    for (int k = 0; k < colNos.length; k++)
-      if (in1[colNos[k]].attrType == AttrType.attrString) destSizes[k] = columnarfile.getAttrSizes()[colNos[k]];
-    ctx = GpuContext.ctx();
-    table = GpuTables.get(columnarfile.get_fileName());
-    outIdx = new int[n_out_flds];
-    projTypes = new int[n_out_flds];
-    projSizes = new short[n_out_flds];
-    for (int k = 0; k < n_out_flds; k++) {
-      outIdx[k] = out_indexes[k];
-      projTypes[k] = in1[outIdx[k]].attrType;
-      projSizes[k] = projTypes[k] == AttrType.attrString ? columnarfile.getAttrSizes()[outIdx[k]] : 4;
-    }
-    plan = Native.planCompile(ctx, table, GpuCondExprs.remap(outFilter, this.colNos));
+                                 int[] out_indexes, FldSpec[] proj_list, CondExpr[] outFilter)
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
+    // the reference's checked exceptions only (R/iterator/ColumnarColumnsScan.java:39,104): a device or plan
+    // failure (PredEvalException on operand types included) is a FileScanException
     try {
-      selection = Native.scanBitmap(ctx, plan);
-      cursor = Native.cursorOpen(ctx, table, selection, outIdx);
+      this.deleteQuery = deleteQuery;
+      this.colNos = colNos.clone();
+      AttrType[] in1 = columnarfile.getAttributeTypes();
+      fieldCount = columnarfile.getFieldCount();
+      if (!deleteQuery) {
+        AttrType[] jtypes = new AttrType[n_out_flds];
+        TupleUtils.setup_op_tuple(Jtuple, jtypes, in1, (short) fieldCount, columnarfile.getStringSizes(), proj_list,
+                                  n_out_flds);                                                   // :57-60
+      }
+      perm_mat = proj_list;
+      // destType / dest_s_sizes exactly as :68-82 (its index quirk included)
+      int nstr = 0;
+      for (int c : colNos)
+        if (in1[c].attrType == AttrType.attrString) nstr++;
+      short[] destSizes = new short[nstr];
+      for (int k = 0; k < colNos.length; k++)
+        if (in1[colNos[k]].attrType == AttrType.attrString) destSizes[k] = columnarfile.getAttrSizes()[colNos[k]];
+      ctx = GpuContext.ctx();
+      table = GpuTables.get(columnarfile.get_fileName());
+      outIdx = new int[n_out_flds];
+      projTypes = new int[n_out_flds];
+      projSizes = new short[n_out_flds];
+      for (int k = 0; k < n_out_flds; k++) {
+        outIdx[k] = out_indexes[k];
+        projTypes[k] = in1[outIdx[k]].attrType;
+        projSizes[k] = projTypes[k] == AttrType.attrString ? columnarfile.getAttrSizes()[outIdx[k]] : 4;
+      }
+      plan = Native.planCompile(ctx, table, GpuCondExprs.remap(outFilter, this.colNos));
+      try {
+        selection = Native.scanBitmap(ctx, plan);
+        cursor = Native.cursorOpen(ctx, table, selection, outIdx);
+      } catch (Exception e) {
+        close();
+        throw new FileScanException(e, "GPU columns scan failed");
+      }
+    } catch (IOException | FileScanException | TupleUtilsException | InvalidRelation | RuntimeException e) {
+      close();
+      throw e;
     } catch (Exception e) {
       close();
-      throw new FileScanException(e, "GPU columns scan failed");
+      throw new FileScanException(e, "GPU scan setup failed");
     }
   }
 

@@ -1,5 +1,7 @@
 package iterator;
 
+import java.io.IOException;
+
 import columnar.GpuTables;
 import global.AttrType;
 import global.GpuContext;
@@ -34,7 +36,8 @@ public class GpuColumnarFileScan extends Iterator implements GpuSelection {
   private int n, i;
 
   public GpuColumnarFileScan(String file_name, AttrType[] in1, short[] s1_sizes, short len_in1, int n_out_flds,
-                             FldSpec[] proj_list, CondExpr[] outFilter) throws Exception {
+                             FldSpec[] proj_list, CondExpr[] outFilter)
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
     this(false, file_name, in1, s1_sizes, len_in1, n_out_flds, proj_list, outFilter);
   }
 
@@ -45,41 +48,52 @@ public class GpuColumnarFileScan extends Iterator implements GpuSelection {
    * NullPointerException the reference's null Jtuple raises (:167, :214).
    */
   public GpuColumnarFileScan(String file_name, AttrType[] in1, short[] s1_sizes, short len_in1,
-                             CondExpr[] outFilter) throws Exception {
+                             CondExpr[] outFilter)
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
     this(true, file_name, in1, s1_sizes, len_in1, 0, null, outFilter);
   }
 
   private GpuColumnarFileScan(boolean deleteQuery, String file_name, AttrType[] in1, short[] s1_sizes,
                               short len_in1, int n_out_flds, FldSpec[] proj_list, CondExpr[] outFilter)
-      throws Exception {
-    this.deleteQuery = deleteQuery;
-    this.len_in1 = len_in1;
-    outTypes = new AttrType[n_out_flds];
-    if (!deleteQuery)
-      TupleUtils.setup_op_tuple(Jtuple, outTypes, in1, len_in1, s1_sizes, proj_list, n_out_flds);  // :66-71
-    perm_mat = proj_list;
-    ctx = GpuContext.ctx();
-    table = GpuTables.get(file_name);
-    // per-column char(n) sizes: s1_sizes lists the string columns' sizes in order
-    short[] colSize = new short[len_in1];
-    for (int c = 0, k = 0; c < len_in1; c++)
-      colSize[c] = in1[c].attrType == AttrType.attrString ? s1_sizes[k++] : 4;
-    proj = new int[n_out_flds];
-    projTypes = new int[n_out_flds];
-    projSizes = new short[n_out_flds];
-    for (int k = 0; k < n_out_flds; k++) {
-      if (proj_list[k].relation.key != RelSpec.outer) throw new InvalidRelation("Invalid relation -innerRel");
-      proj[k] = proj_list[k].offset - 1;
-      projTypes[k] = in1[proj[k]].attrType;
-      projSizes[k] = colSize[proj[k]];
-    }
-    plan = Native.planCompile(ctx, table, outFilter);                    // PredEvalException on type errors
+      throws IOException, FileScanException, TupleUtilsException, InvalidRelation {
+    // the reference's checked exceptions only (R/iterator/ColumnarFileScan.java:51-62): a device or plan
+    // failure (PredEvalException on operand types included) is a FileScanException
     try {
-      selection = Native.scanBitmap(ctx, plan);                         // one kernel launch
-      cursor = Native.cursorOpen(ctx, table, selection, proj);          // positions + projected values in HBM
+      this.deleteQuery = deleteQuery;
+      this.len_in1 = len_in1;
+      outTypes = new AttrType[n_out_flds];
+      if (!deleteQuery)
+        TupleUtils.setup_op_tuple(Jtuple, outTypes, in1, len_in1, s1_sizes, proj_list, n_out_flds);  // :66-71
+      perm_mat = proj_list;
+      ctx = GpuContext.ctx();
+      table = GpuTables.get(file_name);
+      // per-column char(n) sizes: s1_sizes lists the string columns' sizes in order
+      short[] colSize = new short[len_in1];
+      for (int c = 0, k = 0; c < len_in1; c++)
+        colSize[c] = in1[c].attrType == AttrType.attrString ? s1_sizes[k++] : 4;
+      proj = new int[n_out_flds];
+      projTypes = new int[n_out_flds];
+      projSizes = new short[n_out_flds];
+      for (int k = 0; k < n_out_flds; k++) {
+        if (proj_list[k].relation.key != RelSpec.outer) throw new InvalidRelation("Invalid relation -innerRel");
+        proj[k] = proj_list[k].offset - 1;
+        projTypes[k] = in1[proj[k]].attrType;
+        projSizes[k] = colSize[proj[k]];
+      }
+      plan = Native.planCompile(ctx, table, outFilter);                    // PredEvalException on type errors
+      try {
+        selection = Native.scanBitmap(ctx, plan);                         // one kernel launch
+        cursor = Native.cursorOpen(ctx, table, selection, proj);          // positions + projected values in HBM
+      } catch (Exception e) {
+        close();
+        throw new FileScanException(e, "GPU scan failed");
+      }
+    } catch (IOException | FileScanException | TupleUtilsException | InvalidRelation | RuntimeException e) {
+      close();
+      throw e;
     } catch (Exception e) {
       close();
-      throw new FileScanException(e, "GPU scan failed");
+      throw new FileScanException(e, "GPU scan setup failed");
     }
   }
 

@@ -1,5 +1,6 @@
 package iterator;
 
+import java.io.IOException;
 import java.util.ArrayList;
 import java.util.List;
 
@@ -8,6 +9,11 @@ import global.AttrType;
 import global.GlobalConst;
 import global.GpuContext;
 import global.Native;
+import heap.HFBufMgrException;
+import heap.HFDiskMgrException;
+import heap.HFException;
+import heap.InvalidTupleSizeException;
+import heap.InvalidTypeException;
 import heap.Tuple;
 
 /**
@@ -47,50 +53,64 @@ public class GpuColumnarNestedLoopJoins extends Iterator implements GlobalConst 
                                     int in1_len, short[] t1_str_sizes, AttrType in2[], int in2_len,
                                     short[] t2_str_sizes, Iterator outerItr, Iterator innerItr, CondExpr[] outFilter,
                                     CondExpr[] rightFilter, CondExpr[] joinFilter, FldSpec[] proj_list,
-                                    int n_out_flds, int amt_of_mem) throws Exception {
-    if (!(outerItr instanceof GpuSelection) || !(innerItr instanceof GpuSelection))
-      throw new NestedLoopException("GpuColumnarNestedLoopJoins: outerItr / innerItr must be GPU scans "
-                                    + "(GpuColumnarFileScan, GpuColumnarColumnScan, GpuColumnarColumnsScan, "
-                                    + "GpuColumnarIndexScan)");
-    outerFile = outerColumnarFile;
-    innerFile = innerColumnarFile;
-    Jtypes = new AttrType[n_out_flds];
-    perm_mat = proj_list;
-    TupleUtils.setup_op_tuple(Jtuple, Jtypes, in1, in1_len, in2, in2_len, t1_str_sizes, t2_str_sizes, proj_list,
-                              n_out_flds);                                                          // :88-94
-    ctx = GpuContext.ctx();
-    GpuSelection o = (GpuSelection) outerItr, in = (GpuSelection) innerItr;
-    outerTable = o.gpuTable();
-    innerTable = in.gpuTable();
-    ocols = o.fileColumns();
-    icols = in.fileColumns();
-    long osel = filtered(outerTable, o.gpuSelection(), outFilter, ocols);
-    long isel = filtered(innerTable, in.gpuSelection(), rightFilter, icols);
-    iterCount = Native.bitmapCardinality(o.gpuSelection());      // "Total Outer Tuples By Iterator"
-    fullCount = Native.bitmapCardinality(osel);                  // "... By Full Constraint"
-    // the join CNF: outer field OP inner field (NljQuery.buildCNFJoinCondExpr)
-    List<int[]> terms = new ArrayList<>();
-    List<Integer> offs = new ArrayList<>();
-    offs.add(0);
-    for (int c = 0; joinFilter != null && c < joinFilter.length && joinFilter[c] != null; c++) {
-      for (CondExpr e = joinFilter[c]; e != null; e = e.next) {
-        if (e.type1.attrType != AttrType.attrSymbol || e.type2.attrType != AttrType.attrSymbol)
-          throw new NestedLoopException("GpuColumnarNestedLoopJoins: join terms compare an outer and an inner field");
-        terms.add(new int[] {e.op.attrOperator, ocols[e.operand1.symbol.offset - 1], icols[e.operand2.symbol.offset - 1]});
+                                    int n_out_flds, int amt_of_mem)
+      throws IOException, NestedLoopException, InvalidTypeException, InvalidTupleSizeException, JoinsException,
+      HFException, HFBufMgrException, HFDiskMgrException {
+    // the reference constructor's checked exceptions only (R/iterator/ColumnarNestedLoopJoins.java:47-61):
+    // TupleUtilsException and device / plan failures become a NestedLoopException, as the reference wraps
+    // setup_op_tuple's (:88-94)
+    try {
+      if (!(outerItr instanceof GpuSelection) || !(innerItr instanceof GpuSelection))
+        throw new NestedLoopException("GpuColumnarNestedLoopJoins: outerItr / innerItr must be GPU scans "
+                                      + "(GpuColumnarFileScan, GpuColumnarColumnScan, GpuColumnarColumnsScan, "
+                                      + "GpuColumnarIndexScan)");
+      outerFile = outerColumnarFile;
+      innerFile = innerColumnarFile;
+      Jtypes = new AttrType[n_out_flds];
+      perm_mat = proj_list;
+      TupleUtils.setup_op_tuple(Jtuple, Jtypes, in1, in1_len, in2, in2_len, t1_str_sizes, t2_str_sizes, proj_list,
+                                n_out_flds);                                                          // :88-94
+      ctx = GpuContext.ctx();
+      GpuSelection o = (GpuSelection) outerItr, in = (GpuSelection) innerItr;
+      outerTable = o.gpuTable();
+      innerTable = in.gpuTable();
+      ocols = o.fileColumns();
+      icols = in.fileColumns();
+      long osel = filtered(outerTable, o.gpuSelection(), outFilter, ocols);
+      long isel = filtered(innerTable, in.gpuSelection(), rightFilter, icols);
+      iterCount = Native.bitmapCardinality(o.gpuSelection());      // "Total Outer Tuples By Iterator"
+      fullCount = Native.bitmapCardinality(osel);                  // "... By Full Constraint"
+      // the join CNF: outer field OP inner field (NljQuery.buildCNFJoinCondExpr)
+      List<int[]> terms = new ArrayList<>();
+      List<Integer> offs = new ArrayList<>();
+      offs.add(0);
+      for (int c = 0; joinFilter != null && c < joinFilter.length && joinFilter[c] != null; c++) {
+        for (CondExpr e = joinFilter[c]; e != null; e = e.next) {
+          if (e.type1.attrType != AttrType.attrSymbol || e.type2.attrType != AttrType.attrSymbol)
+            throw new NestedLoopException("GpuColumnarNestedLoopJoins: join terms compare an outer and an inner field");
+          terms.add(new int[] {e.op.attrOperator, ocols[e.operand1.symbol.offset - 1], icols[e.operand2.symbol.offset - 1]});
+        }
+        offs.add(terms.size());
       }
-      offs.add(terms.size());
+      int[] t3 = new int[3 * terms.size()];
+      for (int j = 0; j < terms.size(); j++) System.arraycopy(terms.get(j), 0, t3, 3 * j, 3);
+      int[] o1 = new int[offs.size()];
+      for (int j = 0; j < o1.length; j++) o1[j] = offs.get(j);
+      tupleSize = outerItr.getTupleSize();
+      block = (long) (amt_of_mem - 1) * (MINIBASE_PAGESIZE / tupleSize);                             // :122
+      res = Native.join(ctx, outerTable, osel, innerTable, isel, t3, o1, Native.JOIN_NLJ, block);
+      long[] info = Native.joinInfo(res);
+      npairs = info[0];
+      passes = info[1];
+      passHeader(0);                                                                                 // :103-107
+    } catch (IOException | NestedLoopException | InvalidTypeException | InvalidTupleSizeException | JoinsException
+             | HFException | HFBufMgrException | HFDiskMgrException | RuntimeException e) {
+      close();
+      throw e;
+    } catch (Exception e) {
+      close();
+      throw new NestedLoopException(e, "GpuColumnarNestedLoopJoins: GPU join setup failed");
     }
-    int[] t3 = new int[3 * terms.size()];
-    for (int j = 0; j < terms.size(); j++) System.arraycopy(terms.get(j), 0, t3, 3 * j, 3);
-    int[] o1 = new int[offs.size()];
-    for (int j = 0; j < o1.length; j++) o1[j] = offs.get(j);
-    tupleSize = outerItr.getTupleSize();
-    block = (long) (amt_of_mem - 1) * (MINIBASE_PAGESIZE / tupleSize);                             // :122
-    res = Native.join(ctx, outerTable, osel, innerTable, isel, t3, o1, Native.JOIN_NLJ, block);
-    long[] info = Native.joinInfo(res);
-    npairs = info[0];
-    passes = info[1];
-    passHeader(0);                                                                                 // :103-107
   }
 
   /** the iterator's selection AND the pending filter's scan (a new bitmap), or the selection itself */
@@ -163,31 +183,39 @@ public class GpuColumnarNestedLoopJoins extends Iterator implements GlobalConst 
     return byPerm;
   }
 
-  public Tuple get_next() throws Exception {
-    while (true) {
-      if (k < batchN) {
-        for (; curPass < pass[k]; ) passHeader(++curPass);
-        for (int q = 0; q < perm_mat.length; q++) {                                  // Projection.Join
-          Object col = perm_mat[q].relation.key == RelSpec.outer ? outerVals[q] : innerVals[q];
-          switch (Jtypes[q].attrType) {
-            case AttrType.attrInteger: Jtuple.setIntFld(q + 1, ((int[]) col)[k]); break;
-            case AttrType.attrReal: Jtuple.setFloFld(q + 1, ((float[]) col)[k]); break;
-            default: Jtuple.setStrFld(q + 1, ((String[]) col)[k]);
+  public Tuple get_next() throws InvalidTupleSizeException, IOException, InvalidTypeException {
+    // get_next's checked exceptions as the reference declares them (:157); a device failure while
+    // fetching pairs or rows is an IOException (the pairs' I/O), its cause attached
+    try {
+      while (true) {
+        if (k < batchN) {
+          for (; curPass < pass[k]; ) passHeader(++curPass);
+          for (int q = 0; q < perm_mat.length; q++) {                                  // Projection.Join
+            Object col = perm_mat[q].relation.key == RelSpec.outer ? outerVals[q] : innerVals[q];
+            switch (Jtypes[q].attrType) {
+              case AttrType.attrInteger: Jtuple.setIntFld(q + 1, ((int[]) col)[k]); break;
+              case AttrType.attrReal: Jtuple.setFloFld(q + 1, ((float[]) col)[k]); break;
+              default: Jtuple.setStrFld(q + 1, ((String[]) col)[k]);
+            }
           }
+          k++;
+          return Jtuple;
         }
-        k++;
-        return Jtuple;
+        if (fetched < npairs) {
+          fetch();
+          continue;
+        }
+        if (!done) {                            // the passes without a pair, then the statistics (:178-190)
+          for (; curPass < passes - 1; ) passHeader(++curPass);
+          statistics();
+          done = true;
+        }
+        return null;
       }
-      if (fetched < npairs) {
-        fetch();
-        continue;
-      }
-      if (!done) {                            // the passes without a pair, then the statistics (:178-190)
-        for (; curPass < passes - 1; ) passHeader(++curPass);
-        statistics();
-        done = true;
-      }
-      return null;
+    } catch (InvalidTupleSizeException | IOException | InvalidTypeException | RuntimeException e) {
+      throw e;
+    } catch (Exception e) {
+      throw new IOException("GpuColumnarNestedLoopJoins: GPU pair fetch failed", e);
     }
   }
 

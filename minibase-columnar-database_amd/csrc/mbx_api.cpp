@@ -70,14 +70,21 @@ static int64_t scan_tiles_per_block(const mbx_ctx* c, int64_t nrows, const PlanV
   return choose_tiles_per_block(nrows);
 }
 
+#ifdef MBX_DIAG
 static int64_t env_knob(const char* name, int64_t dflt) {
   const char* e = getenv(name);
   return e && *e ? atoll(e) : dflt;
 }
+#endif
 
-// the MBX_* A/B knobs, read once per context (mbx_init)
-static void tuning_from_env(MbxTuning& t) {
+// The context's tuning at mbx_init and after mbx_set_tuning("reset"): the
+// production defaults.  A -DMBX_DIAG build (tools/build_diag.sh,
+// tools/build_variant.sh) also reads the MBX_* A/B knobs from the environment;
+// the default library reads no environment at all -- tests and tools drive the
+// same knobs through mbx_set_tuning.
+static void tuning_defaults(MbxTuning& t) {
   t = MbxTuning();
+#ifdef MBX_DIAG
   t.tiles_per_block = env_knob("MBX_TILES_PER_BLOCK", -1);
   t.force_generic = (int32_t)env_knob("MBX_FORCE_GENERIC", 0);
   t.scan_hoist = (int32_t)env_knob("MBX_SCAN_HOIST", 1);
@@ -87,14 +94,11 @@ static void tuning_from_env(MbxTuning& t) {
   t.sink_lds = (int32_t)env_knob("MBX_SINK_LDS", 1);
   t.ticket_groups = (int32_t)env_knob("MBX_TICKET_GROUPS", -1);
   t.fin_mode = (int32_t)env_knob("MBX_FIN_MODE", -1);
-#ifndef MBX_DIAG
-  if (t.fin_mode == kFinFences || t.fin_mode == kFinSegOnly) t.fin_mode = -1;  // A/B forms: -DMBX_DIAG
-#endif
   t.join_plain = (int32_t)env_knob("MBX_JOIN_PLAIN", 0);
   t.distinct_lds_probes = (int32_t)env_knob("MBX_DISTINCT_LDS_PROBES", -1);
   t.select_dbg = (int32_t)env_knob("MBX_SELECT_DBG", 0);
-  if (((t.select_dbg & 3) | ((t.select_dbg >> 4) & 983)) & ~kDiagDbg) t.select_dbg = 0;  // A/B forms: -DMBX_DIAG
   t.gather_fused = (int32_t)env_knob("MBX_GATHER_FUSED", 1);
+  t.gather_pair = env_knob("MBX_GATHER_PAIR", 1) != 0;
   t.cursor_prefetch = (int32_t)env_knob("MBX_CURSOR_PREFETCH", 1);
   t.scan_select_fused = (int32_t)env_knob("MBX_SCAN_SELECT_FUSED", 1);
   t.scan_select_waves = (int32_t)env_knob("MBX_SCAN_SELECT_WAVES", 16);
@@ -108,6 +112,7 @@ static void tuning_from_env(MbxTuning& t) {
   if (t.cnf_lookback < 0 || t.cnf_lookback > 2) t.cnf_lookback = 0;
   t.select_blocks = (int32_t)env_knob("MBX_SELECT_BLOCKS", 1024);
   if (t.select_blocks < 1) t.select_blocks = 1024;  // as mbx_set_tuning: never a zero / negative grid divisor
+#endif
 }
 
 static int ensure_partials(mbx_ctx* c, int64_t n) {
@@ -210,7 +215,7 @@ extern "C" int mbx_init(int32_t device, mbx_ctx** out) {
   mbx_ctx* c = new (std::nothrow) mbx_ctx();
   if (!c) return fail(MBX_E_NOMEM, "mbx_init: host allocation");
   c->device = device;
-  tuning_from_env(c->tune);
+  tuning_defaults(c->tune);
   int rc = MBX_OK;
   do {
     hipError_t e = hipSetDevice(device);
@@ -283,7 +288,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
   NOTNULL(knob);
   MbxTuning& t = c->tune;
   if (!strcmp(knob, "reset")) {
-    tuning_from_env(t);
+    tuning_defaults(t);
     return MBX_OK;
   }
   const int32_t v = (int32_t)value;
@@ -316,6 +321,7 @@ extern "C" int mbx_set_tuning(mbx_ctx* c, const char* knob, int64_t value) {
     t.select_dbg = v;
   }
   else if (!strcmp(knob, "gather_fused")) t.gather_fused = v;
+  else if (!strcmp(knob, "gather_pair")) t.gather_pair = v != 0;
   else if (!strcmp(knob, "select_blocks")) t.select_blocks = v < 1 ? 1024 : (int32_t)v;
   else if (!strcmp(knob, "cnf_blocks")) t.cnf_blocks = v < 0 ? 0 : (int32_t)v;
   else if (!strcmp(knob, "cnf_flag_stride")) t.cnf_flag_stride = v == kFlagStride ? kFlagStride : 1;
@@ -1726,7 +1732,7 @@ static int materialize_dev(mbx_ctx* c, const mbx_table* t, const mbx_bitmap* sel
   HIPCHK(launch_materialize(sel->words, sel->nwords, sel->wpb, sel->segc, row_offset, dev_ids, pc, dev_out, nproj,
                             dev_total, c->stream, (c->tune.select_dbg & 3) | ((c->tune.select_dbg >> 4) & 32), stamps,
                             c->tune.gather_fused != 0,
-                            c->tune.select_blocks));
+                            c->tune.select_blocks, c->tune.gather_pair != 0));
   return MBX_OK;
 }
 
@@ -1756,6 +1762,7 @@ static CnfTune cnf_tune(const mbx_ctx* c) {
   k.flag_stride = c->tune.cnf_flag_stride;
   k.lookback = c->tune.cnf_lookback;
   k.store = c->tune.cnf_store;
+  k.gather_pair = c->tune.gather_pair;
   return k;
 }
 
@@ -1977,10 +1984,12 @@ static int cursor_next_view(mbx_cursor* k, int64_t max_rows, const int64_t** ids
   if (max_rows <= 0) return fail(MBX_E_INVALID, "cursor_next: max_rows %lld", (long long)max_rows);
   {
     // a batch's buffers (2 pinned + 1 device) are sized by bytes, not rows:
-    // at most kCursorBatchBytes each, however wide the projected row
+    // at most kCursorBatchBytes each, however wide the projected row --
+    // batch_layout rounds each of its 1 + nproj parts up to 16 bytes, so
+    // that padding is set aside first
     int64_t row_bytes = (int64_t)sizeof(int64_t);
     for (size_t j = 0; j < k->outs.size(); j++) row_bytes += host_width(k, j);
-    const int64_t cap = kCursorBatchBytes / row_bytes;
+    const int64_t cap = (kCursorBatchBytes - 16 * (int64_t)(k->outs.size() + 1)) / row_bytes;
     if (max_rows > cap) max_rows = cap > 0 ? cap : 1;
   }
   if (int rc0 = cursor_resolve(k)) return rc0;
@@ -2202,7 +2211,25 @@ extern "C" int mbx_materialize(mbx_ctx* c, const mbx_table* t, const mbx_bitmap*
     mbx_cursor_close(k);
     return fail(MBX_E_INVALID, "materialize: %lld rows, capacity %lld", (long long)k->count, (long long)cap);
   }
-  if (k->count > 0) rc = mbx_cursor_next(k, k->count, host_ids, host_out, n);
+  // batch after batch (a cursor batch holds at most kCursorBatchBytes), each
+  // copied to its rows' offset in the caller's arrays
+  int64_t done = 0;
+  while (rc == MBX_OK && done < k->count) {
+    const int64_t* vids = nullptr;
+    const void* vcols[kMaxProj];
+    int64_t got = 0;
+    rc = cursor_next_view(k, k->count - done, &vids, vcols, &got);
+    if (rc || got == 0) break;
+    if (host_ids) memcpy(host_ids + done, vids, (size_t)got * sizeof(int64_t));
+    for (size_t j = 0; host_out && j < k->outs.size(); j++) {
+      const int64_t w = host_width(k, j);
+      if (host_out[j]) memcpy((uint8_t*)host_out[j] + done * w, vcols[j], (size_t)(got * w));
+    }
+    done += got;
+  }
+  if (rc == MBX_OK && done != k->count)
+    rc = fail(MBX_E_DEVICE, "materialize: %lld of %lld rows delivered", (long long)done, (long long)k->count);
+  if (rc == MBX_OK) *n = done;
   mbx_cursor_close(k);
   return rc;
 }

@@ -47,8 +47,9 @@ struct mbx_graph {
 
 namespace {
 
-// dist.fold_aggregates on the device: rank order, one lane
-__global__ void k_fold_agg(const AggOut* __restrict__ recs, int32_t n, AggOut* __restrict__ out) {
+// dist.fold_aggregates on the device: rank order, one lane.  out may alias
+// recs[0] (mbx_agg_fold_async folds in place), so neither is __restrict__.
+__global__ void k_fold_agg(const AggOut* recs, int32_t n, AggOut* out) {
   if (threadIdx.x != 0) return;
   AggOut r = recs[0];
   double fsum = 0.0;

@@ -339,7 +339,7 @@ hipError_t launch_finalize(const Partial* partials, int64_t nblocks, int32_t agg
 // flag stride (1 or kFlagStride), look-back form (0 auto, 1 chained, 2
 // polled), output stores (0 default, 1 plain, 2 write-through, 3 nontemporal)
 struct CnfTune {
-  int32_t blocks = 0, flag_stride = 1, lookback = 0, store = 0;
+  int32_t blocks = 0, flag_stride = 1, lookback = 0, store = 0, gather_pair = 1;
 };
 hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, int64_t nwords, int64_t nbits,
                                   int64_t* lb, int64_t row_offset, int64_t* ids, const ProjCol* proj,
@@ -374,7 +374,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
                               const int64_t* segc, int64_t row_offset, int64_t* ids,
                               const ProjCol* proj, void* const* out, int32_t nproj, int64_t* total,
                               hipStream_t s, int32_t dbg = 0, int64_t* stamps = nullptr, bool fuse_gather = true,
-                              int64_t max_blocks = 1024);
+                              int64_t max_blocks = 1024, bool gather_pair = true);
 // 4-byte columns (int / float): also writes every output's segment counts
 hipError_t launch_index_build4(const KCol& col, int64_t nrows, const uint64_t* deleted, const uint32_t* values,
                                int32_t nvalues, uint64_t* const* outs, int64_t* const* segs, int64_t words_per_block,

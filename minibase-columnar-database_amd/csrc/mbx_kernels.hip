@@ -558,14 +558,10 @@ struct Gather4 {
 };
 
 // the 8-byte pair form applies: 2 columns, adjacent words of one row of a
-// group (even stride, 8-byte aligned); MBX_GATHER_PAIR=0 keeps two 4-byte
-// loads per row (A/B)
-inline void gather4_pairing(Gather4& G) {
-  static const bool off = [] {
-    const char* e = getenv("MBX_GATHER_PAIR");
-    return e && atoi(e) == 0;
-  }();
-  G.pair = !off && G.n == 2 && G.col[1] == G.col[0] + 1 && G.stride[0] == G.stride[1] && G.stride[0] % 2 == 0 &&
+// group (even stride, 8-byte aligned); allow = false (tuning gather_pair 0)
+// keeps two 4-byte loads per row (A/B)
+inline void gather4_pairing(Gather4& G, bool allow) {
+  G.pair = allow && G.n == 2 && G.col[1] == G.col[0] + 1 && G.stride[0] == G.stride[1] && G.stride[0] % 2 == 0 &&
            ((uintptr_t)G.col[0] & 7) == 0;
 }
 
@@ -2558,7 +2554,7 @@ hipError_t launch_count_sum(const int64_t* segc, int64_t n, int64_t* out, hipStr
 hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t words_per_block,
                               const int64_t* segc, int64_t row_offset, int64_t* ids, const ProjCol* proj,
                               void* const* out, int32_t nproj, int64_t* total, hipStream_t s, int32_t dbg,
-                              int64_t* stamps, bool fuse_gather, int64_t max_blocks) {
+                              int64_t* stamps, bool fuse_gather, int64_t max_blocks, bool gather_pair) {
   if (nwords == 0) return hipMemsetAsync(total, 0, sizeof(int64_t), s);
   if (max_blocks < 1) max_blocks = 1024;
   // ~max_blocks (1024) compaction blocks whatever the segment size: S segments per block
@@ -2577,7 +2573,7 @@ hipError_t launch_materialize(const uint64_t* words, int64_t nwords, int64_t wor
       G.out[j] = (uint32_t*)out[j];
     }
     G.n = nproj;
-    gather4_pairing(G);
+    gather4_pairing(G, gather_pair);
     hipLaunchKernelGGL(k_select_ids<4>, dim3((unsigned)g), dim3(kBlock), 0, s, words, nwords, wpb, segc, S,
                        row_offset, ids, total, dbg, stamps, G);
     return hipGetLastError();
@@ -2625,7 +2621,7 @@ hipError_t launch_cnf_materialize(const BitmapCnf& c, const uint64_t* deleted, i
     W.sw[j] = proj[j].stride_w;
   }
   G.n = narrow ? nproj : 0;
-  gather4_pairing(G);
+  gather4_pairing(G, knobs.gather_pair != 0);
   W.n = nproj;
   G.cap = W.cap = cap;
   // kernel dbg bit 3 = the chained look-back: each block walks back 64

@@ -41,6 +41,9 @@ using mbx::Partial;
 // A/B tuning knobs of the scan path.  Read from the
 // MBX_* environment once in mbx_init and changed only by mbx_set_tuning, so
 // no launch reads the environment.  -1 = the built-in default.
+// The knobs' defaults are the production forms.  Names in comments are the
+// environment variables a -DMBX_DIAG build reads at mbx_init (the default
+// library reads none: mbx_set_tuning only).
 struct MbxTuning {
   int64_t tiles_per_block = -1;   // MBX_TILES_PER_BLOCK: segment size of every scan / BitSet
   int32_t force_generic = 0;      // MBX_FORCE_GENERIC: plans compiled after this use k_scan_generic
@@ -54,6 +57,7 @@ struct MbxTuning {
   int32_t join_plain = 0;         // MBX_JOIN_PLAIN: k_join_matrix instead of the fast form
   int32_t distinct_lds_probes = -1;  // MBX_DISTINCT_LDS_PROBES
   int32_t gather_fused = 1;       // MBX_GATHER_FUSED: 0 = compaction, then k_gather (two launches)
+  int32_t gather_pair = 1;        // MBX_GATHER_PAIR: 0 = two 4-byte loads per grouped pair row instead of one 8-byte
   int32_t cnf_store = 0;          // MBX_CNF_STORE: k_cnf_select outputs 0 default, 1 plain, 2 write-through, 3 nontemporal
   int32_t cnf_lookback = 0;       // MBX_CNF_LOOKBACK: k_cnf_select look-back 0 auto, 1 chained, 2 polled
   int32_t cnf_flag_stride = 1;    // MBX_CNF_FLAG_STRIDE: k_cnf_select's polled count flags 16 words apart, or 1

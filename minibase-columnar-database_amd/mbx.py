@@ -347,7 +347,7 @@ class Context:
 
     def set_tuning(self, knob, value=0):
         """mbx_set_tuning: one A/B knob of this context ("reset" restores the
-        MBX_* environment defaults read at mbx_init)."""
+        production defaults; the default library reads no environment)."""
         _chk(lib().mbx_set_tuning(self.h, knob.encode(), int(value)))
 
     def probe_read(self, table, cols, tiles_per_block=0, interleave=False, grid=0):

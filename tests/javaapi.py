@@ -46,9 +46,20 @@ def _split_params(s):
     return [_param(p) for p in out]
 
 
+def throws_list(tail):
+    """the exception types of a declaration's `throws` clause (text after the
+    parameter list), in source order, as written (simple or qualified)"""
+    m = re.search(r"\bthrows\b(.*)$", tail, flags=re.S)
+    if not m:
+        return []
+    return [re.sub(r"\s+", "", t) for t in m.group(1).split(",") if t.strip()]
+
+
 def public_api(src):
-    """{'class': name, 'ctors': [[types]], 'methods': [{'name','params','returns'}],
-    'fields': [{'name','type'}]} of the first top-level class in src."""
+    """{'class': name, 'ctors': [[types]], 'ctor_throws': [[exception types]] (one
+    list per constructor, same order), 'methods': [{'name', 'params', 'returns',
+    'throws', 'throws_list'}], 'fields': [{'name','type'}]} of the first
+    top-level class in src."""
     s = _strip(src)
     m = re.search(r"\bclass\s+(\w+)", s)
     if not m:
@@ -75,7 +86,7 @@ def public_api(src):
                 break
             if depth == 1:
                 stmt = ""
-    api = {"class": cls, "ctors": [], "methods": [], "fields": []}
+    api = {"class": cls, "ctors": [], "ctor_throws": [], "methods": [], "fields": []}
     for d in decls:
         d = re.sub(r"\s+", " ", d).strip()
         d = d.split(" = ")[0].strip()
@@ -90,12 +101,14 @@ def public_api(src):
             throws = rest.rsplit(")", 1)[1]
             ps = _split_params(params) if params.strip() else []
             toks = head.strip().rsplit(" ", 1)
+            tl = throws_list(throws)
             if len(toks) == 1:
                 api["ctors"].append(ps)
+                api["ctor_throws"].append(tl)
             else:
                 ret, name = toks
                 api["methods"].append({"name": name, "params": ps, "returns": _norm_type(ret),
-                                       "throws": bool(re.search(r"\bthrows\b", throws))})
+                                       "throws": bool(tl), "throws_list": tl})
         elif d.startswith("class ") or d.startswith("interface "):
             continue
         else:

@@ -3,6 +3,7 @@ starts N rank processes with the rank env torch.distributed.run would give
 them (one process per GPU, row-range shards), before any GPU
 call; under an external launcher WORLD_SIZE must equal --gpus."""
 import json
+import time
 import os
 import subprocess
 import sys
@@ -235,3 +236,84 @@ def free_port_local():
 def test_unknown_config_exits_before_any_gpu_work():
     r = run_bench(["--configs", "C2,C9"])
     assert r.returncode == 2 and "C9" in r.stderr and not r.stdout.strip()
+
+
+# ---- graph-phase fallback: fake workers, no GPU --------
+
+def _line(stdout):
+    lines = [json.loads(x) for x in stdout.splitlines() if x.strip().startswith("{")]
+    assert len(lines) == 1, stdout
+    return lines[0]
+
+
+def test_local_launcher_relaunches_eager_after_a_graph_phase_failure():
+    """rank 1's first attempt exits GRAPH_EXIT (its graph replay 'hung'), rank
+    0 waits as if inside a collective: the launcher stops it, starts fresh
+    ranks once with --graph-steps 0 and relays their line, marked"""
+    t0 = time.time()
+    r = run_bench(["--gpus", "2"], {"MBX_BENCH_FAKE": "graph:1"})
+    assert r.returncode == 0, r.stderr
+    x = _line(r.stdout)
+    assert x["graph_steps"] == 0 and x["n_gpus"] == 2
+    assert x["exchange_form"].startswith("eager (graph replay failed: rank 1: C3: first replay"), x
+    assert "fresh ranks, eager steps" in r.stderr
+    assert time.time() - t0 < 50  # rank 0 was stopped, not waited for
+
+
+def test_local_launcher_without_failure_keeps_graphs():
+    r = run_bench(["--gpus", "4"], {"MBX_BENCH_FAKE": "ok"})
+    assert r.returncode == 0, r.stderr
+    x = _line(r.stdout)
+    assert x["graph_steps"] == 20 and x["exchange_form"].startswith("HIP graphs of 20 steps")
+
+
+def test_other_failures_are_not_retried():
+    r = run_bench(["--gpus", "2"], {"MBX_BENCH_FAKE": "fail:1"})
+    assert r.returncode == 7 and not r.stdout.strip()
+    assert "fresh ranks" not in r.stderr
+
+
+def _torchrun(n, env_extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port_local()), BENCH, "--gpus", str(n)]
+    return subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+
+
+@pytest.mark.parametrize("bad", ["0", "1"])
+def test_torchrun_supervisors_relaunch_eager_after_a_graph_phase_failure(bad):
+    """the driver's N > 1 form (python -m torch.distributed.run ... bench.py
+    --gpus N): each rank process supervises one worker; a graph-phase failure
+    on any rank gives one eager relaunch on every rank and one line"""
+    r = _torchrun(2, {"MBX_BENCH_FAKE": f"graph:{bad}"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    x = _line(r.stdout)
+    assert x["graph_steps"] == 0 and x["n_gpus"] == 2
+    assert x["exchange_form"].startswith(f"eager (graph replay failed: rank {bad}: C3"), x
+
+
+def test_torchrun_supervisors_pass_through_success_and_failure():
+    r = _torchrun(2, {"MBX_BENCH_FAKE": "ok"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _line(r.stdout)["graph_steps"] == 20
+    r = _torchrun(2, {"MBX_BENCH_FAKE": "fail:1"})
+    assert r.returncode != 0 and not r.stdout.strip()
+
+
+def test_phase_clock_exits_with_the_phase_code():
+    """PhaseClock: a phase that outlives its budget prints its name and every
+    thread's traceback and exits with the phase's code (GRAPH_EXIT for a
+    graph replay, after writing its reason to $MBX_BENCH_STATUS)"""
+    import tempfile
+    status = os.path.join(tempfile.mkdtemp(), "s.txt")
+    code = (f"import sys, time; sys.path.insert(0, {ROOT!r}); import bench; c = bench.PhaseClock(); "
+            "c.arm('C3: first replay of 1 captured graph(s)', 0.3, bench.GRAPH_EXIT); time.sleep(30)")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, MBX_BENCH_STATUS=status))
+    assert r.returncode == 4 and "outlived its budget" in r.stderr and "Thread" in r.stderr, r.stderr
+    with open(status) as f:
+        assert f.read().startswith("C3: first replay of 1 captured graph(s): did not finish")
+    b = _bench_module()
+    assert b.GRAPH_WAIT_S <= 60 and sum(b.PHASE_S.values()) < 1000

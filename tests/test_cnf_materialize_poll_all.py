@@ -1,11 +1,9 @@
 """k_cnf_select's every-predecessor look-back (the form tables of >= 2^32
 rows take, where the chained look-back's 32-bit inclusive prefixes would
 overflow), forced on a context of its own by the select_dbg knob
-(MBX_SELECT_DBG=128, read at mbx_init): the same numpy / two-call checks as
+(mbx_set_tuning "select_dbg" 128 on that context): the same numpy / two-call checks as
 tests/test_cnf_materialize.py (R/index/ColumnarIndexScan.java:130-181,
 :287-308)."""
-import os
-
 import pytest
 
 import mbx_pkg
@@ -21,15 +19,8 @@ def m():
 
 @pytest.fixture(scope="module")
 def ctx(m):
-    old = os.environ.get("MBX_SELECT_DBG")
-    os.environ["MBX_SELECT_DBG"] = "128"
-    try:
-        c = m.Context(0)
-    finally:
-        if old is None:
-            os.environ.pop("MBX_SELECT_DBG")
-        else:
-            os.environ["MBX_SELECT_DBG"] = old
+    c = m.Context(0)
+    c.set_tuning("select_dbg", 128)
     yield c
     c.close()
 
