@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The C3 scan exactly as bench.py launches it on rank 0 of an N-rank run,
-for rocprofv3 kernel-trace / PMC passes (tools/gpu_r4_shard_pmc.sh): rank 0's
+for rocprofv3 kernel-trace / PMC passes (profiles/r04/scripts/gpu_r4_shard_pmc.sh): rank 0's
 row-range shard of the 100M-row table (mbx_shard_bounds), 4 x int32 columns,
 {(c0 < 2^19)} ^ {(c1 >= 2^19)}, COUNT in the same form bench.py picks at that
 N (in-launch finalize at N = 1, count frame with an exchange).

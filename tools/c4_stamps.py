@@ -4,7 +4,7 @@
 start / count published / offset known / end (tuning select_dbg bit 3,
 mbx_diag_select_stamps), as percentiles in us from the earliest block start,
 for a projection and for positions only.  The stamps' own stores move the
-times a little; the kernel time without them is tools/c4_forms.py's."""
+times a little; the kernel time without them is profiles/r05/scripts/c4_forms.py's."""
 import json
 import os
 import sys

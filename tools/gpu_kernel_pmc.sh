@@ -1,6 +1,6 @@
 # Kernel trace + FETCH_SIZE + WRITE_SIZE passes (separate runs) over one
 # command, summarised per kernel by tools/kernel_pmc_table.py.
-#   CMD="python3 tools/small_sweep.py --rows 100000000 --tpb 0 --rounds 1" TAG=... bash tools/gpu_kernel_pmc.sh
+#   CMD="tools/c4_req_probe 100000000 10 10" TAG=... bash tools/gpu_kernel_pmc.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
