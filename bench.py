@@ -54,19 +54,36 @@ heap C3 leaves, profiles/r05/m):
 Each is checked against torch reductions of the same device data before
 and after its timing.  stdout carries only the JSON line.  A rank still
 running --watchdog seconds (420) after its imports prints its threads'
-tracebacks and exits 1.
+tracebacks and exits 1 (the backstop behind the per-phase deadlines).
+cpu_baseline (N = 1, rank 0): the oracle over the GPU run's own C3 table,
+copied to host after timing; its COUNT must equal the GPU's.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak] [--configs C2,C4,C5|none]
 
 Launch: with WORLD_SIZE unset and --gpus N > 1, this process is only a
-launcher: before anything touches a GPU it starts N rank processes of this
-same script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
-MASTER_PORT in their env), relays rank 0's JSON line and exits with the
-first failing rank's status (the others are then stopped by PID).  Under an
-external torch.distributed.run, WORLD_SIZE must equal --gpus.
+launcher: before anything touches a GPU it starts N rank ("worker")
+processes of this same script (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT in their env); rank 0's stdout is the
+JSON line; it exits with the first failing rank's status (the others are
+then stopped by PID).  Under an external torch.distributed.run (WORLD_SIZE
+set, must equal --gpus) each rank process is a supervisor of ONE worker,
+the supervisors sharing exit codes through a TCPStore.  Neither launcher nor
+supervisor touches a GPU; workers die with them (PR_SET_PDEATHSIG).
+
+Graph-phase fallback: before timing, the first replay of every set of
+captured graphs (scans + their RCCL exchange) is waited for against a 60 s
+deadline (a HIP event polled) and its steps verified on every rank; a hang or
+a wrong result exits 4 (GRAPH_EXIT) with its reason, and the launcher /
+supervisors start fresh workers ONCE with --graph-steps 0 (every step eager);
+the line then says `"exchange_form": "eager (graph replay failed: ...)"`.
+Each phase (setup, each C3 run, probe, each config, cpu baseline) re-arms a
+deadline of its own (PHASE_S).
 --dry-launch: the ranks print their rank env as JSON and exit before
 importing torch (the launcher's CPU test, tests/test_bench_launch.py).
-Rehearsal knobs (never set by the driver): MBX_BENCH_SAME_DEVICE=1 (N ranks on
+Rehearsal knobs (never set by the driver): MBX_BENCH_FORCE_GRAPH_FAIL=verify|timeout
+(rank 0 reports that graph-phase failure: the fallback must follow),
+MBX_BENCH_FAKE=graph:R|fail:R|ok (workers that touch no GPU, for the
+launcher tests), MBX_BENCH_SAME_DEVICE=1 (N ranks on
 one GPU, gloo exchange), MBX_BENCH_FORCE_EXCHANGE=1 (the exchange at N = 1),
 MBX_BENCH_CORRUPT=frame|count (rank 0 damages its pre-check frame: the
 pre-check must fire), MBX_BENCH_TORCH_EXCHANGE=1 (the fallback exchange --
@@ -201,6 +218,29 @@ def worker_cmd(argv):
     return [sys.executable, os.path.abspath(__file__)] + list(argv)
 
 
+def die_with_parent():
+    """Popen preexec_fn (runs in the child before exec, long before any GPU
+    call): the worker gets SIGKILL when its launcher / supervisor dies, so a
+    launcher stopped by the driver's clock or by torch.distributed.run never
+    leaves a rank holding a GPU"""
+    import ctypes
+    import signal
+    ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGKILL))  # PR_SET_PDEATHSIG
+
+
+def forward_term(procs):
+    """SIGTERM / SIGINT to this launcher stop its workers too, then exit"""
+    import signal
+
+    def handler(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        os._exit(128 + signum)
+    signal.signal(signal.SIGTERM, handler)
+    signal.signal(signal.SIGINT, handler)
+
+
 def run_local_attempt(n, argv, env_extra, status_dir, attempt):
     """n worker processes on this node; returns (status, failing rank): 0 or
     the first failing rank's exit status, the others stopped by PID.  Rank
@@ -215,7 +255,8 @@ def run_local_attempt(n, argv, env_extra, status_dir, attempt):
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MBX_BENCH_WORKER="1",
                    MBX_BENCH_STATUS=os.path.join(status_dir, f"a{attempt}_rank{r}.txt"), **env_extra)
         out = None if (r == 0 or dry) else sys.stderr
-        procs.append(subprocess.Popen(worker_cmd(argv), env=env, stdout=out))
+        procs.append(subprocess.Popen(worker_cmd(argv), env=env, stdout=out, preexec_fn=die_with_parent))
+    forward_term(procs)
     status, bad = 0, None
     codes = {}
     live = list(procs)
@@ -290,7 +331,9 @@ def supervise_rank(argv):
             env = dict(os.environ, MASTER_PORT=port, MBX_BENCH_WORKER="1",
                        MBX_BENCH_STATUS=os.path.join(status_dir, f"a{attempt}.txt"), **extra)
             env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the workers' store is hosted by rank 0's worker
-            p = subprocess.Popen(worker_cmd(args_now), env=env, stdout=None if rank == 0 else sys.stderr)
+            p = subprocess.Popen(worker_cmd(args_now), env=env, stdout=None if rank == 0 else sys.stderr,
+                                 preexec_fn=die_with_parent)
+            forward_term([p])
             peers = [key(attempt, r) for r in range(world) if r != rank]
             killed = False
             while p.poll() is None:
@@ -487,8 +530,15 @@ def config_record(workload, rows, rows_per_gpu, gpus, selected, ms_per_query, ke
            "algorithmic_bytes_per_launch": algo_bytes, "achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS,
            "exchange": exchange, "pre_check": pre_check, "timing": timing,
            "traffic": traffic, "traffic_over_algorithmic": traffic / algo_bytes if traffic and algo_bytes else None,
+           # the bytes the kernel really moves per launch over its time: for C4's
+           # random rows every selected row costs a whole 128-byte line
+           # (profiles/r06/c4_req), so its frac of algorithmic bytes is low while
+           # this one is not
+           "traffic_gbs": traffic / (kernel_ms * 1e-3) / 1e9 if traffic and kernel_ms > 0 else None,
+           "traffic_frac": traffic / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic and kernel_ms > 0 else None,
            "traffic_unit": "HBM bytes per launch of rank 0's kernel at this shard size (rocprofv3 PMC, "
-                           "profiles/config_pmc.json)"}
+                           "profiles/config_pmc.json: read = gfx950's request-size split 32 n32 + 64 n64 + 128 n128, "
+                           "write = WRITE_SIZE)"}
     rec.update(extra)
     return rec
 

@@ -285,7 +285,8 @@ int mbx_bitmap_select(mbx_ctx *ctx, const mbx_bitmap *b, int64_t row_offset, int
                       int64_t cap, int64_t *n);
 /* positions + projected column values of every selected row, column-major
  * into host buffers (proj: 0-based columns; value layout as in
- * mbx_table_stage; ids may be NULL) */
+ * mbx_table_stage; ids may be NULL).  All *n rows, however large: the rows
+ * cross PCIe in cursor batches of <= 64 MiB, each copied to its offset. */
 int mbx_materialize(mbx_ctx *ctx, const mbx_table *t, const mbx_bitmap *sel, const int32_t *proj,
                     int32_t nproj, int64_t *host_ids, void *const *host_out, int64_t cap, int64_t *n);
 /* device-side variant (outputs stay in HBM: dev_ids / dev_out[j] of `cap` rows) */

@@ -317,3 +317,23 @@ def test_phase_clock_exits_with_the_phase_code():
         assert f.read().startswith("C3: first replay of 1 captured graph(s): did not finish")
     b = _bench_module()
     assert b.GRAPH_WAIT_S <= 60 and sum(b.PHASE_S.values()) < 1000
+
+
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGKILL"])
+def test_workers_die_with_their_launcher(sig):
+    """a launcher stopped from outside (the driver's clock, torch.distributed.run
+    tearing a failed group down) leaves no rank behind: SIGTERM is forwarded and
+    every worker carries PR_SET_PDEATHSIG"""
+    import signal
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MBX_BENCH_FAKE"] = "fail:9"  # no rank fails: every rank waits 60 s
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2"], env=env, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    time.sleep(3)
+    kids = subprocess.run(["pgrep", "-P", str(p.pid)], capture_output=True, text=True).stdout.split()
+    assert len(kids) == 2, kids
+    p.send_signal(getattr(signal, sig))
+    p.wait(timeout=30)
+    time.sleep(1)
+    for k in kids:
+        assert not os.path.exists(f"/proc/{k}") or open(f"/proc/{k}/stat").read().split()[2] == "Z", k

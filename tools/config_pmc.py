@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
 """profiles/config_pmc.json: HBM bytes per launch of each config record's
-kernel (bench.py `configs.*.traffic`), from a tools/gpu_r5_e.sh run: the
-per-kernel table of rocprofv3 FETCH_SIZE / WRITE_SIZE passes over a short
-bench.py (tools/kernel_pmc_table.py: read = FETCH_SIZE x 2 x 1024, the gfx950
-correction, write = WRITE_SIZE x 1024) and that run's bench line (the rows
-per GPU each config ran at).
-    python3 tools/config_pmc.py profiles/r05/e/kernels.jsonl profiles/r05/e/bench_n1.json"""
+kernel (bench.py `configs.*.traffic`), from the per-kernel table of rocprofv3
+passes over a short bench.py (tools/kernel_pmc_table.py) and that run's bench
+line (the rows per GPU each config ran at).  Read bytes come from gfx950's
+read-request size split (TCC_EA0_RDREQ_32B / _64B / _128B: 32 n32 + 64 n64 +
+128 n128) when the table has it -- the x 2 correction of FETCH_SIZE is then
+not applied anywhere; it is the fallback only for tables without the split
+(round 5's).  Write bytes = WRITE_SIZE x 1024 (64-byte write requests,
+exact: profiles/r06/c4_req).
+    python3 tools/config_pmc.py profiles/r06/b/kernels.jsonl profiles/r06/b/bench_pmc.json"""
 import json
 import os
 import sys
@@ -26,6 +29,8 @@ def main():
         hbm = (k["read_MB"] + k["write_MB"]) * 1e6
         out["configs"][f"{name}:{rec['rows_per_gpu']}"] = {
             "kernel": k["kernel"], "dispatches": k["dispatches"], "avg_us": k["avg_us"],
+            "read_basis": k.get("read_basis"), "read_128B_share": k.get("read_128B_share"),
+            "fetch_x2_bytes_per_launch": k["fetch_x2_MB"] * 1e6 if "fetch_x2_MB" in k else None,
             "read_bytes_per_launch": k["read_MB"] * 1e6, "write_bytes_per_launch": k["write_MB"] * 1e6,
             "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": rec["algorithmic_bytes_per_launch"],
             "traffic_over_algorithmic": hbm / rec["algorithmic_bytes_per_launch"]}
