@@ -189,21 +189,23 @@ def free_port():
 
 # ---------------------------------------------------------------- launchers
 # Neither launcher touches a GPU: they only start rank ("worker") processes,
-# watch their exit codes and, once, start fresh ones.  A worker that finds the
-# first replay of a captured graph (the timed steps' form: scans + their RCCL
-# exchange) hung or wrong exits GRAPH_EXIT after writing a one-line reason to
-# $MBX_BENCH_STATUS; the launcher then stops every rank and starts fresh rank
-# processes ONCE with --graph-steps 0 (every step eager, the same exchange
-# issued step by step), and $MBX_BENCH_FALLBACK carries the reason into the
-# line's `exchange_form`.  Any other failure is final.
+# watch their exit codes and start fresh ones on two failures that another
+# exchange form avoids.  The failing worker writes a one-line reason to
+# $MBX_BENCH_STATUS and exits with the failure's code:
+#   GRAPH_EXIT  the first replay of the captured graphs (the timed steps' form:
+#               scans + their RCCL exchange) hung or was wrong -> relaunch with
+#               --graph-steps 0 (every step eager, the same collective issued
+#               step by step); $MBX_BENCH_FALLBACK carries the reason
+#   COMM_EXIT   the RCCL exchange itself failed: its communicators did not come
+#               up (in time), or the first exchanged step hung / was wrong ->
+#               relaunch with $MBX_BENCH_HOST_EXCHANGE=<reason>: the exchange
+#               as a gloo collective over host copies (the GPU work unchanged)
+# Each fallback is taken at most once (at most 3 attempts); the line's
+# `exchange_form` names what ran and why.  Any other failure is final.
 
 GRAPH_EXIT = 4
+COMM_EXIT = 6
 KILLED = -9
-
-
-def fallback_argv(argv):
-    """the relaunch's arguments: the same, every step eager"""
-    return list(argv) + ["--graph-steps", "0"]
 
 
 def read_reason(path):
@@ -212,6 +214,40 @@ def read_reason(path):
             return f.read().strip().splitlines()[0][:300]
     except (OSError, IndexError):
         return "no reason recorded"
+
+
+def next_attempt(codes, argv, env, who):
+    """The fallback after an attempt whose ranks ended with `codes` [(rank,
+    exit code, reason)]: (argv, env) of the next attempt, or None when the
+    status is final.  A failure whose fallback was already taken is final."""
+    retry = [(r, c, why) for r, c, why in codes
+             if (c == GRAPH_EXIT and "MBX_BENCH_FALLBACK" not in env)
+             or (c == COMM_EXIT and "MBX_BENCH_HOST_EXCHANGE" not in env)]
+    if not retry:
+        return None
+    own = [x for x in retry if not x[2].startswith("another rank")]
+    r, c, why = (own or retry)[0]
+    env = dict(env)
+    if c == GRAPH_EXIT:
+        env["MBX_BENCH_FALLBACK"] = f"rank {r}: {why}"
+        argv = list(argv) + ["--graph-steps", "0"]
+        what = "fresh ranks, eager steps"
+    else:
+        env["MBX_BENCH_HOST_EXCHANGE"] = f"rank {r}: {why}"
+        what = "fresh ranks, host exchange"
+    if who:
+        print(f"bench {who}: {'graph replay' if c == GRAPH_EXIT else 'RCCL exchange'} failed on rank {r} ({why}); "
+              f"{what}", file=sys.stderr, flush=True)
+    return argv, env
+
+
+def final_status(codes):
+    """0, or the exit status of the first rank that failed on its own (not
+    killed for a peer's failure)"""
+    fails = [c for _, c, _ in codes if c not in (0, KILLED)]
+    if fails:
+        return fails[0] if fails[0] > 0 else 128 - fails[0]
+    return 1 if any(c == KILLED for _, c, _ in codes) else 0
 
 
 def worker_cmd(argv):
@@ -242,23 +278,24 @@ def forward_term(procs):
 
 
 def run_local_attempt(n, argv, env_extra, status_dir, attempt):
-    """n worker processes on this node; returns (status, failing rank): 0 or
-    the first failing rank's exit status, the others stopped by PID.  Rank
-    0's stdout is this process's (the JSON line), the others' go to stderr
-    (--dry-launch: every rank's to stdout)."""
+    """n worker processes on this node; returns [(rank, exit code, reason)]
+    once all ended: the first failure stops the others by PID (their code is
+    then KILLED).  Rank 0's stdout is this process's (the JSON line), the
+    others' go to stderr (--dry-launch: every rank's to stdout)."""
     import subprocess
     port = free_port()
     dry = "--dry-launch" in argv
-    procs = []
+    procs, status = [], []
     for r in range(n):
+        st = os.path.join(status_dir, f"a{attempt}_rank{r}.txt")
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MBX_BENCH_WORKER="1",
-                   MBX_BENCH_STATUS=os.path.join(status_dir, f"a{attempt}_rank{r}.txt"), **env_extra)
+                   MBX_BENCH_STATUS=st, **env_extra)
         out = None if (r == 0 or dry) else sys.stderr
         procs.append(subprocess.Popen(worker_cmd(argv), env=env, stdout=out, preexec_fn=die_with_parent))
+        status.append(st)
     forward_term(procs)
-    status, bad = 0, None
-    codes = {}
+    codes, killed, failed = {}, set(), False
     live = list(procs)
     while live:
         for p in list(live):
@@ -266,19 +303,17 @@ def run_local_attempt(n, argv, env_extra, status_dir, attempt):
             if rc is None:
                 continue
             live.remove(p)
-            codes[procs.index(p)] = rc
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 128 - rc
-                bad = procs.index(p)
-                print(f"bench launcher: rank {bad} exited with {rc}; stopping the others", file=sys.stderr)
+            r = procs.index(p)
+            codes[r] = KILLED if r in killed else rc
+            if rc != 0 and not failed and r not in killed:
+                failed = True
+                print(f"bench launcher: rank {r} exited with {rc}; stopping the others", file=sys.stderr)
                 for q in live:
+                    killed.add(procs.index(q))
                     q.kill()
         time.sleep(0.05)
-    # a graph-phase failure wins over the peers it left failing in a collective
-    graph = [r for r in sorted(codes) if codes[r] == GRAPH_EXIT]
-    if graph:
-        return GRAPH_EXIT, graph[0]
-    return status, bad
+    return [(r, codes[r], read_reason(status[r]) if codes[r] in (GRAPH_EXIT, COMM_EXIT) else "")
+            for r in range(n)]
 
 
 def launch_ranks(n, argv):
@@ -287,14 +322,14 @@ def launch_ranks(n, argv):
     import tempfile
     status_dir = tempfile.mkdtemp(prefix="mbx_bench_")
     try:
-        status, bad = run_local_attempt(n, argv, {}, status_dir, 0)
-        if status == GRAPH_EXIT:
-            reason = read_reason(os.path.join(status_dir, f"a0_rank{bad}.txt"))
-            print(f"bench launcher: graph replay failed on rank {bad} ({reason}); fresh ranks, eager steps",
-                  file=sys.stderr, flush=True)
-            status, _ = run_local_attempt(n, fallback_argv(argv), {"MBX_BENCH_FALLBACK": f"rank {bad}: {reason}"},
-                                          status_dir, 1)
-        return status
+        env = {}
+        for attempt in range(3):
+            codes = run_local_attempt(n, argv, env, status_dir, attempt)
+            nxt = next_attempt(codes, argv, env, "launcher")
+            if nxt is None:
+                return final_status(codes)
+            argv, env = nxt
+        return final_status(codes)
     finally:
         shutil.rmtree(status_dir, ignore_errors=True)
 
@@ -304,10 +339,11 @@ def supervise_rank(argv):
     MASTER_* set), this process supervises ONE worker: it starts it, shares
     its exit code with the other ranks' supervisors through a TCPStore (torch
     run's own agent store when TORCHELASTIC_USE_AGENT_STORE, else one hosted by
-    rank 0), stops its worker when another rank's worker failed, and on a
-    graph-phase failure anywhere every supervisor starts one fresh worker with
-    --graph-steps 0.  Workers rendezvous on a fresh port per attempt (rank 0's
-    worker hosts that store).  Returns the exit status."""
+    rank 0), stops its worker when another rank's worker failed, and after a
+    graph-phase or exchange failure anywhere every supervisor starts one fresh
+    worker with the same fallback (next_attempt: every supervisor sees the same
+    codes, so all decide alike).  Workers rendezvous on a fresh port per
+    attempt (rank 0's worker hosts that store).  Returns the exit status."""
     import datetime
     import shutil
     import subprocess
@@ -324,7 +360,7 @@ def supervise_rank(argv):
     status_dir = tempfile.mkdtemp(prefix="mbx_bench_")
     extra, args_now = {}, list(argv)
     try:
-        for attempt in (0, 1):
+        for attempt in range(3):
             if rank == 0:
                 store.set(f"mbx_bench/{run_id}/a{attempt}/port", str(free_port()))
             port = store.get(f"mbx_bench/{run_id}/a{attempt}/port").decode()
@@ -338,14 +374,14 @@ def supervise_rank(argv):
             killed = False
             while p.poll() is None:
                 for k in peers:  # a peer's worker already failed: this one would wait on it
-                    if store.check([k]) and not store.get(k).decode().startswith("0|"):
+                    if store.check([k]) and not store.get(k).decode().startswith(("0|", f"{KILLED}|")):
                         p.kill()
                         killed = True
                         break
                 time.sleep(0.1)
             rc = p.wait()
             rc = KILLED if killed else rc
-            reason = read_reason(env["MBX_BENCH_STATUS"]) if rc == GRAPH_EXIT else ""
+            reason = read_reason(env["MBX_BENCH_STATUS"]) if rc in (GRAPH_EXIT, COMM_EXIT) else ""
             store.set(key(attempt, rank), f"{rc}|{reason}")
             deadline = time.time() + 600
             while not store.check([key(attempt, r) for r in range(world)]):
@@ -357,49 +393,45 @@ def supervise_rank(argv):
             for r in range(world):
                 c, _, why = store.get(key(attempt, r)).decode().partition("|")
                 codes.append((r, int(c), why))
-            graph = [(r, why) for r, c, why in codes if c == GRAPH_EXIT]
-            if graph and attempt == 0:
-                r0, why = graph[0]
-                if rank == 0:
-                    print(f"bench supervisor: graph replay failed on rank {r0} ({why}); fresh workers, eager steps",
-                          file=sys.stderr, flush=True)
-                extra = {"MBX_BENCH_FALLBACK": f"rank {r0}: {why}"}
-                args_now = fallback_argv(argv)
-                continue
-            fails = [c for _, c, _ in codes if c not in (0, KILLED)]
-            if fails:
-                return fails[0] if fails[0] > 0 else 128 - fails[0]
-            return 1 if any(c == KILLED for _, c, _ in codes) else 0
-        return 1
+            nxt = next_attempt(codes, args_now, extra, "supervisor" if rank == 0 else None)
+            if nxt is None:
+                return final_status(codes)
+            args_now, extra = nxt
+        return final_status(codes)
     finally:
         shutil.rmtree(status_dir, ignore_errors=True)
 
 
 def fake_worker(args, world, rank):
-    """MBX_BENCH_FAKE=graph:R (launcher tests, no GPU): rank R's first attempt
-    fails its graph phase, the other ranks wait as if inside a collective; the
-    eager relaunch prints a line as rank 0 would."""
-    mode, _, who = os.environ["MBX_BENCH_FAKE"].partition(":")
-    fallback = os.environ.get("MBX_BENCH_FALLBACK")
-    if mode == "graph" and args.graph_steps and not fallback:
-        if str(rank) == who:
-            time.sleep(0.5)
-            graph_failed("C3: first replay of the captured graphs did not finish within 60 s (fake)")
-        time.sleep(60)
-        sys.exit(1)
-    if mode == "fail":  # any other failure is final
+    """MBX_BENCH_FAKE=<modes>:R (launcher tests, no GPU).  Modes, '+'-joined:
+    graph (rank R's graph phase fails until the eager fallback), comm (its
+    exchange fails until the host fallback), fail (it exits 7: final); the
+    other ranks wait as if inside a collective.  A rank with nothing left to
+    fail prints a line as rank 0 would."""
+    modes, _, who = os.environ["MBX_BENCH_FAKE"].partition(":")
+    modes = modes.split("+")
+    fallback, host = os.environ.get("MBX_BENCH_FALLBACK"), os.environ.get("MBX_BENCH_HOST_EXCHANGE")
+    pending = [m for m in modes if (m == "graph" and args.graph_steps and not fallback)
+               or (m == "comm" and not host) or m == "fail"]
+    if pending:
         time.sleep(0.5)
         if str(rank) == who:
+            m = pending[0]
+            if m == "graph":
+                fail_exit(GRAPH_EXIT, "C3: first replay of the captured graphs did not finish within 60 s (fake)")
+            if m == "comm":
+                fail_exit(COMM_EXIT, "communicators: ncclCommInitRank did not return within 120 s (fake)")
             sys.exit(7)
         time.sleep(60)
         sys.exit(1)
     if rank == 0:
         print(json.dumps({"fake": True, "n_gpus": world, "graph_steps": args.graph_steps,
-                          "exchange_form": exchange_form(args.graph_steps, fallback)}), flush=True)
+                          "exchange_form": exchange_form(args.graph_steps, fallback, host)}), flush=True)
 
 
-def graph_failed(reason):
-    """a graph-phase failure: the reason into $MBX_BENCH_STATUS, exit GRAPH_EXIT"""
+def fail_exit(code, reason):
+    """a failure the launcher may answer with a fallback: the reason into
+    $MBX_BENCH_STATUS, then exit `code`"""
     path = os.environ.get("MBX_BENCH_STATUS")
     if path:
         try:
@@ -407,12 +439,20 @@ def graph_failed(reason):
                 f.write(reason + "\n")
         except OSError:
             pass
-    print(f"bench: graph phase failed: {reason}", file=sys.stderr, flush=True)
+    what = {GRAPH_EXIT: "graph phase", COMM_EXIT: "exchange"}.get(code, "run")
+    print(f"bench: {what} failed: {reason}", file=sys.stderr, flush=True)
     sys.stderr.flush()
-    os._exit(GRAPH_EXIT)
+    os._exit(code)
 
 
-def exchange_form(graph_steps, fallback):
+def graph_failed(reason):
+    fail_exit(GRAPH_EXIT, reason)
+
+
+def exchange_form(graph_steps, fallback, host=None):
+    if host:
+        form = f"host gloo exchange of the device results, eager (RCCL exchange failed: {host})"
+        return form + (f"; earlier, graph replay failed: {fallback}" if fallback else "")
     if fallback:
         return f"eager (graph replay failed: {fallback})"
     return f"HIP graphs of {graph_steps} steps (first replay verified)" if graph_steps else "eager"
@@ -421,7 +461,8 @@ def exchange_form(graph_steps, fallback):
 class PhaseClock:
     """Per-phase deadlines: a daemon thread that, when the armed phase outlives
     its budget, prints the phase and every thread's traceback and exits with
-    the phase's code (GRAPH_EXIT for a graph replay, 1 otherwise).  Ctypes and
+    the phase's code (GRAPH_EXIT for a graph replay, COMM_EXIT for the
+    exchange's setup and first use, 1 otherwise).  Ctypes and
     torch calls release the GIL while they wait, so the thread runs while the
     main thread is stuck in a HIP / RCCL call; faulthandler's --watchdog stays
     as the backstop for a wait that holds the GIL."""
@@ -446,12 +487,12 @@ class PhaseClock:
             if late:
                 print(f"bench: phase `{phase}` outlived its budget", file=sys.stderr, flush=True)
                 faulthandler.dump_traceback(all_threads=True)
-                if code == GRAPH_EXIT:
-                    graph_failed(f"{phase}: did not finish within its budget")
+                if code in (GRAPH_EXIT, COMM_EXIT):
+                    fail_exit(code, f"{phase}: did not finish within its budget")
                 os._exit(code)
 
 
-PHASE_S = {"setup": 240, "c3": 120, "probe": 60, "config": 150, "cpu": 120}
+PHASE_S = {"comm": 120, "setup": 180, "c3": 120, "probe": 60, "config": 150, "cpu": 120}
 GRAPH_WAIT_S = 60.0
 CLOCK = None
 
@@ -577,11 +618,13 @@ def make_parser():
     return ap
 
 
-def agree(torch, dist, world, rank, reason):
+def agree(torch, dist, world, rank, reason, code=PRECHECK_EXIT):
     """A collective verdict: every rank learns whether any rank's check
     failed (reason not None); then each failing rank prints its one-line
-    reason, the others a line naming the cause, and ALL exit PRECHECK_EXIT --
-    no rank is left waiting in a later collective."""
+    reason, the others a line naming the cause, and ALL exit `code`
+    (PRECHECK_EXIT; COMM_EXIT for the first exchanged step, which the
+    launcher answers with the host exchange) -- no rank is left waiting in a
+    later collective."""
     bad = int(reason is not None)
     if world > 1:
         t = torch.tensor([bad], dtype=torch.int32)
@@ -593,6 +636,8 @@ def agree(torch, dist, world, rank, reason):
         print(f"bench: pre-check failed on rank {rank}: {reason}" if reason else
               f"bench: rank {rank} stops: another rank's pre-check failed", file=sys.stderr, flush=True)
         sys.stderr.flush()
+        if code != PRECHECK_EXIT:
+            fail_exit(code, reason or "another rank's pre-check failed")
         os._exit(PRECHECK_EXIT)
 
 
@@ -637,8 +682,8 @@ class Harness:
         self.dist.all_reduce(t)
         return int(t[0])
 
-    def agree(self, reason):
-        agree(self.torch, self.dist, self.world, self.rank, reason)
+    def agree(self, reason, code=PRECHECK_EXIT):
+        agree(self.torch, self.dist, self.world, self.rank, reason, code)
 
     def graphs(self, enqueue, k0, k1, per):
         """HIP graphs of `per` steps each covering steps k0..k1-1 (None when
@@ -814,7 +859,12 @@ def run_c3(H, args, cols, n, s, glob, label, bucket=None):
     `args.steps` timed steps (graph replay), kernel time, every step's count
     checked.  Returns the measurements (the table stays open for the probe)."""
     torch, ctx, m, world, rank = H.torch, H.ctx, H.m, H.world, H.rank
-    arm(f"{label}: pre-check, graph capture", PHASE_S["c3"])
+    # the first exchanged step of the run is the exchange's first use: a hang or
+    # a wrong global result there is an exchange failure (COMM_EXIT: the
+    # launcher's host-exchange fallback), later ones are ordinary failures
+    rccl = H.comm is not None or H.torch_pg is not None
+    first_use = rccl and label == "C3"
+    arm(f"{label}: pre-check, graph capture", PHASE_S["c3"], COMM_EXIT if first_use else 1)
     table = ctx.wrap([(m.mbx.INTEGER, 4)] * 4, [col.data_ptr() for col in cols], n, None, row_offset=s)
     cnf = [[(m.mbx.LT, ("sym", 1), ("int", THRESH))], [(m.mbx.GE, ("sym", 2), ("int", THRESH))]]
     plan = ctx.compile(table, cnf)
@@ -891,7 +941,8 @@ def run_c3(H, args, cols, n, s, glob, label, bucket=None):
     if corrupt and rank == 0:  # rehearsal: a damaged frame / count must stop the run here
         counts[0, 0] += (1 << 24) if (corrupt == "count" or not frames) else 1
         torch.cuda.synchronize()
-    H.agree(verify(0, 1, f"{label} pre-check"))
+    H.agree(verify(0, 1, f"{label} pre-check"), COMM_EXIT if first_use else PRECHECK_EXIT)
+    arm(f"{label}: graph capture", PHASE_S["c3"])
     counts.zero_()
     torch.cuda.synchronize()
 
@@ -922,7 +973,8 @@ def exchange_name(H, what):
     if H.torch_pg is not None:
         return "torch.distributed RCCL group (fallback: libmbx's communicator failed), eager"
     if H.exchange:
-        return "gloo (same-device rehearsal)"
+        return (f"gloo over host copies (fallback: the RCCL exchange failed: {H.host_reason})"
+                if getattr(H, "host_reason", None) else "gloo (same-device rehearsal)")
     return "none"
 
 
@@ -1214,6 +1266,7 @@ def main():
         fake_worker(args, world, rank)
         return
     fallback = os.environ.get("MBX_BENCH_FALLBACK")
+    host_reason = os.environ.get("MBX_BENCH_HOST_EXCHANGE")
     out_fd = quiet_stdout()
 
     import torch
@@ -1226,9 +1279,10 @@ def main():
         import faulthandler
         faulthandler.dump_traceback_later(args.watchdog, exit=True)
         CLOCK = PhaseClock()
-    arm("setup: communicators, tables", PHASE_S["setup"])
+    arm("setup: process group, context", PHASE_S["setup"])
 
     same_device = os.environ.get("MBX_BENCH_SAME_DEVICE") == "1"
+    host_xchg = same_device or bool(host_reason)  # the exchange as gloo over host copies
     device = 0 if same_device else local_rank
     torch.cuda.set_device(device)
     # MBX_BENCH_TORCH_EXCHANGE=1 (rehearsal): the fallback exchange
@@ -1240,7 +1294,7 @@ def main():
         # host-side bootstrap, barriers, verdicts and the max-over-ranks clock
         # only: the data-path exchange is libmbx's own RCCL communicator
         dist.init_process_group("gloo")
-    elif torch_exchange:
+    elif torch_exchange or (exchange and host_xchg):  # a one-rank group for the rehearsals' exchange at N = 1
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{free_port()}", rank=0, world_size=1)
     m = mbx_pkg.load()
     ctx = m.Context(device)
@@ -1248,7 +1302,13 @@ def main():
     comm = None
     torch_pg = None  # fallback exchange: torch.distributed's own RCCL group (eager)
     reason = None
-    if exchange and not same_device:
+    if exchange and not host_xchg:
+        # the RCCL exchange's setup: a hang or an error here is COMM_EXIT (the
+        # launcher's host-exchange fallback), as is MBX_BENCH_FORCE_COMM_FAIL=1
+        # on rank 0 (rehearsal)
+        arm("communicators: RCCL clique", PHASE_S["comm"], COMM_EXIT)
+        if os.environ.get("MBX_BENCH_FORCE_COMM_FAIL") == "1" and rank == 0:
+            fail_exit(COMM_EXIT, "communicators: forced failure (MBX_BENCH_FORCE_COMM_FAIL)")
         uid = m.mbx.comm_unique_id() if rank == 0 else None
         if world > 1:
             box = [uid]
@@ -1270,11 +1330,17 @@ def main():
                 if comm is not None:
                     comm.close()
                     comm = None
-                torch_pg = dist.new_group(backend="nccl")
+                try:
+                    torch_pg = dist.new_group(backend="nccl")
+                except Exception as err:  # neither RCCL form came up
+                    fail_exit(COMM_EXIT, f"communicators: libmbx ({reason or 'peer failed'}) and torch.distributed "
+                                         f"nccl ({type(err).__name__}: {err}) both failed")
                 reason = None
                 print(f"rank {rank}: exchange falls back to torch.distributed (nccl = RCCL)", file=sys.stderr)
     H = Harness(torch, dist, m, ctx, world, rank, comm, same_device, exchange, torch_pg)
-    H.agree(reason)
+    H.host_reason = host_reason
+    H.agree(reason, COMM_EXIT)
+    arm("setup: tables", PHASE_S["setup"])
 
     # ---- headline: C3 ------------------------------------------------------
     if args.scaling == "strong":
@@ -1366,7 +1432,9 @@ def main():
                       "after the step's scan on the same stream)")
                 if comm is not None else None) or (
             "torch.distributed RCCL all-reduce per step (fallback: libmbx's communicator failed), eager"
-            if torch_pg is not None else None) or ("gloo all-reduce (same-device rehearsal)" if exchange else "none")
+            if torch_pg is not None else None) or (
+            (f"gloo all-reduce over host copies (fallback: the RCCL exchange failed: {host_reason})" if host_reason
+             else "gloo all-reduce (same-device rehearsal)") if exchange else "none")
         out = {
             "metric": METRIC,
             "value": n_global * steps / (ms_per_step * 1e-3 * steps),
@@ -1397,7 +1465,7 @@ def main():
             },
             "pre_check": "ok: one exchanged step verified on every rank before timing" if exchange else
                          "ok: one step verified before timing",
-            "exchange_form": exchange_form(r3["G"], fallback),
+            "exchange_form": exchange_form(r3["G"], fallback, host_reason),
             "phases_us": {
                 "step_wall": ms_per_step * 1e3,
                 "scan_kernel_max_over_ranks": kern_max * 1e3,
@@ -1439,7 +1507,7 @@ def main():
 
     arm("teardown", 60)
     ctx.close()
-    if world > 1 or torch_exchange:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

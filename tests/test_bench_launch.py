@@ -337,3 +337,44 @@ def test_workers_die_with_their_launcher(sig):
     time.sleep(1)
     for k in kids:
         assert not os.path.exists(f"/proc/{k}") or open(f"/proc/{k}/stat").read().split()[2] == "Z", k
+
+
+@pytest.mark.parametrize("launch", ["local", "torchrun"])
+def test_exchange_failure_falls_back_to_the_host_exchange(launch):
+    """an RCCL exchange that does not come up (COMM_EXIT) -> fresh ranks with
+    the exchange as a gloo collective over host copies, marked in the line"""
+    env = {"MBX_BENCH_FAKE": "comm:1"}
+    r = run_bench(["--gpus", "2"], env) if launch == "local" else _torchrun(2, env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    x = _line(r.stdout)
+    assert x["graph_steps"] == 20  # the graph form is kept: only the exchange changed
+    assert x["exchange_form"].startswith("host gloo exchange of the device results, eager (RCCL exchange failed: "
+                                         "rank 1: communicators: ncclCommInitRank"), x
+
+
+@pytest.mark.parametrize("launch", ["local", "torchrun"])
+def test_both_fallbacks_in_turn(launch):
+    """graph replay fails first (eager relaunch), then the exchange itself
+    (host relaunch): three attempts, one line naming both"""
+    env = {"MBX_BENCH_FAKE": "graph+comm:0"}
+    r = run_bench(["--gpus", "2"], env) if launch == "local" else _torchrun(2, env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    x = _line(r.stdout)
+    assert x["graph_steps"] == 0
+    assert "RCCL exchange failed: rank 0: communicators" in x["exchange_form"]
+    assert "earlier, graph replay failed: rank 0: C3" in x["exchange_form"]
+
+
+def test_a_fallback_is_taken_once():
+    b = _bench_module()
+    codes = [(0, b.COMM_EXIT, "communicators: x"), (1, b.KILLED, "")]
+    argv, env = b.next_attempt(codes, ["--gpus", "2"], {}, None)
+    assert env["MBX_BENCH_HOST_EXCHANGE"] == "rank 0: communicators: x" and argv == ["--gpus", "2"]
+    assert b.next_attempt(codes, argv, env, None) is None            # the same failure again: final
+    assert b.final_status(codes) == b.COMM_EXIT
+    g = [(0, b.KILLED, ""), (1, b.GRAPH_EXIT, "another rank's first graph replay failed"),
+         (2, b.GRAPH_EXIT, "C4 first graph replay: x")]
+    argv2, env2 = b.next_attempt(g, argv, env, None)
+    assert argv2[-2:] == ["--graph-steps", "0"] and env2["MBX_BENCH_FALLBACK"] == "rank 2: C4 first graph replay: x"
+    assert b.next_attempt([(0, 7, ""), (1, b.KILLED, "")], argv, {}, None) is None
+    assert b.final_status([(0, 0, ""), (1, 0, "")]) == 0
