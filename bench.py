@@ -255,13 +255,18 @@ def worker_cmd(argv):
 
 
 def die_with_parent():
-    """Popen preexec_fn (runs in the child before exec, long before any GPU
-    call): the worker gets SIGKILL when its launcher / supervisor dies, so a
-    launcher stopped by the driver's clock or by torch.distributed.run never
-    leaves a rank holding a GPU"""
+    """A worker's first act (long before any GPU call): SIGKILL when its
+    launcher / supervisor dies (PR_SET_PDEATHSIG), so a launcher stopped by
+    the driver's clock or by torch.distributed.run never leaves a rank holding
+    a GPU; a parent already gone by then ends the worker at once.  Set here
+    rather than in a Popen preexec_fn, which is unsafe in a launcher with
+    threads (torch's TCPStore client)."""
     import ctypes
     import signal
     ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGKILL))  # PR_SET_PDEATHSIG
+    parent = os.environ.get("MBX_BENCH_PARENT")
+    if parent and os.getppid() != int(parent):
+        os._exit(1)
 
 
 def forward_term(procs):
@@ -290,9 +295,9 @@ def run_local_attempt(n, argv, env_extra, status_dir, attempt):
         st = os.path.join(status_dir, f"a{attempt}_rank{r}.txt")
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MBX_BENCH_WORKER="1",
-                   MBX_BENCH_STATUS=st, **env_extra)
+                   MBX_BENCH_PARENT=str(os.getpid()), MBX_BENCH_STATUS=st, **env_extra)
         out = None if (r == 0 or dry) else sys.stderr
-        procs.append(subprocess.Popen(worker_cmd(argv), env=env, stdout=out, preexec_fn=die_with_parent))
+        procs.append(subprocess.Popen(worker_cmd(argv), env=env, stdout=out))
         status.append(st)
     forward_term(procs)
     codes, killed, failed = {}, set(), False
@@ -364,11 +369,10 @@ def supervise_rank(argv):
             if rank == 0:
                 store.set(f"mbx_bench/{run_id}/a{attempt}/port", str(free_port()))
             port = store.get(f"mbx_bench/{run_id}/a{attempt}/port").decode()
-            env = dict(os.environ, MASTER_PORT=port, MBX_BENCH_WORKER="1",
+            env = dict(os.environ, MASTER_PORT=port, MBX_BENCH_WORKER="1", MBX_BENCH_PARENT=str(os.getpid()),
                        MBX_BENCH_STATUS=os.path.join(status_dir, f"a{attempt}.txt"), **extra)
             env.pop("TORCHELASTIC_USE_AGENT_STORE", None)  # the workers' store is hosted by rank 0's worker
-            p = subprocess.Popen(worker_cmd(args_now), env=env, stdout=None if rank == 0 else sys.stderr,
-                                 preexec_fn=die_with_parent)
+            p = subprocess.Popen(worker_cmd(args_now), env=env, stdout=None if rank == 0 else sys.stderr)
             forward_term([p])
             peers = [key(attempt, r) for r in range(world) if r != rank]
             killed = False
@@ -1245,6 +1249,8 @@ def main():
         print(f"bench: unknown config(s) {bad}", file=sys.stderr)
         sys.exit(2)
     worker = os.environ.get("MBX_BENCH_WORKER") == "1"
+    if worker:
+        die_with_parent()
     if "WORLD_SIZE" not in os.environ:
         if args.gpus > 1:
             sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
