@@ -31,7 +31,7 @@ def minidata():
 
 @pytest.fixture
 def tune(ctx):
-    """ctx.set_tuning for one test (the A/B knobs mbx_init otherwise reads
-    once from MBX_*), restored to the defaults afterwards."""
+    """ctx.set_tuning for one test (the A/B knobs; every context starts on
+    the production defaults), restored to the defaults afterwards."""
     yield ctx.set_tuning
     ctx.set_tuning("reset")
