@@ -140,7 +140,7 @@ def check_all(m, ctx, tune, t, ot, cols, cnf, rng):
 
 
 @pytest.mark.parametrize("n", [1, 77, 4099, 100_003, 1_000_003])
-@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("seed", list(range(1, 9)))
 def test_random_cnfs_every_entry_point(m, ctx, tune, n, seed):
     rng = np.random.Generator(np.random.PCG64(1000 * seed + n % 997))
     cols, dele = random_table(rng, n)
