@@ -1018,9 +1018,19 @@ def config_c2(H, args):
     H.agree(verify(warmup, warmup + steps, "C2 timed steps"))
     kms, kmax = H.kernel_ms(lambda i: query(0), max(1, args.kernel_graph))
     byts = n * 4 + n // 8 + want * 8
+    # C2's 40 MB column stays in the 256 MB Infinity Cache across back-to-back
+    # queries, so 8 TB/s is a generous denominator: beside it, the
+    # predicate-free read of that column with the scan's own tiles and loads
+    # (k_read_probe, one launch, timed like the query)
+    pms, _ = H.kernel_ms(lambda i: ctx.probe_read(t, [0]), max(1, args.kernel_graph))
+    probe_gbs = 4 * (n // 256 * 256) / (pms * 1e-3) / 1e9
     rec = config_record("C2: 10M-row 4xint32, c0 < 104858 -> BitSet + positions + COUNT (one launch)",
                         n, n, 1, want, ms, "mbx::k_scan_select", kms, kmax, byts, "none", "ok",
-                        timing_label(G, steps))
+                        timing_label(G, steps),
+                        resident_read_probe={"kernel_ms": pms, "gbs": probe_gbs,
+                                             "what": "k_read_probe over c0 (40 MB, cache-resident across launches), "
+                                                     "no predicate, no outputs: the launch + read floor"},
+                        kernel_over_read_probe=kms / pms)
     del cols, t, plan, bm, ids, sel, wpos
     torch.cuda.empty_cache()
     return rec
