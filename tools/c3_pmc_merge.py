@@ -18,10 +18,13 @@ def main():
     mbx = mbx_pkg.load().mbx
     path = os.path.join(ROOT, "profiles", "c3_scan_pmc.json")
     d = json.load(open(path))
-    for n in (1, 2, 4, 8):
+    # (file tag, gpus, COUNT form): N = 1's finalize; weak N > 1's 100 M-row frame
+    # shard (tools/gpu_r6_e.sh's n1frame pass); strong N = 2, 4, 8's frame shards
+    for tag, n, mode in (("n1", 1, "finalize"), ("n1frame", 1, "frame"), ("n2", 2, "frame"), ("n4", 4, "frame"),
+                         ("n8", 8, "frame")):
         s, e = mbx.shard_bounds(100_000_000, n, 0)
-        rows, mode = e - s, ("finalize" if n == 1 else "frame")
-        k = [json.loads(x) for x in open(os.path.join(src, f"n{n}_kernels.jsonl")) if "k_scan_fast" in x]
+        rows = e - s
+        k = [json.loads(x) for x in open(os.path.join(src, f"{tag}_kernels.jsonl")) if "k_scan_fast" in x]
         assert len(k) == 1, (n, [x["kernel"] for x in k])
         k = k[0]
         assert k.get("read_basis") == "request split", k
