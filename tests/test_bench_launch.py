@@ -378,3 +378,26 @@ def test_a_fallback_is_taken_once():
     assert argv2[-2:] == ["--graph-steps", "0"] and env2["MBX_BENCH_FALLBACK"] == "rank 2: C4 first graph replay: x"
     assert b.next_attempt([(0, 7, ""), (1, b.KILLED, "")], argv, {}, None) is None
     assert b.final_status([(0, 0, ""), (1, 0, "")]) == 0
+
+
+def test_every_shard_size_has_request_split_traffic():
+    """roofline.traffic at every N the driver runs (C3 shard of rank 0, its
+    COUNT form) and every config record's traffic come from rocprofv3 passes
+    with gfx950's read-request size split (profiles/r06/e, profiles/r06/final)"""
+    b = _bench_module()
+    sys.path.insert(0, ROOT)
+    import mbx_pkg
+    m = mbx_pkg.load().mbx
+    with open(os.path.join(ROOT, "profiles", "c3_scan_pmc.json")) as f:
+        shards = json.load(f)["shards"]
+    for n in (1, 2, 4, 8):
+        s, e = m.shard_bounds(100_000_000, n, 0)
+        mode = "finalize" if n == 1 else "frame"
+        key = f"{e - s}:{mode}"
+        assert b.load_traffic(e - s, mode) and "request-size split" in shards[key]["correction"], key
+        assert abs(shards[key]["traffic_over_algorithmic"] - 1) < 0.002, key
+    assert "request-size split" in shards["100000000:frame"]["correction"]  # weak N > 1
+    with open(os.path.join(ROOT, "profiles", "config_pmc.json")) as f:
+        cfg = json.load(f)["configs"]
+    for key in ("C2:10000000", "C4:100000000", "C5:125000000"):
+        assert cfg[key]["read_basis"] == "request split", key
