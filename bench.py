@@ -157,7 +157,7 @@ def load_traffic(rows, count_mode):
     """HBM bytes per launch of the C3 scan over a `rows`-row shard with the
     given COUNT form ("finalize" | "frame"), from the committed rocprofv3 PMC
     summary (profiles/c3_scan_pmc.json: one entry per shard size bench.py
-    runs at N = 1, 2, 4, 8; written by tools/pmc_summary.py), or None."""
+    runs at N = 1, 2, 4, 8; written by tools/c3_pmc_merge.py from tools/gpu_r6_e.sh), or None."""
     path = os.path.join(ROOT, "profiles", "c3_scan_pmc.json")
     try:
         with open(path) as f:
